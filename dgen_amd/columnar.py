@@ -1,0 +1,169 @@
+"""Agent rows -> structure-of-arrays columns for the device.
+
+Replaces the per-row work the reference does inside
+``calc_system_size_and_performance`` before any arithmetic
+(financial_functions.py:330-421): profile lookup (elec.py:508-558), tariff
+normalisation (ff:374-382, re-done per evaluation in the reference), the rate
+switch table filter (elec.py:840-847) and the finance-column reads.
+"""
+from __future__ import annotations
+
+import hashlib
+from typing import Any, Dict, Hashable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .engine import SWITCH_DTYPE
+from .tariff import TariffTable, series_8760
+
+
+def _is_ca(state) -> bool:
+    return str(state if state is not None else "").upper() == "CA"
+
+
+class SwitchIndex:
+    """rate_switch_lkup rows grouped by (tech, eia_id, res_com), expanded per
+    agent into device candidate lists.  Every row gets its own tariff-table
+    entry so that the final tariff index identifies the row (tariff_id)."""
+
+    def __init__(self, table, tariffs: TariffTable):
+        self.tariffs = tariffs
+        self.groups: Dict[Tuple[Any, Any, Any], List[dict]] = {}
+        self.rows: List[np.ndarray] = []
+        self.row_of_tariff: Dict[int, dict] = {}
+        self._cache: Dict[Tuple, Tuple[int, int]] = {}
+        self._n = 0
+        if table is not None and len(table):
+            recs = table.to_dict(orient="records")
+            for k, r in enumerate(recs):
+                r = dict(r)
+                r["_row"] = k
+                key = (r.get("tech"), r.get("eia_id"), r.get("res_com"))
+                self.groups.setdefault(key, []).append(r)
+
+    def _lookup(self, tech, eia_id, res_com) -> List[dict]:
+        try:
+            return self.groups.get((tech, eia_id, res_com), [])
+        except TypeError:      # unhashable eia_id
+            return []
+
+    def candidates(self, tech: str, eia_id, sector_abbr, is_ca: bool) -> Tuple[int, int]:
+        res_com = str(sector_abbr).upper()[0]
+        ckey = (tech, eia_id if isinstance(eia_id, Hashable) else repr(eia_id), res_com, is_ca)
+        hit = self._cache.get(ckey)
+        if hit is not None:
+            return hit
+        rows = self._lookup(tech, eia_id, res_com)
+        off = self._n
+        for r in rows:
+            tix = self.tariffs.add(r["json"], is_ca, key=f"switch-row:{r['_row']}")
+            rec = np.zeros((), dtype=SWITCH_DTYPE)
+            rec["min_kw"] = float(r["min_kw_limit"])
+            rec["max_kw"] = float(r["max_kw_limit"])
+            rec["one_time_charge"] = float(r["one_time_charge"])
+            rec["tariff"] = tix
+            self.rows.append(rec)
+            self.row_of_tariff[tix] = r
+            self._n += 1
+        res = (off, len(rows))
+        self._cache[ckey] = res
+        return res
+
+    def array(self) -> np.ndarray:
+        if not self.rows:
+            return np.zeros(0, dtype=SWITCH_DTYPE)
+        return np.stack(self.rows).astype(SWITCH_DTYPE)
+
+
+class WholesaleIndex:
+    """Deduplicates the per-agent 8760 wholesale_prices arrays (per county)."""
+
+    def __init__(self):
+        self.rows: List[np.ndarray] = []
+        self._index: Dict[bytes, int] = {}
+
+    def add(self, arr, mult: float) -> int:
+        if arr is None:
+            return -1
+        try:
+            a = np.asarray(arr, dtype=np.float64).ravel()
+        except Exception:
+            return -1
+        # ff:182 np.asarray(...).ravel() * mult, then _list1d_8760 (f32, finite, 8760)
+        if series_8760(a * mult) is None:
+            return -1
+        key = hashlib.blake2b(a.tobytes(), digest_size=16).digest()
+        k = self._index.get(key)
+        if k is None:
+            k = len(self.rows)
+            self._index[key] = k
+            self.rows.append(a)
+        return k
+
+    def array(self) -> Optional[np.ndarray]:
+        return np.stack(self.rows) if self.rows else None
+
+
+def empty_columns(n: int) -> Dict[str, np.ndarray]:
+    return {name: np.zeros(n, dtype=dt) for name, dt in _lib.AGENT_COLUMNS}
+
+
+class PopulationBuilder:
+    """Accumulates agents into SoA columns + the tables they index."""
+
+    def __init__(self, switch_table=None):
+        self.tariffs = TariffTable()
+        self.switches = SwitchIndex(switch_table, self.tariffs)
+        self.wholesale = WholesaleIndex()
+        self.rows: List[Dict[str, Any]] = []
+
+    def add(self, *, load_row: int, cf_row: int, sector_abbr, state_abbr, eia_id, tariff_dict,
+            wholesale, load_kwh, price_mult, econ_life, loan_term, inflation, pv_deg, escalator,
+            down_payment, tax_rate, real_discount, itc_frac, capex, capex_combined, batt_capex_kwh,
+            ccm, vor) -> int:
+        is_ca = _is_ca(state_abbr)
+        is_res = sector_abbr == "res"
+        t0 = self.tariffs.add(tariff_dict, is_ca)
+        so, sc = self.switches.candidates("solar", eia_id, sector_abbr, is_ca)
+        to, tc = self.switches.candidates("storage", eia_id, sector_abbr, is_ca)
+        wrow = -1 if is_ca else self.wholesale.add(wholesale, float(price_mult))
+        self.rows.append(dict(
+            load_row=int(load_row), cf_row=int(cf_row), wholesale_row=wrow, tariff0=t0,
+            sw_solar_off=so, sw_solar_cnt=sc, sw_storage_off=to, sw_storage_cnt=tc,
+            scratch_slot=-1, flags=(1 if is_res else 0) | (2 if is_ca else 0),
+            econ_life=int(econ_life), loan_term=int(loan_term), load_kwh=float(load_kwh),
+            price_mult=float(price_mult), inflation=float(inflation), pv_deg=float(pv_deg),
+            escalator=float(escalator), down_payment=float(down_payment), tax_rate=float(tax_rate),
+            real_discount=float(real_discount), itc_frac=float(itc_frac), capex=float(capex),
+            capex_combined=float(capex_combined), batt_capex_kwh=float(batt_capex_kwh),
+            ccm=float(ccm), vor=float(vor)))
+        return len(self.rows) - 1
+
+    def columns(self) -> Dict[str, np.ndarray]:
+        n = len(self.rows)
+        cols = empty_columns(n)
+        for i, r in enumerate(self.rows):
+            for k, v in r.items():
+                cols[k][i] = v
+        assign_scratch(cols, self.tariffs.array(), self.switches.array())
+        return cols
+
+
+def assign_scratch(cols: Dict[str, np.ndarray], tariffs: np.ndarray, switches: np.ndarray) -> int:
+    """Give an hourly scratch slot to every agent whose battery-case tariff can
+    be net billing (mo 2): its initial tariff or any rate-switch candidate."""
+    n = len(cols["load_kwh"])
+    mo2 = tariffs["mo"] == 2 if tariffs.size else np.zeros(0, bool)
+    need = mo2[cols["tariff0"]] if n else np.zeros(0, bool)
+    if switches.size:
+        sw_mo2 = mo2[switches["tariff"]]
+        csum = np.concatenate([[0], np.cumsum(sw_mo2.astype(np.int64))])
+        for k in ("solar", "storage"):
+            off = cols[f"sw_{k}_off"].astype(np.int64)
+            cnt = cols[f"sw_{k}_cnt"].astype(np.int64)
+            need |= (csum[off + cnt] - csum[off]) > 0
+    slots = np.full(n, -1, dtype=np.int32)
+    slots[need] = np.arange(int(need.sum()), dtype=np.int32)
+    cols["scratch_slot"] = slots
+    return int(need.sum())

@@ -1,0 +1,42 @@
+"""Engine configuration.
+
+The reference never sets these PySAM inputs; they come from the
+CustomGenerationBattery{Residential,Commercial} config defaults that
+``_init_pv_batt_stack`` loads (financial_functions.py:49-89) and that are not
+available offline.  The values below are this project's documented choices
+(DESIGN.md "SSC subset"); every one is overridable.  They must match
+oracle/oracle.py DEFAULT_CFG for the parity tests.
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass
+
+from . import _lib
+
+
+@dataclass
+class EngineConfig:
+    skip_demand_charges: int = 1        # financial_functions.py:35
+    force_net_billing: int = 0          # financial_functions.py:38
+    nm_yearend_sell_rate: float = 0.02  # $/kWh   Utilityrate5 ur_nm_yearend_sell_rate
+    loan_rate_pct: float = 7.5          # %       Cashloan loan_rate (ff no longer sets it)
+    insurance_rate_pct: float = 0.0     # %       Cashloan insurance_rate
+    itc_fed_max: float = 1e38           # $       Cashloan itc_fed_percent_maxvalue
+    depr_sl_years: int = 7              # years   straight-line depreciation (type 2)
+    batt_v_nom: float = 3.6             # V       Li-ion cell nominal voltage
+    batt_q_full: float = 3.2            # Ah      cell capacity
+    batt_min_soc: float = 0.10          # ff:138 intends 10 %
+    batt_max_soc: float = 0.95
+    batt_init_soc: float = 0.30         # ff:151
+    batt_eta_in: float = 0.9408         # AC->DC 0.96 x cell 0.98
+    batt_eta_out: float = 0.9408        # cell 0.98 x DC->AC 0.96
+
+    def to_c(self) -> _lib.Cfg:
+        d = asdict(self)
+        return _lib.Cfg(pad0=0, **d)
+
+    def oracle_kwargs(self) -> dict:
+        d = asdict(self)
+        d.pop("skip_demand_charges")
+        d.pop("force_net_billing")
+        return d

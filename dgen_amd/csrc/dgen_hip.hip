@@ -1,0 +1,1233 @@
+// dgen_hip.hip -- gfx950 kernels + C-ABI for dGen's per-agent sizing & economics
+// hot path (financial_functions.calc_system_size_and_performance and the PySAM
+// Utilityrate5 / Cashloan / Battery work it drives).  See include/dgen_hip.h
+// for the interface and DESIGN.md for the data layout and rooflines.
+//
+// Build (dgen_amd/build.py):
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
+// -ffp-contract=off keeps a*b+c as two roundings, like numpy / scipy / the
+// oracle; the Brent search and the bracket are then bit-identical to scipy.
+//
+// Kernel map (one launch each per batch, all stream-ordered):
+//   k_row_pairwise   once per table: numpy-order row sums (np.sum, elec.py:574;
+//                    naep, ff:351)                          thread per row
+//   k_row_slots      once per table: 576 (month, daytype, hour) slot sums
+//                                                            thread per (row, slot)
+//   k_size           Brent over PV kW (ff:440-447); each evaluation = sticky
+//                    rate switch + 25-year bills + cash flow + NPV (ff:96-288),
+//                    last-evaluation capture (ff:449-474)    thread per agent
+//   k_hourly_batt    one sequential 8760 h scan per agent: baseline / PV-only
+//                    hourly nets, battery sizing + storage rate switch +
+//                    peak-shaving dispatch with SOC in registers (ff:130-164),
+//                    per-(month, period) bins for the battery-case bill
+//                                                            thread per agent
+//   k_batt_finance   battery-case Utilityrate5 + Cashloan (ff:178-288)
+//                                                            thread per agent
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "../../include/dgen_hip.h"
+
+namespace {
+
+constexpr int NH = DGEN_NH;
+constexpr int NSLOT = DGEN_NSLOT;
+constexpr int MAXP = DGEN_MAXP;
+constexpr int MAXT = DGEN_MAXT;
+constexpr int MAXY = DGEN_MAXY;
+constexpr int NBIN = 12 * MAXP;
+constexpr int BLOCK = 128;   // threads per block for the per-agent kernels
+
+__constant__ int c_month_start_day[13] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334, 365};
+__constant__ int c_days_in_month[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+
+thread_local char g_err[512] = {0};
+
+void set_err(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+#define HIP_TRY(expr)                                                              \
+    do {                                                                           \
+        hipError_t _e = (expr);                                                    \
+        if (_e != hipSuccess) {                                                    \
+            set_err("%s failed: %s", #expr, hipGetErrorString(_e));                \
+            return DGEN_E_HIP;                                                     \
+        }                                                                          \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// numpy pairwise summation (loops_utils.h.src), chunked by the 8192-element
+// reduction buffer; identical association order => bit-identical to np.sum.
+// ---------------------------------------------------------------------------
+template <class F>
+__device__ double pw_leaf(const F& f, int off, int n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; i++) res += f(off + i);
+        return res;
+    }
+    double r0 = f(off + 0), r1 = f(off + 1), r2 = f(off + 2), r3 = f(off + 3);
+    double r4 = f(off + 4), r5 = f(off + 5), r6 = f(off + 6), r7 = f(off + 7);
+    int i = 8;
+    for (; i < n - (n % 8); i += 8) {
+        r0 += f(off + i + 0); r1 += f(off + i + 1); r2 += f(off + i + 2); r3 += f(off + i + 3);
+        r4 += f(off + i + 4); r5 += f(off + i + 5); r6 += f(off + i + 6); r7 += f(off + i + 7);
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; i++) res += f(off + i);
+    return res;
+}
+
+// Post-order walk of the pairwise split tree with an explicit stack.
+template <class F>
+__device__ double pw_sum(const F& f, int off, int n) {
+    int so[16], sn[16], st[16];
+    double sl[16];
+    int sp = 0;
+    so[0] = off; sn[0] = n; st[0] = 0; sp = 1;
+    double ret = 0.0;
+    bool have_ret = false;
+    while (sp > 0) {
+        int k = sp - 1;
+        if (have_ret) {
+            have_ret = false;
+            if (st[k] == 1) {            // left child done -> run right child
+                sl[k] = ret;
+                st[k] = 2;
+                int n2 = sn[k] / 2; n2 -= n2 % 8;
+                so[sp] = so[k] + n2; sn[sp] = sn[k] - n2; st[sp] = 0; sp++;
+            } else {                     // right child done -> combine
+                ret = sl[k] + ret;
+                sp--;
+                have_ret = true;
+            }
+            continue;
+        }
+        if (sn[k] <= 128) {
+            ret = pw_leaf(f, so[k], sn[k]);
+            sp--;
+            have_ret = true;
+        } else {
+            int n2 = sn[k] / 2; n2 -= n2 % 8;
+            st[k] = 1;
+            so[sp] = so[k]; sn[sp] = n2; st[sp] = 0; sp++;
+        }
+    }
+    return ret;
+}
+
+template <class F>
+__device__ double np_sum(const F& f, int n) {
+    double res = 0.0;
+    for (int s = 0; s < n; s += 8192) {
+        int m = n - s < 8192 ? n - s : 8192;
+        res += pw_sum(f, s, m);
+    }
+    return res;
+}
+
+struct ShapeVal {
+    const float* p;
+    __device__ double operator()(int i) const { return (double)p[i]; }
+};
+struct CfVal {
+    const int32_t* p;
+    __device__ double operator()(int i) const { return (double)p[i] / 1e6; }
+};
+
+__global__ void k_row_pairwise_shape(const float* __restrict__ rows, int64_t n_rows,
+                                     double* __restrict__ out) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    ShapeVal f{rows + r * NH};
+    out[r] = np_sum(f, NH);
+}
+
+__global__ void k_row_pairwise_cf(const int32_t* __restrict__ rows, int64_t n_rows,
+                                  double* __restrict__ out) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rows) return;
+    CfVal f{rows + r * NH};
+    out[r] = np_sum(f, NH);
+}
+
+// slot = month * 48 + daytype * 24 + hour_of_day; day type from SSC's calendar
+// (hour i is weekend iff (i % 168) >= 120: the year starts on a Monday).
+template <class F>
+__device__ double slot_sum(const F& f, int slot) {
+    int m = slot / 48, dt = (slot / 24) % 2, hod = slot % 24;
+    double acc = 0.0;
+    for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
+        int weekend = (d % 7) >= 5;
+        if (weekend == dt) acc += f(d * 24 + hod);
+    }
+    return acc;
+}
+
+__global__ void k_row_slots_shape(const float* __restrict__ rows, int64_t n_rows,
+                                  double* __restrict__ out) {
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_rows * NSLOT) return;
+    int64_t r = g / NSLOT;
+    int s = (int)(g % NSLOT);
+    ShapeVal f{rows + r * NH};
+    out[g] = slot_sum(f, s);
+}
+
+__global__ void k_row_slots_cf(const int32_t* __restrict__ rows, int64_t n_rows,
+                               double* __restrict__ out) {
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_rows * NSLOT) return;
+    int64_t r = g / NSLOT;
+    int s = (int)(g % NSLOT);
+    CfVal f{rows + r * NH};
+    out[g] = slot_sum(f, s);
+}
+
+// ---------------------------------------------------------------------------
+// Utilityrate5 subset (semantics: DESIGN.md "SSC subset"; oracle/orc.c)
+// ---------------------------------------------------------------------------
+
+// Energy charge of one month from per-period billed kWh u[0..P): tier amounts
+// from the monthly total, each period billed its share at its own price.
+__device__ __forceinline__ double month_energy_charge(const dgen_tariff& t, int m,
+                                                      const double (&u)[MAXP]) {
+    const int P = t.P, T = t.T;
+    double U = 0.0;
+#pragma unroll
+    for (int p = 0; p < MAXP; p++)
+        if (p < P) U += u[p];
+    if (!(U > 0.0)) return 0.0;
+    double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
+    double charge = 0.0, prev = 0.0;
+    for (int k = 0; k < T; k++) {
+        double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
+        double top = U < hi ? U : hi;
+        double amt = top - prev;
+        if (amt < 0.0) amt = 0.0;
+        if (hi > prev) prev = hi;
+#pragma unroll
+        for (int p = 0; p < MAXP; p++)
+            if (p < P) charge += (u[p] / U) * amt * t.buy[p][k];
+    }
+    return charge;
+}
+
+// NEM (mo 0) bill for one year from monthly per-period net kWh:
+//   net[m][p] = L[m][p] - gscale * G[m][p], bins plane-major [bin * n + agent].
+// Per-period kWh credits roll over month to month; December true-up at the
+// year-end sell rate.  Returns the bill before the escalation factor.
+__device__ double year_bill_mo0(const dgen_tariff& t, const double* __restrict__ L,
+                                const double* __restrict__ G, int64_t stride, double gscale,
+                                double yearend_rate) {
+    const int P = t.P;
+    double credit[MAXP];
+#pragma unroll
+    for (int p = 0; p < MAXP; p++) credit[p] = 0.0;
+    double total = 0.0;
+    for (int m = 0; m < 12; m++) {
+        double u[MAXP];
+#pragma unroll
+        for (int p = 0; p < MAXP; p++) {
+            u[p] = 0.0;
+            if (p < P) {
+                int64_t b = (int64_t)(m * MAXP + p) * stride;
+                double g = G ? G[b] : 0.0;
+                double n = L[b] - gscale * g;
+                if (n >= 0.0) {
+                    double use = n < credit[p] ? n : credit[p];
+                    u[p] = n - use;
+                    credit[p] -= use;
+                } else {
+                    credit[p] += -n;
+                }
+            }
+        }
+        double bill = t.fixed + month_energy_charge(t, m, u);
+        if (m == 11) {
+            double c = 0.0;
+#pragma unroll
+            for (int p = 0; p < MAXP; p++)
+                if (p < P) c += credit[p];
+            bill -= c * yearend_rate;
+        }
+        total += bill;
+    }
+    return total;
+}
+
+// Per-thread LDS accumulators for the hourly (mo 2) bill: [k][BLOCK] layout,
+// conflict-free (each lane owns a column).
+struct LdsAcc {
+    double* base;
+    __device__ double& at(int k) const { return base[k * BLOCK]; }
+};
+
+// Hourly source for the net-billing year pass.
+struct HourSrc {
+    const float* shape;     // load row
+    const int32_t* cf;      // cf row (PV-only) or nullptr
+    const double* sysgen;   // battery scratch [h * stride] or nullptr
+    int64_t sys_stride;
+    double load_scale;      // load_kwh / row_sum
+    double gen_scale;       // kW scale for cf (PV-only)
+    const double* ts;       // wholesale row or nullptr
+    double ts_mult;
+};
+
+// Net-billing (mo 2) bill for one year: hourly imports billed through the
+// tier/period charge, hourly exports credited at the tier-1 sell rate of the
+// hour's period or at the float32-rounded TS sell rate (ff:751-761).
+__device__ double year_bill_mo2(const dgen_tariff& t, const HourSrc& src, double s,
+                                bool with_gen, const LdsAcc& acc) {
+    const int P = t.P;
+    double total = 0.0;
+    int h = 0;
+    for (int m = 0; m < 12; m++) {
+        for (int p = 0; p < MAXP; p++) { acc.at(p) = 0.0; acc.at(MAXP + p) = 0.0; }
+        for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
+            const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
+            for (int hod = 0; hod < 24; hod++, h++) {
+                double load = (double)src.shape[h] * src.load_scale;
+                double g = 0.0;
+                if (with_gen) {
+                    if (src.sysgen) g = src.sysgen[(int64_t)h * src.sys_stride];
+                    else g = ((double)src.cf[h] / 1e6) * src.gen_scale;
+                }
+                double dd = load - g * s;
+                int p = sched[hod];
+                if (dd > 0.0) {
+                    acc.at(p) += dd;
+                } else {
+                    double e = -dd;
+                    if (src.ts) e *= (double)(float)(src.ts[h] * src.ts_mult);
+                    acc.at(MAXP + p) += e;
+                }
+            }
+        }
+        double u[MAXP];
+        double cr = 0.0;
+#pragma unroll
+        for (int p = 0; p < MAXP; p++) {
+            u[p] = 0.0;
+            if (p < P) {
+                u[p] = acc.at(p);
+                double e = acc.at(MAXP + p);
+                cr += src.ts ? e : e * t.sell[p][0];
+            }
+        }
+        total += t.fixed + month_energy_charge(t, m, u) - cr;
+    }
+    return total;
+}
+
+// ---------------------------------------------------------------------------
+// Cashloan subset: one year's step of the after-tax cash flow
+// ---------------------------------------------------------------------------
+struct LoanParams {
+    int N, term, market;
+    double infl, rr, fed, sta, r_loan, loan_f;  // loan_f = (1+r)^term
+    double itc_pct, itc_max, ins_rate, debt_frac;
+    int sl_years, depr_type;
+};
+
+struct LoanState {
+    double C, debt, pmt, itc, basis, ins0, balance, ins_esc, df, npv_acc, cum, payback;
+    bool paid;
+};
+
+__device__ __forceinline__ double depr_frac(int type, int year, int sl) {
+    if (type == 1) {
+        const double m5[6] = {0.20, 0.32, 0.192, 0.1152, 0.1152, 0.0576};
+        return (year >= 1 && year <= 6) ? m5[year - 1] : 0.0;
+    }
+    if (type == 2) return (year >= 1 && year <= sl) ? 1.0 / (double)sl : 0.0;
+    return 0.0;
+}
+
+__device__ __forceinline__ void loan_begin(const LoanParams& lp, double C, LoanState& s) {
+    s.C = C;
+    s.debt = lp.debt_frac * C;
+    s.pmt = 0.0;
+    if (lp.term > 0 && s.debt != 0.0) {
+        if (lp.r_loan != 0.0) s.pmt = s.debt * lp.r_loan / (1.0 - 1.0 / lp.loan_f);
+        else s.pmt = s.debt / (double)lp.term;
+    }
+    double itc = lp.itc_pct * 0.01 * C;
+    s.itc = itc > lp.itc_max ? lp.itc_max : itc;
+    s.basis = C - 0.5 * s.itc;
+    s.ins0 = lp.ins_rate * C;
+    s.balance = s.debt;
+    s.ins_esc = 1.0;
+    s.df = 1.0;
+    s.npv_acc = -(C - s.debt);
+    s.cum = -C;
+    s.payback = 1e99;
+    s.paid = false;
+}
+
+// Returns cf_payback_with_expenses[i]; accumulates NPV (forward discounting)
+// and the payback interpolation of SSC compute_payback.
+__device__ __forceinline__ double loan_year(const LoanParams& lp, int i, double ev, LoanState& s) {
+    double oe = s.ins0 * s.ins_esc;
+    s.ins_esc = s.ins_esc * (1.0 + lp.infl);
+    double interest = 0.0, payment = 0.0;
+    if (i <= lp.term && s.pmt != 0.0) {
+        interest = s.balance * lp.r_loan;
+        payment = s.pmt;
+        s.balance = s.balance - (s.pmt - interest);
+    }
+    double itc_i = (i == 1) ? s.itc : 0.0;
+    double sta_tax = 0.0, fed_tax = 0.0;
+    if (lp.market != 0) {
+        double dep = depr_frac(lp.depr_type, i, lp.sl_years) * s.basis;
+        sta_tax = lp.sta * (ev - oe - interest - dep);
+        fed_tax = lp.fed * (ev - oe - interest - dep - sta_tax);
+    }
+    double taxsav = itc_i - sta_tax - fed_tax;
+    double atcf = ev - oe - payment + taxsav;
+    double pb = ev - oe + taxsav;
+    s.df = s.df * lp.rr;
+    s.npv_acc += atcf * s.df;
+    s.cum += pb;
+    if (!s.paid && s.cum > 0.0) {
+        s.paid = true;
+        s.payback = (pb != 0.0) ? (double)i - s.cum / pb : (double)i - 0.5;
+    }
+    return pb;
+}
+
+__device__ __forceinline__ LoanParams make_loan(const dgen_agents& A, const dgen_cfg& cfg, int64_t i,
+                                                int N, bool is_res) {
+    LoanParams lp;
+    lp.N = N;
+    lp.term = A.loan_term[i];
+    lp.market = is_res ? 0 : 1;
+    double infl_pct = A.inflation[i] * 100.0;
+    lp.infl = infl_pct * 0.01;
+    double real = (A.real_discount[i] * 100.0) * 0.01;
+    double nom = (1.0 + real) * (1.0 + lp.infl) - 1.0;
+    lp.rr = 1.0 / (1.0 + nom);
+    double tax_pct = A.tax_rate[i] * 100.0;
+    lp.fed = (tax_pct * 0.7) * 0.01;
+    lp.sta = (tax_pct * 0.3) * 0.01;
+    lp.r_loan = cfg.loan_rate_pct * 0.01;
+    double f = 1.0;
+    for (int k = 0; k < lp.term; k++) f = f * (1.0 + lp.r_loan);
+    lp.loan_f = f;
+    lp.itc_pct = A.itc_frac[i];          // ff:285 passes the fraction as the percent
+    lp.itc_max = cfg.itc_fed_max;
+    lp.ins_rate = cfg.insurance_rate_pct * 0.01;
+    lp.debt_frac = (100.0 - (A.down_payment[i] * 100.0)) * 0.01;
+    lp.sl_years = cfg.depr_sl_years;
+    lp.depr_type = is_res ? 0 : 2;
+    return lp;
+}
+
+// ---------------------------------------------------------------------------
+// bins for the PV-only search (kW independent; rebuilt on a tariff switch)
+// ---------------------------------------------------------------------------
+__device__ void build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
+                           const double* __restrict__ gslots, double load_scale,
+                           double* __restrict__ L, double* __restrict__ G, int64_t stride) {
+    for (int m = 0; m < 12; m++) {
+        double lb[MAXP], gb[MAXP];
+#pragma unroll
+        for (int p = 0; p < MAXP; p++) { lb[p] = 0.0; gb[p] = 0.0; }
+        for (int dt = 0; dt < 2; dt++) {
+            const uint8_t* sched = dt ? t.wkend[m] : t.wkday[m];
+            for (int hod = 0; hod < 24; hod++) {
+                int s = m * 48 + dt * 24 + hod;
+                int p = sched[hod];
+                double lv = lslots[s], gv = gslots[s];
+#pragma unroll
+                for (int q = 0; q < MAXP; q++)
+                    if (q == p) { lb[q] += lv; gb[q] += gv; }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < MAXP; p++) {
+            if (p < t.P) {
+                int64_t b = (int64_t)(m * MAXP + p) * stride;
+                L[b] = lb[p] * load_scale;
+                G[b] = gb[p];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_size: PV-only bounded-Brent search, one thread per agent
+// ---------------------------------------------------------------------------
+struct SizeCtx {
+    const dgen_tables* T;
+    const dgen_agents* A;
+    const dgen_cfg* cfg;
+    int64_t i, n;
+    int N;
+    bool is_res, is_ca;
+    int tariff;
+    int switched;
+    int status;
+    double load_scale, kwh;
+    double rate_base, sys_base;
+    LoanParams lp;
+    double* L;            // workspace bins [bin * n + i]
+    double* G;
+    double wo1;           // year-1 no-system bill for the current tariff
+    HourSrc src;          // for mo 2
+    LdsAcc acc;
+    const double* lslots;
+    const double* gslots;
+};
+
+__device__ void set_tariff(SizeCtx& c, int tix) {
+    const dgen_tariff& t = c.T->tariffs[tix];
+    c.tariff = tix;
+    c.status |= t.flags;
+    if (t.mo == 0) {
+        build_bins(t, c.lslots, c.gslots, c.load_scale, c.L, c.G, c.n);
+        c.wo1 = year_bill_mo0(t, c.L, nullptr, c.n, 0.0, c.cfg->nm_yearend_sell_rate);
+    } else {
+        c.wo1 = year_bill_mo2(t, c.src, 1.0, false, c.acc);
+    }
+}
+
+// apply_rate_switch (elec.py:838-863): exactly one row with min <= size < max.
+__device__ double rate_switch(SizeCtx& c, const dgen_switch* rows, int cnt, double size,
+                              int* new_tariff) {
+    int hit = -1, k = 0;
+    for (int r = 0; r < cnt; r++)
+        if (rows[r].min_kw <= size && rows[r].max_kw > size) { k++; hit = r; }
+    *new_tariff = -1;
+    if (size > 0.0 && k == 1) {
+        *new_tariff = rows[hit].tariff;
+        return rows[hit].one_time_charge;
+    }
+    return 0.0;
+}
+
+// One evaluation of calc_system_performance(kw, en_batt=False); returns -NPV.
+// With `out` set, writes the 26-long arrays and scalars of this evaluation.
+__device__ double objective(SizeCtx& c, double kw, const dgen_outputs* out) {
+    double otc = 0.0;
+    if (kw > 0.0) {
+        int nt;
+        otc = rate_switch(c, c.T->switches + c.A->sw_solar_off[c.i], c.A->sw_solar_cnt[c.i], kw, &nt);
+        if (nt >= 0) {
+            c.switched = 1;
+            if (nt != c.tariff) set_tariff(c, nt);
+        }
+    }
+    const dgen_tariff& t = c.T->tariffs[c.tariff];
+    double kws = ((kw * 1000.0) * 0.96) / 1000.0;       // ff:118-120 per-kW scale
+    double total = ((c.A->capex[c.i] * kw + 0.0) * c.A->ccm[c.i]) + 0.0 + otc;   // ff:263,280-282
+    LoanState ls;
+    loan_begin(c.lp, total, ls);
+    double r = 1.0, s = 1.0, w1 = 0.0;
+    const int64_t n = c.n;
+    if (out) {
+        out->cash_flow[c.i] = -total;
+        out->cfev_pv[c.i] = 0.0;
+        out->bill_w_pv[c.i] = 0.0;
+        out->bill_wo_pv[c.i] = 0.0;
+    }
+    if (t.mo == 2) {
+        c.src.ts = (!c.is_ca && c.src.ts_mult == c.src.ts_mult) ? c.src.ts : nullptr;
+        c.src.gen_scale = kws;
+    }
+    for (int y = 1; y <= c.N; y++) {
+        double wb;
+        if (t.mo == 0) wb = year_bill_mo0(t, c.L, c.G, n, s * kws, c.cfg->nm_yearend_sell_rate);
+        else wb = year_bill_mo2(t, c.src, s, true, c.acc);
+        double w = wb * r;
+        double wo = c.wo1 * r;
+        double ev = wo - w;
+        if (y == 1) w1 = w;
+        double pb = loan_year(c.lp, y, ev, ls);
+        if (out) {
+            out->cash_flow[(int64_t)y * n + c.i] = pb;
+            out->cfev_pv[(int64_t)y * n + c.i] = ev;
+            out->bill_w_pv[(int64_t)y * n + c.i] = w;
+            out->bill_wo_pv[(int64_t)y * n + c.i] = wo;
+        }
+        r = r * c.rate_base;
+        s = s * c.sys_base;
+    }
+    double npv = ls.npv_acc;
+    if (out) {
+        out->npv[c.i] = npv;
+        out->payback_raw[c.i] = ls.payback;
+        double pb = isfinite(ls.payback) ? ls.payback : 30.1;
+        out->payback_period[c.i] = rint(pb * 10.0) / 10.0;
+        out->first_with[c.i] = w1;
+        out->first_without[c.i] = c.wo1;
+        out->price_per_kwh[c.i] = c.wo1 / c.kwh;
+    }
+    return -npv;
+}
+
+__device__ __forceinline__ double np_sign(double v) {
+    return (v > 0.0) ? 1.0 : ((v < 0.0) ? -1.0 : 0.0);
+}
+
+// scipy 1.15.3 _minimize_scalar_bounded, op for op (maxfun 500).
+template <class Obj>
+__device__ double brent_bounded(Obj&& f, double x1, double x2, double xatol, int* nfev,
+                                double* x_last) {
+    const double sqrt_eps = 1.4832396974191326e-08;     // sqrt(2.2e-16)
+    const double golden_mean = 0.3819660112501051;      // 0.5 * (3 - sqrt(5))
+    double a = x1, b = x2;
+    double fulc = a + golden_mean * (b - a);
+    double nfc = fulc, xf = fulc;
+    double rat = 0.0, e = 0.0;
+    double x = xf;
+    double fx = f(x);
+    *x_last = x;
+    int num = 1;
+    double ffulc = fx, fnfc = fx;
+    double xm = 0.5 * (a + b);
+    double tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+    double tol2 = 2.0 * tol1;
+    while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {
+        bool golden = true;
+        if (fabs(e) > tol1) {
+            golden = false;
+            double r = (xf - nfc) * (fx - ffulc);
+            double q = (xf - fulc) * (fx - fnfc);
+            double p = (xf - fulc) * q - (xf - nfc) * r;
+            q = 2.0 * (q - r);
+            if (q > 0.0) p = -p;
+            q = fabs(q);
+            r = e;
+            e = rat;
+            if ((fabs(p) < fabs(0.5 * q * r)) && (p > q * (a - xf)) && (p < q * (b - xf))) {
+                rat = (p + 0.0) / q;
+                x = xf + rat;
+                if (((x - a) < tol2) || ((b - x) < tol2)) {
+                    double si = np_sign(xm - xf) + (((xm - xf) == 0.0) ? 1.0 : 0.0);
+                    rat = tol1 * si;
+                }
+            } else {
+                golden = true;
+            }
+        }
+        if (golden) {
+            if (xf >= xm) e = a - xf; else e = b - xf;
+            rat = golden_mean * e;
+        }
+        double si = np_sign(rat) + ((rat == 0.0) ? 1.0 : 0.0);
+        double ar = fabs(rat);
+        x = xf + si * (ar > tol1 ? ar : tol1);
+        double fu = f(x);
+        *x_last = x;
+        num += 1;
+        if (fu <= fx) {
+            if (x >= xf) a = xf; else b = xf;
+            fulc = nfc; ffulc = fnfc;
+            nfc = xf; fnfc = fx;
+            xf = x; fx = fu;
+        } else {
+            if (x < xf) a = x; else b = x;
+            if ((fu <= fnfc) || (nfc == xf)) {
+                fulc = nfc; ffulc = fnfc;
+                nfc = x; fnfc = fu;
+            } else if ((fu <= ffulc) || (fulc == xf) || (fulc == nfc)) {
+                fulc = x; ffulc = fu;
+            }
+        }
+        xm = 0.5 * (a + b);
+        tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+        tol2 = 2.0 * tol1;
+        if (num >= 500) break;
+    }
+    *nfev = num;
+    return xf;
+}
+
+struct WsLayout {
+    // doubles, plane-major [k][n]
+    double* L;        // NBIN planes
+    double* G;        // NBIN planes
+    double* Lb;       // NBIN planes (battery case, final tariff)
+    double* Gb;       // NBIN planes
+    double* otc_b;    // 1 plane: storage one-time charge
+    double* scratch;  // [8760][n_scratch] battery system output (mo 2)
+};
+
+__host__ __device__ inline WsLayout ws_layout(void* base, int64_t n) {
+    WsLayout w;
+    double* p = (double*)base;
+    w.L = p; p += (int64_t)NBIN * n;
+    w.G = p; p += (int64_t)NBIN * n;
+    w.Lb = p; p += (int64_t)NBIN * n;
+    w.Gb = p; p += (int64_t)NBIN * n;
+    w.otc_b = p; p += n;
+    w.scratch = p;
+    return w;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_size(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws) {
+    __shared__ double lds[2 * MAXP * BLOCK];
+    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    WsLayout W = ws_layout(ws, n);
+    SizeCtx c;
+    c.T = &T; c.A = &A; c.cfg = &cfg; c.i = i; c.n = n;
+    c.status = 0; c.switched = 0;
+    c.acc.base = lds + threadIdx.x;
+    uint8_t fl = A.flags[i];
+    c.is_res = (fl & 1) != 0;
+    c.is_ca = (fl & 2) != 0;
+    c.N = A.econ_life[i];
+    c.kwh = A.load_kwh[i];
+    int lr = A.load_row[i], cr = A.cf_row[i];
+    int t0 = A.tariff0[i];
+    double S = T.shape_sum[lr];
+    double naep0 = T.cf_naep[cr];
+    c.load_scale = c.kwh / S;
+    c.lslots = T.shape_slots + (int64_t)lr * NSLOT;
+    c.gslots = T.cf_slots + (int64_t)cr * NSLOT;
+    c.L = W.L + i; c.G = W.G + i;
+    // ff:364-368: escalation (1 + infl + esc)^i, degradation (1 - d)^i
+    c.rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
+    c.sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+    c.lp = make_loan(A, cfg, i, c.N, c.is_res);
+    c.src.shape = T.shapes + (int64_t)lr * NH;
+    c.src.cf = T.cfs + (int64_t)cr * NH;
+    c.src.sysgen = nullptr; c.src.sys_stride = 0;
+    c.src.load_scale = c.load_scale;
+    c.src.gen_scale = 0.0;
+    int wr = A.wholesale_row[i];
+    c.src.ts = (wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+    c.src.ts_mult = A.price_mult[i];
+    if (c.is_ca) c.src.ts = nullptr;
+
+    bool bad = false;
+    if (c.N < 1 || c.N > MAXY) { c.status |= DGEN_ST_YEARS; bad = true; }
+    if (t0 < 0 || t0 >= T.n_tariffs) { c.status |= DGEN_ST_TARIFF; bad = true; }
+    // ff:440-444 bracket and xatol
+    double max_load = c.kwh / naep0;
+    double low = max_load * 0.8, high = max_load * 1.25;
+    double span = high - low;
+    double tl = (span > 1.0 ? span : 1.0) * 1e-3;      // max(1, high - low) * 1e-3
+    double fl_tl = floor(tl);
+    double xatol = fl_tl < 2.0 ? 2.0 : fl_tl;           // max(2, int(...))
+    if (!isfinite(low) || !isfinite(high)) { c.status |= DGEN_ST_BOUNDS; bad = true; }
+    if (c.kwh == 0.0) c.status |= DGEN_ST_ZERO_LOAD;
+    if (bad) {
+        O.status[i] = c.status;
+        O.nfev[i] = 0;
+        O.system_kw[i] = NAN; O.x_last[i] = NAN; O.npv[i] = NAN;
+        O.tariff_final[i] = t0; O.switched[i] = 0;
+        return;
+    }
+    set_tariff(c, t0);
+    int nfev = 0;
+    double x_last = 0.0;
+    double kw_star = brent_bounded([&](double x) { return objective(c, x, nullptr); },
+                                   low, high, xatol, &nfev, &x_last);
+    // ff:449-474: outputs of the LAST evaluation.  Re-running it is exact: the
+    // sticky switch is idempotent at the same x and the state is unchanged.
+    objective(c, x_last, &O);
+    O.system_kw[i] = kw_star;
+    O.x_last[i] = x_last;
+    O.nfev[i] = nfev;
+    O.tariff_final[i] = c.tariff;
+    O.switched[i] = c.switched;
+    O.status[i] = c.status;
+}
+
+// ---------------------------------------------------------------------------
+// k_hourly_batt: one sequential scan over the year per agent
+// ---------------------------------------------------------------------------
+// BatteryTools.battery_model_sizing restated (ff:140-147).
+__device__ __forceinline__ void batt_size(double desired_kw, double desired_kwh, double v,
+                                          const dgen_cfg& cfg, double* bank, double* power) {
+    if (!(desired_kwh > 0.0)) { *bank = 0.0; *power = 0.0; return; }
+    double series = ceil(v / cfg.batt_v_nom);
+    double strings = floor(desired_kwh * 1000.0 / (cfg.batt_q_full * cfg.batt_v_nom * series) + 0.5);
+    if (strings < 1.0) strings = 1.0;
+    double b = cfg.batt_q_full * cfg.batt_v_nom * series * strings * 0.001;
+    *bank = b;
+    *power = b * (desired_kw / desired_kwh);
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
+              int64_t n_scratch) {
+    __shared__ double lds[2 * MAXP * BLOCK];
+    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
+    WsLayout W = ws_layout(ws, n);
+    LdsAcc acc{lds + threadIdx.x};
+    const bool is_res = (A.flags[i] & 1) != 0;
+    const int lr = A.load_row[i], cr = A.cf_row[i];
+    const double kwh = A.load_kwh[i];
+    const double load_scale = kwh / T.shape_sum[lr];
+    const double kw_star = O.system_kw[i];
+    const double x_last = O.x_last[i];
+    const double c_last = ((x_last * 1000.0) * 0.96) / 1000.0;
+    const double c_star = ((kw_star * 1000.0) * 0.96) / 1000.0;
+    const float* __restrict__ shp = T.shapes + (int64_t)lr * NH;
+    const int32_t* __restrict__ cfp = T.cfs + (int64_t)cr * NH;
+
+    // battery sizing at kW* (ff:140-147) and the storage rate switch (ff:167-175)
+    double desired_kwh = kw_star / 0.8, desired_kw = desired_kwh / 2.0;
+    double bank, power;
+    batt_size(desired_kw, desired_kwh, is_res ? 240.0 : 500.0, cfg, &bank, &power);
+    int tariff = O.tariff_final[i];
+    int switched = O.switched[i];
+    double otc = 0.0;
+    if (bank > 0.0) {
+        const dgen_switch* rows = T.switches + A.sw_storage_off[i];
+        int cnt = A.sw_storage_cnt[i], hit = -1, k = 0;
+        for (int r = 0; r < cnt; r++)
+            if (rows[r].min_kw <= bank && rows[r].max_kw > bank) { k++; hit = r; }
+        if (k == 1) { tariff = rows[hit].tariff; switched = 1; otc = rows[hit].one_time_charge; }
+    }
+    const dgen_tariff& t = T.tariffs[tariff];
+    const int P = t.P;
+    const bool mo2 = (t.mo == 2);
+    const int slot = A.scratch_slot[i];
+    double* scratch = (mo2 && slot >= 0) ? W.scratch + slot : nullptr;
+    int status = O.status[i] | t.flags;
+    if (mo2 && slot < 0) status |= DGEN_ST_SCRATCH;
+
+    const double eta_in = cfg.batt_eta_in, eta_out = cfg.batt_eta_out;
+    const double min_soc = cfg.batt_min_soc, max_soc = cfg.batt_max_soc;
+    const bool has_batt = bank > 0.0;
+    double soc = cfg.batt_init_soc;
+    double annual = 0.0;
+
+    for (int m = 0; m < 12; m++) {
+#pragma unroll
+        for (int p = 0; p < MAXP; p++) { acc.at(p) = 0.0; acc.at(MAXP + p) = 0.0; }
+        for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
+            const int h0 = d * 24;
+            const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
+            double load[24], pv[24];
+            // 96 B of the shape row and 96 B of the cf row per day: 6 x 16 B loads each
+            const float4* s4 = reinterpret_cast<const float4*>(shp + h0);
+            const int4* c4 = reinterpret_cast<const int4*>(cfp + h0);
+            double need0 = 0.0, dmax = 0.0;
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                float4 sv = s4[q];
+                int4 cv = c4[q];
+                float sa[4] = {sv.x, sv.y, sv.z, sv.w};
+                int ca[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int hh = q * 4 + j;
+                    const int64_t h = h0 + hh;
+                    double ld = (double)sa[j] * load_scale;
+                    double g = (double)ca[j] / 1e6;
+                    double pl = g * c_last;
+                    double ps = g * c_star;
+                    load[hh] = ld;
+                    pv[hh] = ps;
+                    annual += pl;
+                    if (O.baseline) O.baseline[h * n + i] = (float)ld;
+                    if (O.net_pvonly) {
+                        double dn = ld - pl;
+                        O.net_pvonly[h * n + i] = (float)(dn > 0.0 ? dn : 0.0);
+                    }
+                    double dd = ld - ps;
+                    if (dd < 0.0) dd = 0.0;
+                    if (dd > dmax) dmax = dd;
+                    need0 += dd < power ? dd : power;
+                }
+            }
+            // daily peak-shaving target with perfect 24 h look-ahead
+            double target = 0.0;
+            if (has_batt) {
+                double avail = (soc - min_soc) * bank * eta_out;
+                if (avail < 0.0) avail = 0.0;
+                if (need0 > avail) {
+                    double lo = 0.0, hi = dmax;
+                    for (int it = 0; it < 48; it++) {
+                        double mid = 0.5 * (lo + hi);
+                        double need = 0.0;
+#pragma unroll
+                        for (int hh = 0; hh < 24; hh++) {
+                            double dd = load[hh] - pv[hh] - mid;
+                            if (dd < 0.0) dd = 0.0;
+                            need += dd < power ? dd : power;
+                        }
+                        if (need <= avail) hi = mid; else lo = mid;
+                    }
+                    target = hi;
+                }
+            }
+#pragma unroll
+            for (int hh = 0; hh < 24; hh++) {
+                const int64_t h = h0 + hh;
+                double nn = load[hh] - pv[hh];
+                double sys, g2l;
+                if (!has_batt) {
+                    sys = pv[hh];
+                    g2l = nn > 0.0 ? nn : 0.0;
+                } else if (nn < 0.0) {
+                    double room = (max_soc - soc) * bank / eta_in;
+                    if (room < 0.0) room = 0.0;
+                    double cc = -nn;
+                    if (cc > power) cc = power;
+                    if (cc > room) cc = room;
+                    soc = soc + cc * eta_in / bank;
+                    sys = pv[hh] - cc;
+                    g2l = 0.0;
+                } else {
+                    double avail = (soc - min_soc) * bank * eta_out;
+                    if (avail < 0.0) avail = 0.0;
+                    double dd = nn - target;
+                    if (dd < 0.0) dd = 0.0;
+                    if (dd > power) dd = power;
+                    if (dd > avail) dd = avail;
+                    soc = soc - dd / (eta_out * bank);
+                    sys = pv[hh] + dd;
+                    g2l = nn - dd;
+                }
+                if (O.net_with_batt) O.net_with_batt[h * n + i] = (float)g2l;
+                if (mo2) {
+                    if (scratch) scratch[h * n_scratch] = sys;    // plane [h][slot]
+                } else {
+                    int p = sched[hh];
+                    acc.at(p) += load[hh];
+                    acc.at(MAXP + p) += sys;
+                }
+            }
+        }
+        if (!mo2) {
+#pragma unroll
+            for (int p = 0; p < MAXP; p++) {
+                if (p < P) {
+                    int64_t b = (int64_t)(m * MAXP + p) * n + i;
+                    W.Lb[b] = acc.at(p);
+                    W.Gb[b] = acc.at(MAXP + p);
+                }
+            }
+        }
+    }
+    O.annual_kwh[i] = annual;
+    double den = kw_star > 1e-9 ? kw_star : 1e-9;
+    double naep = annual / den;
+    O.naep[i] = naep;
+    O.capacity_factor[i] = naep / 8760.0;
+    O.batt_kw[i] = power;
+    O.batt_kwh[i] = bank;
+    O.tariff_final[i] = tariff;
+    O.switched[i] = switched;
+    O.status[i] = status;
+    W.otc_b[i] = otc;
+}
+
+// ---------------------------------------------------------------------------
+// k_batt_finance: Utilityrate5 + Cashloan of the PV+battery run (ff:178-288)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK)
+k_batt_finance(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
+               int64_t n_scratch) {
+    __shared__ double lds[2 * MAXP * BLOCK];
+    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const int st = O.status[i];
+    if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH)) return;
+    WsLayout W = ws_layout(ws, n);
+    LdsAcc acc{lds + threadIdx.x};
+    const bool is_res = (A.flags[i] & 1) != 0;
+    const bool is_ca = (A.flags[i] & 2) != 0;
+    const int N = A.econ_life[i];
+    const dgen_tariff& t = T.tariffs[O.tariff_final[i]];
+    const double kw = O.system_kw[i];
+    const double bank = O.batt_kwh[i];
+    const double otc = W.otc_b[i];
+    const double rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
+    const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+    const LoanParams lp = make_loan(A, cfg, i, N, is_res);
+    // ff:203-219 costs of the PV+battery system
+    double system_costs = (kw > 0.0) ? A.capex_combined[i] * kw : A.capex[i] * kw;
+    double batt_costs = A.batt_capex_kwh[i] * bank * 0.7;
+    double total = ((system_costs + batt_costs) * A.ccm[i]) + 0.0 + otc;
+    const double vor = A.vor[i];
+
+    HourSrc src;
+    const int lr = A.load_row[i];
+    src.shape = T.shapes + (int64_t)lr * NH;
+    src.cf = nullptr;
+    src.load_scale = A.load_kwh[i] / T.shape_sum[lr];
+    src.gen_scale = 0.0;
+    src.sys_stride = n_scratch;
+    const int slot = A.scratch_slot[i];
+    src.sysgen = (slot >= 0) ? W.scratch + slot : nullptr;
+    int wr = A.wholesale_row[i];
+    src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+    src.ts_mult = A.price_mult[i];
+    const bool mo2 = t.mo == 2;
+    const double yr = cfg.nm_yearend_sell_rate;
+    const double* Lb = W.Lb + i;
+    const double* Gb = W.Gb + i;
+
+    double wo1 = mo2 ? year_bill_mo2(t, src, 1.0, false, acc) : year_bill_mo0(t, Lb, nullptr, n, 0.0, yr);
+    LoanState ls;
+    loan_begin(lp, total, ls);
+    O.cfev_batt[i] = 0.0;
+    O.bill_w_batt[i] = 0.0;
+    O.bill_wo_batt[i] = 0.0;
+    double r = 1.0, s = 1.0;
+    for (int y = 1; y <= N; y++) {
+        double wb = mo2 ? year_bill_mo2(t, src, s, true, acc) : year_bill_mo0(t, Lb, Gb, n, s, yr);
+        double w = wb * r;
+        double wo = wo1 * r;
+        double ev = (wo - w) + vor;          // ff:275: VOR added to every year
+        loan_year(lp, y, ev, ls);
+        O.cfev_batt[(int64_t)y * n + i] = ev;
+        O.bill_w_batt[(int64_t)y * n + i] = w;
+        O.bill_wo_batt[(int64_t)y * n + i] = wo;
+        r = r * rate_base;
+        s = s * sys_base;
+    }
+    O.npv_pv_batt[i] = ls.npv_acc;
+}
+
+// ---------------------------------------------------------------------------
+// Brent self-test kernel (closed-form objective; tests the search alone)
+// ---------------------------------------------------------------------------
+__global__ void k_brent_selftest(const double* lo, const double* hi, const double* xatol,
+                                 const double* c2, const double* x0, const double* c1, int64_t n,
+                                 double* xs, int maxn, double* xopt, int32_t* nfev) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int k = 0;
+    double a2 = c2[i], b0 = x0[i], a1 = c1[i];
+    double* rec = xs + i * maxn;
+    int nf = 0;
+    double xl = 0.0;
+    double xo = brent_bounded(
+        [&](double x) {
+            if (k < maxn) rec[k] = x;
+            k++;
+            double d = x - b0;
+            return a2 * d * d + a1 * x;
+        },
+        lo[i], hi[i], xatol[i], &nf, &xl);
+    xopt[i] = xo;
+    nfev[i] = nf;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+struct dgen_ctx {
+    int device;
+    dgen_cfg cfg;
+    static constexpr int RING = 64;
+    hipEvent_t ev[RING][4];
+    int head;          // next ring slot to record
+    int pending;       // recorded, not yet folded
+    double sum_ms[3];
+    int64_t count;
+};
+
+static int fold_one(dgen_ctx* c, int slot) {
+    HIP_TRY(hipEventSynchronize(c->ev[slot][3]));
+    for (int k = 0; k < 3; k++) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[slot][k], c->ev[slot][k + 1]));
+        c->sum_ms[k] += ms;
+    }
+    c->count++;
+    return 0;
+}
+
+extern "C" {
+
+int32_t dgen_abi_version(void) { return DGEN_ABI_VERSION; }
+
+int32_t dgen_last_error(char* buf, size_t n) {
+    if (!buf || n == 0) return DGEN_E_ARG;
+    snprintf(buf, n, "%s", g_err);
+    return DGEN_OK;
+}
+
+int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
+    if (!cfg || !out) { set_err("dgen_open: null argument"); return DGEN_E_ARG; }
+    if (cfg->skip_demand_charges != 1) {
+        set_err("dgen_open: demand charges are disabled in the reference (ff:35); "
+                "skip_demand_charges must be 1");
+        return DGEN_E_UNSUPPORTED;
+    }
+    if (!(cfg->batt_v_nom > 0.0) || !(cfg->batt_q_full > 0.0) || !(cfg->batt_eta_in > 0.0) ||
+        !(cfg->batt_eta_out > 0.0) || cfg->depr_sl_years < 1) {
+        set_err("dgen_open: invalid battery/loan configuration");
+        return DGEN_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(device));
+    dgen_ctx* c = new (std::nothrow) dgen_ctx();
+    if (!c) { set_err("dgen_open: out of host memory"); return DGEN_E_ARG; }
+    c->device = device;
+    c->cfg = *cfg;
+    c->head = 0; c->pending = 0; c->count = 0;
+    c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
+    for (int r = 0; r < dgen_ctx::RING; r++)
+        for (int k = 0; k < 4; k++) {
+            hipError_t e = hipEventCreate(&c->ev[r][k]);
+            if (e != hipSuccess) {
+                set_err("hipEventCreate failed: %s", hipGetErrorString(e));
+                delete c;
+                return DGEN_E_HIP;
+            }
+        }
+    *out = c;
+    return DGEN_OK;
+}
+
+int32_t dgen_close(dgen_ctx* c) {
+    if (!c) return DGEN_OK;
+    (void)hipSetDevice(c->device);
+    for (int r = 0; r < dgen_ctx::RING; r++)
+        for (int k = 0; k < 4; k++) (void)hipEventDestroy(c->ev[r][k]);
+    delete c;
+    return DGEN_OK;
+}
+
+int32_t dgen_prep_shapes(dgen_ctx* c, const float* shapes, int64_t n_rows, double* row_sum,
+                         double* row_slots, void* stream) {
+    if (!c || !shapes || !row_sum || !row_slots || n_rows <= 0) {
+        set_err("dgen_prep_shapes: bad argument");
+        return DGEN_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_row_pairwise_shape, dim3((unsigned)((n_rows + 127) / 128)), dim3(128), 0, s,
+                       shapes, n_rows, row_sum);
+    int64_t tot = n_rows * NSLOT;
+    hipLaunchKernelGGL(k_row_slots_shape, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                       shapes, n_rows, row_slots);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_prep_cfs(dgen_ctx* c, const int32_t* cfs, int64_t n_rows, double* row_naep,
+                      double* row_slots, void* stream) {
+    if (!c || !cfs || !row_naep || !row_slots || n_rows <= 0) {
+        set_err("dgen_prep_cfs: bad argument");
+        return DGEN_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_row_pairwise_cf, dim3((unsigned)((n_rows + 127) / 128)), dim3(128), 0, s,
+                       cfs, n_rows, row_naep);
+    int64_t tot = n_rows * NSLOT;
+    hipLaunchKernelGGL(k_row_slots_cf, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s,
+                       cfs, n_rows, row_slots);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+size_t dgen_workspace_bytes(int64_t n, int64_t n_scratch) {
+    if (n < 0 || n_scratch < 0) return 0;
+    return sizeof(double) * ((size_t)4 * NBIN * (size_t)n + (size_t)n + (size_t)NH * (size_t)n_scratch);
+}
+
+int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A,
+                         const dgen_outputs* O, int64_t n, void* ws, size_t ws_bytes,
+                         int64_t n_scratch, void* stream) {
+    if (!c || !T || !A || !O) { set_err("dgen_size_agents: null argument"); return DGEN_E_ARG; }
+    if (n <= 0) return DGEN_OK;
+    if (!T->shapes || !T->shape_sum || !T->shape_slots || !T->cfs || !T->cf_naep || !T->cf_slots ||
+        !T->tariffs || T->n_tariffs <= 0) {
+        set_err("dgen_size_agents: incomplete tables");
+        return DGEN_E_ARG;
+    }
+    const void* req_a[] = {A->load_row, A->cf_row, A->wholesale_row, A->tariff0, A->sw_solar_off,
+                           A->sw_solar_cnt, A->sw_storage_off, A->sw_storage_cnt, A->scratch_slot,
+                           A->flags, A->econ_life, A->loan_term, A->load_kwh, A->price_mult,
+                           A->inflation, A->pv_deg, A->escalator, A->down_payment, A->tax_rate,
+                           A->real_discount, A->itc_frac, A->capex, A->capex_combined,
+                           A->batt_capex_kwh, A->ccm, A->vor};
+    for (const void* p : req_a)
+        if (!p) { set_err("dgen_size_agents: missing agent column"); return DGEN_E_ARG; }
+    const void* req_o[] = {O->system_kw, O->x_last, O->annual_kwh, O->naep, O->capacity_factor,
+                           O->price_per_kwh, O->npv, O->payback_raw, O->payback_period,
+                           O->first_with, O->first_without, O->batt_kw, O->batt_kwh,
+                           O->npv_pv_batt, O->nfev, O->tariff_final, O->switched, O->status,
+                           O->cash_flow, O->cfev_pv, O->bill_w_pv, O->bill_wo_pv, O->cfev_batt,
+                           O->bill_w_batt, O->bill_wo_batt};
+    for (const void* p : req_o)
+        if (!p) { set_err("dgen_size_agents: missing output column"); return DGEN_E_ARG; }
+    if (!ws || ws_bytes < dgen_workspace_bytes(n, n_scratch)) {
+        set_err("dgen_size_agents: workspace too small (%zu < %zu)", ws_bytes,
+                dgen_workspace_bytes(n, n_scratch));
+        return DGEN_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (c->pending == dgen_ctx::RING) {   // fold the oldest record before reuse
+        int r = fold_one(c, c->head);
+        if (r) return r;
+        c->pending--;
+    }
+    int slot = c->head;
+    c->head = (c->head + 1) % dgen_ctx::RING;
+    c->pending++;
+    dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK)), block(BLOCK);
+    HIP_TRY(hipEventRecord(c->ev[slot][0], s));
+    hipLaunchKernelGGL(k_size, grid, block, 0, s, *T, *A, *O, c->cfg, n, ws);
+    HIP_TRY(hipEventRecord(c->ev[slot][1], s));
+    hipLaunchKernelGGL(k_hourly_batt, grid, block, 0, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
+    HIP_TRY(hipEventRecord(c->ev[slot][2], s));
+    hipLaunchKernelGGL(k_batt_finance, grid, block, 0, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
+    HIP_TRY(hipEventRecord(c->ev[slot][3], s));
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_kernel_times(dgen_ctx* c, double* ms_size, double* ms_hourly, double* ms_finance) {
+    if (!c) { set_err("dgen_kernel_times: null ctx"); return DGEN_E_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    int start = (c->head - c->pending + dgen_ctx::RING) % dgen_ctx::RING;
+    for (int k = 0; k < c->pending; k++) {
+        int r = fold_one(c, (start + k) % dgen_ctx::RING);
+        if (r) return r;
+    }
+    c->pending = 0;
+    double cnt = c->count > 0 ? (double)c->count : 1.0;
+    if (ms_size) *ms_size = c->sum_ms[0] / cnt;
+    if (ms_hourly) *ms_hourly = c->sum_ms[1] / cnt;
+    if (ms_finance) *ms_finance = c->sum_ms[2] / cnt;
+    int64_t got = c->count;
+    c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
+    c->count = 0;
+    return (int32_t)got;
+}
+
+int32_t dgen_brent_selftest(dgen_ctx* c, const double* lo, const double* hi, const double* xatol,
+                            const double* c2, const double* x0, const double* c1, int64_t n,
+                            double* xs, int32_t maxn, double* xopt, int32_t* nfev, void* stream) {
+    if (!c || !lo || !hi || !xatol || !c2 || !x0 || !c1 || !xs || !xopt || !nfev || maxn <= 0) {
+        set_err("dgen_brent_selftest: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n <= 0) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_brent_selftest, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                       (hipStream_t)stream, lo, hi, xatol, c2, x0, c1, n, xs, maxn, xopt, nfev);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,245 @@
+"""Device engine: resident profile/tariff tables + batched sizing on one GPU.
+
+PyTorch-ROCm is used only for device memory and the stream; all compute is in
+libdgen_hip.so (hand-written gfx950 kernels) reached through the C-ABI.  There
+is no CPU fallback: without a HIP device or the library every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _lib
+from .config import EngineConfig
+
+SWITCH_DTYPE = np.dtype([("min_kw", "<f8"), ("max_kw", "<f8"), ("one_time_charge", "<f8"),
+                         ("tariff", "<i4"), ("pad", "<i4")])
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else int(t.data_ptr())
+
+
+@dataclass
+class AgentBatch:
+    n: int
+    n_scratch: int
+    cols: Dict[str, object]          # name -> device tensor
+    workspace: object                # uint8 device tensor
+    c_agents: _lib.Agents = field(default=None)
+
+
+class Engine:
+    def __init__(self, device: int = 0, cfg: Optional[EngineConfig] = None):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise _lib.DgenError("no HIP device visible: the dGen MI355X engine has no CPU path")
+        self.lib = _lib.load()
+        self.device = int(device)
+        self.cfg = cfg or EngineConfig()
+        torch.cuda.set_device(self.device)
+        self.dev = torch.device("cuda", self.device)
+        h = ctypes.c_void_p()
+        c = self.cfg.to_c()
+        _lib.check(self.lib.dgen_open(self.device, ctypes.byref(c), ctypes.byref(h)), "dgen_open")
+        self.ctx = h
+        self.tables = _lib.Tables()
+        self._keep: Dict[str, object] = {}
+
+    # ------------------------------------------------------------------ utils
+    def stream_handle(self) -> int:
+        return int(_torch().cuda.current_stream(self.dev).cuda_stream)
+
+    def _to_dev(self, a, dtype):
+        torch = _torch()
+        if isinstance(a, torch.Tensor):
+            return a.to(device=self.dev, dtype=dtype).contiguous()
+        return torch.from_numpy(np.ascontiguousarray(a)).to(device=self.dev, dtype=dtype)
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.dgen_close(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ----------------------------------------------------------------- tables
+    def load_profiles(self, shapes, cfs, wholesale=None):
+        """Upload kwh_load_profile rows (float32 [R, 8760]), solar cf x 1e6 rows
+        (int32 [C, 8760]) and optional wholesale $/kWh rows (float64 [W, 8760]);
+        precompute numpy-order row sums and slot sums on device."""
+        torch = _torch()
+        sh = self._to_dev(shapes, torch.float32)
+        cf = self._to_dev(cfs, torch.int32)
+        if sh.dim() != 2 or sh.shape[1] != _lib.NH or cf.dim() != 2 or cf.shape[1] != _lib.NH:
+            raise ValueError("profile tables must be [rows, 8760]")
+        R, C = sh.shape[0], cf.shape[0]
+        s_sum = torch.empty(R, dtype=torch.float64, device=self.dev)
+        s_slots = torch.empty((R, _lib.NSLOT), dtype=torch.float64, device=self.dev)
+        c_naep = torch.empty(C, dtype=torch.float64, device=self.dev)
+        c_slots = torch.empty((C, _lib.NSLOT), dtype=torch.float64, device=self.dev)
+        st = self.stream_handle()
+        _lib.check(self.lib.dgen_prep_shapes(self.ctx, _ptr(sh), R, _ptr(s_sum), _ptr(s_slots), st),
+                   "dgen_prep_shapes")
+        _lib.check(self.lib.dgen_prep_cfs(self.ctx, _ptr(cf), C, _ptr(c_naep), _ptr(c_slots), st),
+                   "dgen_prep_cfs")
+        ws = None
+        if wholesale is not None and len(wholesale):
+            ws = self._to_dev(wholesale, torch.float64)
+            if ws.dim() != 2 or ws.shape[1] != _lib.NH:
+                raise ValueError("wholesale table must be [rows, 8760]")
+        self._keep.update(shapes=sh, shape_sum=s_sum, shape_slots=s_slots, cfs=cf,
+                          cf_naep=c_naep, cf_slots=c_slots, wholesale=ws)
+        T = self.tables
+        T.shapes, T.shape_sum, T.shape_slots = _ptr(sh), _ptr(s_sum), _ptr(s_slots)
+        T.cfs, T.cf_naep, T.cf_slots = _ptr(cf), _ptr(c_naep), _ptr(c_slots)
+        T.wholesale = _ptr(ws)
+        T.n_shapes, T.n_cfs = R, C
+        T.n_wholesale = 0 if ws is None else ws.shape[0]
+
+    def set_tariffs(self, records: np.ndarray):
+        from .tariff import TARIFF_DTYPE
+        recs = np.ascontiguousarray(records, dtype=TARIFF_DTYPE)
+        if recs.size == 0:
+            raise ValueError("empty tariff table")
+        raw = np.frombuffer(recs.tobytes(), dtype=np.uint8)
+        t = self._to_dev(raw, _torch().uint8)
+        self._keep["tariffs"] = t
+        self.tariff_records = recs
+        self.tables.tariffs = _ptr(t)
+        self.tables.n_tariffs = int(recs.size)
+
+    def set_switches(self, sw: np.ndarray):
+        sw = np.ascontiguousarray(sw, dtype=SWITCH_DTYPE)
+        if sw.size == 0:
+            sw = np.zeros(1, dtype=SWITCH_DTYPE)
+        raw = np.frombuffer(sw.tobytes(), dtype=np.uint8)
+        t = self._to_dev(raw, _torch().uint8)
+        self._keep["switches"] = t
+        self.tables.switches = _ptr(t)
+        self.tables.n_switches = int(sw.size)
+
+    def profile_sums(self):
+        """(shape row sums, cf naep) as host arrays (for tests / host checks)."""
+        return (self._keep["shape_sum"].cpu().numpy(), self._keep["cf_naep"].cpu().numpy())
+
+    # ------------------------------------------------------------------ batch
+    def upload_agents(self, cols: Dict[str, np.ndarray], n_scratch: Optional[int] = None) -> AgentBatch:
+        torch = _torch()
+        n = len(cols["load_kwh"])
+        dev = {}
+        tmap = {"int32": torch.int32, "uint8": torch.uint8, "float64": torch.float64}
+        for name, dt in _lib.AGENT_COLUMNS:
+            if name not in cols:
+                raise KeyError(f"agent column {name!r} missing")
+            v = cols[name]
+            if len(v) != n:
+                raise ValueError(f"agent column {name!r} has length {len(v)} != {n}")
+            dev[name] = self._to_dev(np.asarray(v, dtype=dt) if not isinstance(v, torch.Tensor) else v,
+                                     tmap[dt])
+        if n_scratch is None:
+            slots = dev["scratch_slot"]
+            n_scratch = int(slots.max().item()) + 1 if n > 0 else 0
+            n_scratch = max(n_scratch, 0)
+        self.validate_agents(dev, n)
+        wsb = int(self.lib.dgen_workspace_bytes(n, n_scratch))
+        ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
+        ca = _lib.Agents(**{name: _ptr(dev[name]) for name, _ in _lib.AGENT_COLUMNS})
+        return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca)
+
+    def validate_agents(self, dev, n):
+        """Host-side bounds checks before any kernel indexes a table."""
+        T = self.tables
+        if T.n_tariffs <= 0 or not T.shapes:
+            raise _lib.DgenError("tables not loaded")
+        def rng(name, lo, hi):
+            v = dev[name]
+            if n and (int(v.min().item()) < lo or int(v.max().item()) >= hi):
+                raise ValueError(f"agent column {name!r} out of range [{lo}, {hi})")
+        rng("load_row", 0, T.n_shapes)
+        rng("cf_row", 0, T.n_cfs)
+        rng("wholesale_row", -1, max(T.n_wholesale, 0))
+        rng("tariff0", 0, T.n_tariffs)
+        for k in ("solar", "storage"):
+            off, cnt = dev[f"sw_{k}_off"], dev[f"sw_{k}_cnt"]
+            if n and (int(off.min().item()) < 0 or int(cnt.min().item()) < 0
+                      or int((off.long() + cnt.long()).max().item()) > T.n_switches):
+                raise ValueError(f"rate-switch ({k}) offsets out of range")
+
+    def alloc_outputs(self, n: int, hourly: bool = True) -> Dict[str, object]:
+        torch = _torch()
+        out = {}
+        for name, dt in _lib.OUTPUT_SCALARS:
+            out[name] = torch.empty(n, dtype=torch.float64 if dt == "float64" else torch.int32,
+                                    device=self.dev)
+        for name in _lib.OUTPUT_YEARLY:
+            out[name] = torch.zeros((_lib.MAXY + 1, n), dtype=torch.float64, device=self.dev)
+        for name in _lib.OUTPUT_HOURLY:
+            out[name] = (torch.empty((_lib.NH, n), dtype=torch.float32, device=self.dev)
+                         if hourly else None)
+        return out
+
+    @staticmethod
+    def c_outputs(out: Dict[str, object]) -> _lib.Outputs:
+        fields = {name: _ptr(out[name]) for name, _ in _lib.OUTPUT_SCALARS}
+        fields.update({name: _ptr(out[name]) for name in _lib.OUTPUT_YEARLY})
+        fields.update({name: _ptr(out.get(name)) for name in _lib.OUTPUT_HOURLY})
+        return _lib.Outputs(**fields)
+
+    def size(self, batch: AgentBatch, out: Dict[str, object], c_out: Optional[_lib.Outputs] = None):
+        """Launch the sizing kernels for `batch` on the current stream (async)."""
+        co = c_out if c_out is not None else self.c_outputs(out)
+        _lib.check(self.lib.dgen_size_agents(self.ctx, ctypes.byref(self.tables),
+                                             ctypes.byref(batch.c_agents), ctypes.byref(co),
+                                             batch.n, _ptr(batch.workspace),
+                                             batch.workspace.numel(), batch.n_scratch,
+                                             self.stream_handle()),
+                   "dgen_size_agents")
+
+    def kernel_times(self):
+        """Average per-launch device time (ms) of the three sizing kernels over
+        the calls since the last query, from HIP events on the launch stream."""
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        cnt = _lib.check(self.lib.dgen_kernel_times(self.ctx, ctypes.byref(a), ctypes.byref(b),
+                                                    ctypes.byref(c)), "dgen_kernel_times")
+        return a.value, b.value, c.value, cnt
+
+    def brent_selftest(self, lo, hi, xatol, c2, x0, c1, maxn=64):
+        torch = _torch()
+        f = lambda v: self._to_dev(np.asarray(v, dtype=np.float64), torch.float64)
+        tl, th, ta, t2, t0, t1 = (f(v) for v in (lo, hi, xatol, c2, x0, c1))
+        n = tl.numel()
+        xs = torch.zeros((n, maxn), dtype=torch.float64, device=self.dev)
+        xo = torch.zeros(n, dtype=torch.float64, device=self.dev)
+        nf = torch.zeros(n, dtype=torch.int32, device=self.dev)
+        _lib.check(self.lib.dgen_brent_selftest(self.ctx, _ptr(tl), _ptr(th), _ptr(ta), _ptr(t2),
+                                                _ptr(t0), _ptr(t1), n, _ptr(xs), maxn, _ptr(xo),
+                                                _ptr(nf), self.stream_handle()),
+                   "dgen_brent_selftest")
+        torch.cuda.synchronize(self.dev)
+        return xs.cpu().numpy(), xo.cpu().numpy(), nf.cpu().numpy()
+
+
+def outputs_to_host(out: Dict[str, object]) -> Dict[str, np.ndarray]:
+    """Device outputs -> host numpy (yearly planes transposed to [agent][year])."""
+    res = {}
+    for name, _ in _lib.OUTPUT_SCALARS:
+        res[name] = out[name].cpu().numpy()
+    for name in _lib.OUTPUT_YEARLY:
+        res[name] = out[name].cpu().numpy().T.copy()
+    for name in _lib.OUTPUT_HOURLY:
+        t = out.get(name)
+        res[name] = None if t is None else t.cpu().numpy().T.copy()
+    return res

@@ -1,0 +1,231 @@
+"""Synthetic agent populations: the reference's DB and agent
+files are remote downloads, so every benchmark / scale test runs on
+populations generated here with numpy PCG64, seed = 20260000 + config number.
+
+Profiles: diurnal x seasonal x lognormal load shapes normalised to 1 (float32),
+solar cf x 1e6 (int32, 1100-1900 kWh/kW-yr, zero at night), per-county 8760
+wholesale $/kWh.  Scalars: the 2026 rows of the reference's input CSVs
+(financing_atb_FY23.csv:14, pv_price_atb23_mid.csv:14,
+pv_plus_batt_prices_FY23_mid.csv:14, pv_tech_performance_defaultFY19.csv:14).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _lib
+from .columnar import assign_scratch, empty_columns
+from .engine import SWITCH_DTYPE
+from .tariff import TariffTable
+
+NH = _lib.NH
+
+CONFIGS = {
+    # name: (config number, sector mix, tariff metering, description)
+    "de_res": (1, "res", "nem", "DE-like residential PV-only stand-in (50k)"),
+    "ca_res_storage": (2, "res", "ca", "CA-like residential PV+storage stand-in (200k)"),
+    "res_1m_nem_tou": (3, "res", "nem", "synthetic 1M residential, NEM TOU tariffs"),
+    "com_8m": (4, "com", "nem", "synthetic commercial with battery"),
+    "national_mixed": (5, "mixed", "mixed", "national mixed population"),
+}
+
+
+@dataclass
+class Population:
+    shapes: np.ndarray           # float32 [R, 8760]
+    cfs: np.ndarray              # int32 [C, 8760]
+    wholesale: Optional[np.ndarray]  # float64 [W, 8760]
+    tariffs: np.ndarray          # TARIFF_DTYPE
+    switches: np.ndarray         # SWITCH_DTYPE
+    cols: Dict[str, np.ndarray]  # agent SoA columns
+    n_scratch: int
+    config: str
+
+
+def load_shapes(rng, n_rows: int, commercial: bool) -> np.ndarray:
+    hod = np.arange(NH) % 24
+    doy = np.arange(NH) // 24
+    dow = doy % 7
+    out = np.empty((n_rows, NH), dtype=np.float32)
+    step = 256
+    for s in range(0, n_rows, step):
+        k = min(step, n_rows - s)
+        ph = rng.uniform(-2.0, 2.0, (k, 1))
+        amp = rng.uniform(0.3, 0.9, (k, 1))
+        sea = rng.uniform(0.1, 0.5, (k, 1))
+        if commercial:
+            occ = ((hod >= 7) & (hod <= 19) & (dow < 5)).astype(float)
+            diurnal = 0.45 + amp * occ + 0.05 * np.sin((hod - 12 - ph) / 24 * 2 * np.pi)
+        else:
+            diurnal = (1.0 + amp * np.sin((hod - 7 - ph) / 24 * 2 * np.pi) ** 2
+                       + 0.4 * amp * ((hod >= 17) & (hod <= 21)))
+        seasonal = 1.0 + sea * np.cos((doy - 200 + 20 * ph) / 365 * 2 * np.pi)
+        noise = rng.lognormal(0.0, 0.25, (k, NH))
+        x = diurnal * seasonal * noise
+        out[s:s + k] = (x / x.sum(axis=1, keepdims=True)).astype(np.float32)
+    return out
+
+
+def solar_cfs(rng, n_rows: int) -> np.ndarray:
+    hod = np.arange(NH) % 24
+    doy = np.arange(NH) // 24
+    out = np.empty((n_rows, NH), dtype=np.int32)
+    step = 256
+    for s in range(0, n_rows, step):
+        k = min(step, n_rows - s)
+        lat = rng.uniform(-0.8, 0.8, (k, 1))
+        daylen = 12.0 + 3.0 * np.cos((doy - 172) / 365 * 2 * np.pi) * (1 + 0.3 * lat)
+        rise = 12.0 - daylen / 2
+        t = (hod + 0.5 - rise) / daylen
+        sun = np.clip(np.sin(np.pi * t), 0.0, None) * ((t > 0) & (t < 1))
+        cloud = np.clip(rng.normal(0.85, 0.22, (k, NH)), 0.05, 1.0)
+        cf = sun * cloud
+        target = rng.uniform(1100.0, 1900.0, (k, 1))
+        cf = cf * (target / cf.sum(axis=1, keepdims=True))
+        out[s:s + k] = np.round(np.clip(cf, 0.0, 1.0) * 1e6).astype(np.int32)
+    return out
+
+
+def wholesale_rows(rng, n_rows: int) -> np.ndarray:
+    hod = np.arange(NH) % 24
+    doy = np.arange(NH) // 24
+    base = rng.uniform(0.02, 0.08, (n_rows, 1))
+    w = base * (1.0 + 0.35 * np.sin((hod - 14) / 24 * 2 * np.pi)[None, :]
+                + 0.15 * np.cos((doy - 200) / 365 * 2 * np.pi)[None, :])
+    w += rng.normal(0.0, 0.003, (n_rows, NH))
+    return np.clip(w, 0.005, None)
+
+
+def random_tariffs(rng, n: int, metering: str):
+    """256-ish synthetic URDB-style tariffs: P 1..4, T 1..3 (mostly BIG caps),
+    prices U[0.06, 0.40] $/kWh, fixed U[0, 25] $/month; legacy e_* and ur_*
+    forms mixed.  metering: 'nem' -> mo 0; 'nb' -> mo 2; 'mixed' -> 20 % mo 2."""
+    out = []
+    for k in range(n):
+        P = int(rng.integers(1, 5))
+        T = int(rng.integers(1, 4))
+        prices = np.sort(np.round(rng.uniform(0.06, 0.40, (T, P)), 5), axis=0)
+        fixed = float(np.round(rng.uniform(0.0, 25.0), 2))
+        on0 = int(rng.integers(12, 18))
+        wk = np.zeros((12, 24), dtype=int)
+        for p in range(1, P):
+            wk[:, (on0 + 2 * p) % 24:(on0 + 2 * p + 3) % 24 or 24] = p
+        we = np.zeros((12, 24), dtype=int)
+        mo = 0 if metering == "nem" else (2 if metering == "nb" else int(rng.random() < 0.2) * 2)
+        lv = None
+        if T > 1:
+            lv = np.sort(rng.choice([250.0, 400.0, 600.0, 900.0], size=(T, P)), axis=0)
+            lv[-1, :] = 1e38
+        if k % 2 == 0:
+            d = {"e_prices": prices.tolist(), "e_wkday_12by24": wk.tolist(),
+                 "e_wkend_12by24": we.tolist(), "fixed_charge": fixed, "ur_metering_option": mo}
+            if lv is not None:
+                d["e_levels"] = lv.tolist()
+        else:
+            rows = [[p + 1, t + 1, 1e38 if lv is None else float(lv[t, p]), 0, float(prices[t, p]), 0.0]
+                    for p in range(P) for t in range(T)]
+            d = {"ur_ec_tou_mat": rows, "ur_ec_sched_weekday": (wk + 1).tolist(),
+                 "ur_ec_sched_weekend": (we + 1).tolist(), "ur_monthly_fixed_charge": fixed,
+                 "ur_metering_option": mo}
+        out.append(d)
+    return out
+
+
+STATES = ["AL", "AZ", "AR", "CA", "CO", "CT", "DE", "FL", "GA", "ID", "IL", "IN", "IA", "KS", "KY",
+          "LA", "ME", "MD", "MA", "MI", "MN", "MS", "MO", "MT", "NE", "NV", "NH", "NJ", "NM", "NY",
+          "NC", "ND", "OH", "OK", "OR", "PA", "RI", "SC", "SD", "TN", "TX", "UT", "VT", "VA", "WA",
+          "WV", "WI", "WY", "DC", "AK", "HI"]
+
+
+def make_population(config: str, n_agents: int, seed: Optional[int] = None,
+                    n_res_shapes: int = 4096, n_com_shapes: int = 2048, n_cf: int = 2048,
+                    n_counties: int = 3100, n_tariffs: int = 256) -> Population:
+    if config not in CONFIGS:
+        raise KeyError(f"unknown config {config!r}; one of {sorted(CONFIGS)}")
+    cnum, sector, metering, _ = CONFIGS[config]
+    rng = np.random.default_rng(20260000 + cnum if seed is None else seed)
+    n = int(n_agents)
+
+    res_shapes = load_shapes(rng, n_res_shapes, commercial=False)
+    com_shapes = load_shapes(rng, n_com_shapes, commercial=True)
+    shapes = np.concatenate([res_shapes, com_shapes])
+    cfs = solar_cfs(rng, n_cf)
+    wholesale = wholesale_rows(rng, n_counties)
+
+    tt = TariffTable()
+    raw = random_tariffs(rng, n_tariffs, "nem" if metering in ("nem", "ca") else metering)
+    base_idx = np.array([tt.add(d, False) for d in raw], dtype=np.int32)
+    ca_idx = np.array([tt.add(d, True) for d in raw], dtype=np.int32)
+
+    if sector == "res":
+        is_res = np.ones(n, dtype=bool)
+    elif sector == "com":
+        is_res = np.zeros(n, dtype=bool)
+    else:
+        is_res = rng.random(n) < 0.75
+    if metering == "ca":
+        is_ca = np.ones(n, dtype=bool)
+    elif sector == "mixed" or metering == "mixed":
+        is_ca = rng.integers(0, len(STATES), n) == STATES.index("CA")
+    else:
+        is_ca = np.zeros(n, dtype=bool)
+
+    cols = empty_columns(n)
+    cols["load_row"] = np.where(is_res, rng.integers(0, n_res_shapes, n),
+                                n_res_shapes + rng.integers(0, n_com_shapes, n)).astype(np.int32)
+    cols["cf_row"] = rng.integers(0, n_cf, n).astype(np.int32)
+    county = rng.integers(0, n_counties, n).astype(np.int32)
+    cols["wholesale_row"] = np.where(is_ca, -1, county).astype(np.int32)
+    tix = rng.integers(0, n_tariffs, n)
+    cols["tariff0"] = np.where(is_ca, ca_idx[tix], base_idx[tix]).astype(np.int32)
+    cols["flags"] = (is_res.astype(np.uint8) | (is_ca.astype(np.uint8) << 1)).astype(np.uint8)
+    res_load = rng.lognormal(np.log(10000.0), 0.35, n)
+    com_load = np.clip(rng.lognormal(np.log(150000.0), 1.2, n), 1e4, 5e7)
+    cols["load_kwh"] = np.where(is_res, res_load, com_load)
+    cols["price_mult"] = rng.uniform(0.9, 1.1, n)
+    cols["econ_life"] = np.full(n, 25, dtype=np.int32)
+    cols["loan_term"] = np.where(is_res, 20, 30).astype(np.int32)
+    cols["inflation"] = np.full(n, 0.025)
+    cols["pv_deg"] = np.full(n, 0.005)
+    cols["escalator"] = rng.uniform(-0.01, 0.01, n)
+    cols["down_payment"] = np.where(is_res, 0.3, 1.0)
+    cols["tax_rate"] = np.full(n, 0.2574)
+    cols["real_discount"] = np.where(is_res, 0.05, 0.0378)
+    cols["itc_frac"] = np.full(n, 0.3)
+    cols["capex"] = np.where(is_res, 4637.5, 1672.9)
+    cols["capex_combined"] = np.where(is_res, 4500.0, 1600.0)
+    cols["batt_capex_kwh"] = np.where(is_res, 431.0, 197.3)
+    cols["ccm"] = rng.uniform(0.9, 1.2, n)
+    cols["vor"] = np.where(rng.random(n) < 0.2, rng.uniform(0.0, 300.0, n), 0.0)
+
+    # 10 % of (utility, sector) get one DG rate-switch row (solar)
+    n_util = 3000
+    util = rng.integers(0, n_util, n)
+    has_dg = rng.random((n_util, 2)) < 0.10
+    sw = []
+    first = np.full((n_util, 2, 2), -1, dtype=np.int64)   # [util, is_res, is_ca] -> switch index
+    for u in range(n_util):
+        for r in range(2):
+            if not has_dg[u, r]:
+                continue
+            lim = 10.0 if r == 1 else 200.0
+            k = int(rng.integers(0, n_tariffs))
+            otc = float(rng.uniform(0.0, 500.0))
+            for c in range(2):
+                rec = np.zeros((), dtype=SWITCH_DTYPE)
+                rec["min_kw"], rec["max_kw"], rec["one_time_charge"] = 0.0, lim, otc
+                rec["tariff"] = ca_idx[k] if c else base_idx[k]
+                first[u, r, c] = len(sw)
+                sw.append(rec)
+    switches = np.stack(sw).astype(SWITCH_DTYPE) if sw else np.zeros(0, dtype=SWITCH_DTYPE)
+    idx = first[util, is_res.astype(int), is_ca.astype(int)]
+    cols["sw_solar_off"] = np.where(idx >= 0, idx, 0).astype(np.int32)
+    cols["sw_solar_cnt"] = (idx >= 0).astype(np.int32)
+    cols["sw_storage_off"] = np.zeros(n, dtype=np.int32)
+    cols["sw_storage_cnt"] = np.zeros(n, dtype=np.int32)
+    tariffs = tt.array()
+    n_scratch = assign_scratch(cols, tariffs, switches)
+    return Population(shapes=shapes, cfs=cfs, wholesale=wholesale, tariffs=tariffs,
+                      switches=switches, cols=cols, n_scratch=n_scratch, config=config)

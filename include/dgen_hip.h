@@ -1,0 +1,229 @@
+/*
+ * dgen_hip.h -- C-ABI of libdgen_hip.so, the MI355X (gfx950) sizing & economics
+ * engine that replaces dGen's per-agent hot path.
+ *
+ * Reference interface replaced (tsgsteele/dgen @ 2025-09-19, /root/reference):
+ *   financial_functions.calc_system_size_and_performance   dgen_os/python/financial_functions.py:291-568
+ *   financial_functions.calc_system_performance (objective) dgen_os/python/financial_functions.py:96-288
+ *   financial_functions.size_chunk (worker loop)            dgen_os/python/financial_functions.py:1136-1218
+ *   agent_mutation.elec.get_and_apply_agent_load_profiles   dgen_os/python/agent_mutation/elec.py:508-532
+ *   agent_mutation.elec.get_and_apply_normalized_hourly_resource_solar  elec.py:535-558
+ *   agent_mutation.elec.apply_rate_switch                    dgen_os/python/agent_mutation/elec.py:838-863
+ *   PySAM Utilityrate5 / Cashloan / Battery .execute()       financial_functions.py:164,270,287
+ *   scipy.optimize.minimize_scalar(method='bounded')         financial_functions.py:445-447
+ *
+ * Conventions
+ *   - Plain C types only; every pointer in dgen_tables / dgen_agents /
+ *     dgen_outputs is a DEVICE pointer owned by the caller (the Python host keeps
+ *     them in torch-ROCm tensors) and borrowed for the duration of a call.
+ *   - Every entry point returns 0 on success or a negative DGEN_E_* code; the
+ *     message is available from dgen_last_error().  No exception crosses the ABI.
+ *   - Per-agent problems are reported in dgen_outputs.status (DGEN_ST_* bits);
+ *     the host raises like the reference's abort-the-year behaviour
+ *     (dgen_model.py:382).
+ *   - Calls are stream-ordered on the given hipStream_t (NULL = default stream)
+ *     and asynchronous unless stated otherwise.
+ *   - Array outputs are plane-major: value (y, agent) at [y * n + agent]; hourly
+ *     outputs are time-major: (hour, agent) at [hour * n + agent].
+ */
+#ifndef DGEN_HIP_H
+#define DGEN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DGEN_ABI_VERSION 1
+#define DGEN_NH    8760   /* hours per year                                    */
+#define DGEN_NSLOT 576    /* 12 months x {weekday, weekend} x 24 hours         */
+#define DGEN_MAXP  12     /* TOU periods                                        */
+#define DGEN_MAXT  6      /* tiers                                              */
+#define DGEN_MAXY  50     /* analysis years                                     */
+
+/* error codes */
+#define DGEN_OK            0
+#define DGEN_E_ARG        -1
+#define DGEN_E_HIP        -2
+#define DGEN_E_UNSUPPORTED -3
+
+/* per-agent status bits */
+#define DGEN_ST_BOUNDS       0x01  /* non-finite Brent bracket (scipy raises)       */
+#define DGEN_ST_TARIFF       0x02  /* tariff index out of range / malformed          */
+#define DGEN_ST_EMPTY_EC     0x04  /* tariff has no energy-charge matrix              */
+#define DGEN_ST_UNIT         0x08  /* unsupported usage unit code (1, 3)              */
+#define DGEN_ST_YEARS        0x10  /* analysis period outside 1..DGEN_MAXY            */
+#define DGEN_ST_SCRATCH      0x20  /* mo=2 battery run without a scratch slot         */
+#define DGEN_ST_ZERO_LOAD    0x40  /* load_kwh == 0: reference divides by zero (ff:549)*/
+
+/* Engine configuration: the PySAM config defaults the reference never sets
+ * (CustomGenerationBattery{Residential,Commercial}, ff:59-80) plus the
+ * reference's module switches (ff:35,38).                                     */
+typedef struct {
+    int32_t skip_demand_charges;   /* must be 1 (ff:35 SKIP_DEMAND_CHARGES=True)   */
+    int32_t force_net_billing;     /* ff:38; applied by the host tariff compiler    */
+    double  nm_yearend_sell_rate;  /* $/kWh, Utilityrate5 ur_nm_yearend_sell_rate  */
+    double  loan_rate_pct;         /* Cashloan loan_rate (%)                        */
+    double  insurance_rate_pct;    /* Cashloan insurance_rate (%)                   */
+    double  itc_fed_max;           /* Cashloan itc_fed_percent_maxvalue ($)         */
+    int32_t depr_sl_years;         /* straight-line depreciation years (type 2)     */
+    int32_t pad0;
+    double  batt_v_nom;            /* Li-ion cell nominal voltage (V)               */
+    double  batt_q_full;           /* cell capacity (Ah)                            */
+    double  batt_min_soc;          /* fraction                                      */
+    double  batt_max_soc;          /* fraction                                      */
+    double  batt_init_soc;         /* fraction (ff:151: 30 %)                       */
+    double  batt_eta_in;           /* AC -> stored                                  */
+    double  batt_eta_out;          /* stored -> AC                                  */
+} dgen_cfg;
+
+/* Compiled tariff = the Utilityrate5.ElectricityRates energy fields that
+ * process_tariff (ff:575-648) writes, after normalize_tariff (ff:962-1007).
+ * Built on the host, bit-exact to the reference compile (tests/golden).      */
+typedef struct {
+    int32_t P, T;                  /* periods, tiers                               */
+    int32_t mo;                    /* ur_metering_option (0 or 2)                  */
+    int32_t unit;                  /* usage unit code (0 kWh/mo, 2 kWh/day)        */
+    double  fixed;                 /* ur_monthly_fixed_charge ($/month)            */
+    double  cap[DGEN_MAXT];        /* tier upper bounds (single cap per tier)      */
+    double  buy[DGEN_MAXP][DGEN_MAXT];
+    double  sell[DGEN_MAXP][DGEN_MAXT];
+    uint8_t wkday[12][24];         /* 0-based period per (month, hour)             */
+    uint8_t wkend[12][24];
+    int32_t flags;                 /* DGEN_ST_EMPTY_EC / DGEN_ST_UNIT if applicable*/
+    int32_t pad;
+} dgen_tariff;
+
+/* One row of diffusion_shared.rate_switch_lkup_2020 (elec.py:828-836), already
+ * filtered to one agent's (tech, eia_id, res_com) on the host.                */
+typedef struct {
+    double  min_kw, max_kw, one_time_charge;
+    int32_t tariff;                /* index into dgen_tables.tariffs                */
+    int32_t pad;
+} dgen_switch;
+
+/* Resident tables (device pointers). */
+typedef struct {
+    const float*   shapes;         /* [n_shapes][8760] kwh_load_profile rows        */
+    const double*  shape_sum;      /* [n_shapes]   np.sum of the row (numpy order)  */
+    const double*  shape_slots;    /* [n_shapes][576] slot sums of the row          */
+    const int32_t* cfs;            /* [n_cfs][8760] solar cf x 1e6                  */
+    const double*  cf_naep;        /* [n_cfs]      np.sum(cf / 1e6)                 */
+    const double*  cf_slots;       /* [n_cfs][576] slot sums of cf / 1e6            */
+    const double*  wholesale;      /* [n_wholesale][8760] $/kWh (may be NULL)       */
+    const dgen_tariff* tariffs;
+    const dgen_switch* switches;
+    int64_t n_shapes, n_cfs, n_wholesale, n_switches;
+    int32_t n_tariffs, pad;
+} dgen_tables;
+
+/* Agent batch, structure of arrays (device pointers, length n).  Column
+ * meaning follows the agent row read by the reference. */
+typedef struct {
+    const int32_t* load_row;       /* row of shapes  <- (bldg_id, sector, state)     */
+    const int32_t* cf_row;         /* row of cfs     <- (gid, tilt, azimuth)         */
+    const int32_t* wholesale_row;  /* row of wholesale or -1 (no finite 8760 series) */
+    const int32_t* tariff0;        /* initial tariff (tariff_dict)                   */
+    const int32_t* sw_solar_off;   /* rate-switch candidates, tech = 'solar'          */
+    const int32_t* sw_solar_cnt;
+    const int32_t* sw_storage_off; /* rate-switch candidates, tech = 'storage'        */
+    const int32_t* sw_storage_cnt;
+    const int32_t* scratch_slot;   /* hourly scratch slot for mo=2 battery runs or -1 */
+    const uint8_t* flags;          /* bit0 sector_abbr == 'res', bit1 state == 'CA'  */
+    const int32_t* econ_life;      /* economic_lifetime_yrs                           */
+    const int32_t* loan_term;      /* loan_term_yrs                                   */
+    const double* load_kwh;        /* load_kwh_per_customer_in_bin                    */
+    const double* price_mult;      /* elec_price_multiplier                           */
+    const double* inflation;       /* inflation_rate (fraction)                       */
+    const double* pv_deg;          /* pv_degradation_factor                           */
+    const double* escalator;       /* elec_price_escalator                            */
+    const double* down_payment;    /* down_payment_fraction                           */
+    const double* tax_rate;        /* tax_rate                                        */
+    const double* real_discount;   /* real_discount_rate                              */
+    const double* itc_frac;        /* itc_fraction_of_capex                           */
+    const double* capex;           /* system_capex_per_kw                             */
+    const double* capex_combined;  /* system_capex_per_kw_combined                    */
+    const double* batt_capex_kwh;  /* batt_capex_per_kwh_combined                     */
+    const double* ccm;             /* cap_cost_multiplier                             */
+    const double* vor;             /* value_of_resiliency_usd                         */
+} dgen_agents;
+
+/* Outputs (device pointers).  Hourly planes may be NULL (on-device reduction
+ * mode: nothing hourly is materialised).                                     */
+typedef struct {
+    double* system_kw;             /* res.x                                           */
+    double* x_last;                /* last evaluated x (source of PV-only outputs)    */
+    double* annual_kwh;            /* annual_energy_production_kwh                    */
+    double* naep;                  /* annual / max(system_kw, 1e-9)                   */
+    double* capacity_factor;
+    double* price_per_kwh;
+    double* npv;
+    double* payback_raw;           /* Cashloan payback                                */
+    double* payback_period;        /* np.round(payback if finite else 30.1, 1)        */
+    double* first_with;            /* utility_bill_w_sys_year1                        */
+    double* first_without;         /* utility_bill_wo_sys_year1                       */
+    double* batt_kw;               /* batt_power_discharge_max_kwdc                   */
+    double* batt_kwh;              /* batt_bank_installed_capacity                    */
+    double* npv_pv_batt;           /* NPV of the PV+battery run (not in the ref row)  */
+    int32_t* nfev;                 /* PV-only objective evaluations                   */
+    int32_t* tariff_final;         /* sticky tariff state after both runs             */
+    int32_t* switched;             /* any rate switch happened (nem limit -> 1e6)     */
+    int32_t* status;               /* DGEN_ST_* bits                                  */
+    double* cash_flow;             /* [(MAXY+1)][n] cf_payback_with_expenses          */
+    double* cfev_pv;               /* [(MAXY+1)][n] cf_energy_value_pv_only           */
+    double* bill_w_pv;             /* [(MAXY+1)][n] utility_bill_w_sys_pv_only        */
+    double* bill_wo_pv;            /* [(MAXY+1)][n] utility_bill_wo_sys_pv_only       */
+    double* cfev_batt;             /* [(MAXY+1)][n] cf_energy_value_pv_batt           */
+    double* bill_w_batt;           /* [(MAXY+1)][n] utility_bill_w_sys_pv_batt        */
+    double* bill_wo_batt;          /* [(MAXY+1)][n] utility_bill_wo_sys_pv_batt       */
+    float*  baseline;              /* [8760][n] baseline_net_hourly (may be NULL)     */
+    float*  net_pvonly;            /* [8760][n] adopter_net_hourly_pvonly             */
+    float*  net_with_batt;         /* [8760][n] adopter_net_hourly_with_batt          */
+} dgen_outputs;
+
+typedef struct dgen_ctx dgen_ctx;
+
+/* Version / build info. */
+int32_t dgen_abi_version(void);
+
+/* Copy the last error message of this thread into buf (NUL-terminated). */
+int32_t dgen_last_error(char* buf, size_t n);
+
+/* Open an engine on HIP device `device` with configuration `cfg`. */
+int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out);
+int32_t dgen_close(dgen_ctx* ctx);
+
+/* Profile-table preparation (replaces the per-agent SQL fetch + scaling of
+ * elec.py:508-558, done once per table load instead of once per agent):
+ * row sums in numpy's exact pairwise order and 576 slot sums per row.        */
+int32_t dgen_prep_shapes(dgen_ctx* ctx, const float* shapes, int64_t n_rows, double* row_sum,
+                         double* row_slots, void* stream);
+int32_t dgen_prep_cfs(dgen_ctx* ctx, const int32_t* cfs, int64_t n_rows, double* row_naep,
+                      double* row_slots, void* stream);
+
+/* Workspace bytes for a batch of n agents with n_scratch mo=2 scratch slots. */
+size_t dgen_workspace_bytes(int64_t n, int64_t n_scratch);
+
+/* Size a batch: Brent over PV kW with 25-year bills + cash flow per
+ * evaluation, then one PV+battery forward run at kW*, all on device.         */
+int32_t dgen_size_agents(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
+                         const dgen_outputs* out, int64_t n, void* workspace, size_t ws_bytes,
+                         int64_t n_scratch, void* stream);
+
+/* Test entry: the device Brent on f(x) = c2 (x - x0)^2 + c1 x per lane,
+ * recording up to maxn evaluated x per lane (xs: [lane][maxn]).              */
+int32_t dgen_brent_selftest(dgen_ctx* ctx, const double* lo, const double* hi,
+                            const double* xatol, const double* c2, const double* x0,
+                            const double* c1, int64_t n, double* xs, int32_t maxn,
+                            double* xopt, int32_t* nfev, void* stream);
+
+/* Per-kernel timing of the most recent dgen_size_agents call on this context
+ * (HIP events recorded on the launch stream; milliseconds).                   */
+int32_t dgen_kernel_times(dgen_ctx* ctx, double* ms_size, double* ms_hourly, double* ms_finance);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGEN_HIP_H */

@@ -1,0 +1,113 @@
+"""Shared test helpers: golden fixtures -> product columns / oracle population."""
+from __future__ import annotations
+
+import json
+import os
+from functools import lru_cache
+
+import numpy as np
+import pandas as pd
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+
+@lru_cache(maxsize=None)
+def golden_agents():
+    with open(os.path.join(GOLDEN, "agents.json")) as f:
+        meta = json.load(f)
+    z = np.load(os.path.join(GOLDEN, "agents.npz"), allow_pickle=False)
+    arrays = {k: z[k] for k in z.files}
+    return meta, arrays
+
+
+@lru_cache(maxsize=None)
+def golden_tariffs():
+    with open(os.path.join(GOLDEN, "tariffs.json")) as f:
+        return json.load(f)
+
+
+@lru_cache(maxsize=None)
+def golden_brent():
+    with open(os.path.join(GOLDEN, "brent.json")) as f:
+        return json.load(f)
+
+
+def golden_population():
+    """PopulationBuilder over the golden agents (product host path)."""
+    from dgen_amd.columnar import PopulationBuilder
+    meta, arr = golden_agents()
+    tariffs = {name: raw for name, raw in meta["tariff_cases"]}
+    table = pd.DataFrame(meta["switch_table"])
+    b = PopulationBuilder(table)
+    ws = arr["wholesale"]
+    for i, a in enumerate(meta["agents"]):
+        s = a["inputs"]
+        b.add(load_row=s["load_row"], cf_row=s["cf_row"], sector_abbr=s["sector_abbr"],
+              state_abbr=s["state_abbr"], eia_id=s["eia_id"], tariff_dict=tariffs[s["tariff"]],
+              wholesale=ws[s["wholesale_row"]], load_kwh=s["load_kwh_per_customer_in_bin"],
+              price_mult=s["elec_price_multiplier"], econ_life=s["economic_lifetime_yrs"],
+              loan_term=s["loan_term_yrs"], inflation=s["inflation_rate"],
+              pv_deg=s["pv_degradation_factor"], escalator=s["elec_price_escalator"],
+              down_payment=s["down_payment_fraction"], tax_rate=s["tax_rate"],
+              real_discount=s["real_discount_rate"], itc_frac=s["itc_fraction_of_capex"],
+              capex=s["system_capex_per_kw"], capex_combined=s["system_capex_per_kw_combined"],
+              batt_capex_kwh=s["batt_capex_per_kwh_combined"], ccm=s["cap_cost_multiplier"],
+              vor=s["value_of_resiliency_usd"])
+    cols = b.columns()
+    return b, cols, arr["shapes"], arr["cfs"], b.wholesale.array()
+
+
+def oracle_tariffs(records):
+    from oracle import oracle as orc
+    out = []
+    for r in records:
+        t = orc.Tariff()
+        t.P, t.T, t.mo, t.unit = int(r["P"]), int(r["T"]), int(r["mo"]), int(r["unit"])
+        t.fixed = float(r["fixed"])
+        for k in range(orc.MAXT):
+            t.cap[k] = float(r["cap"][k])
+        for p in range(orc.MAXP):
+            for k in range(orc.MAXT):
+                t.buy[p][k] = float(r["buy"][p, k])
+                t.sell[p][k] = float(r["sell"][p, k])
+        for m in range(12):
+            for h in range(24):
+                t.wkday[m][h] = int(r["wkday"][m, h])
+                t.wkend[m][h] = int(r["wkend"][m, h])
+        out.append(t)
+    return out
+
+
+def oracle_population(cols, tariff_records, switches, shapes, cfs, wholesale):
+    """orc.Population mirroring product columns (same tables, same indices)."""
+    from oracle import oracle as orc
+    n = len(cols["load_kwh"])
+    sw_solar, sw_storage = [], []
+    for i in range(n):
+        for k, dst in (("solar", sw_solar), ("storage", sw_storage)):
+            off, cnt = int(cols[f"sw_{k}_off"][i]), int(cols[f"sw_{k}_cnt"][i])
+            dst.append([(float(r["min_kw"]), float(r["max_kw"]), float(r["one_time_charge"]),
+                         int(r["tariff"])) for r in switches[off:off + cnt]])
+    ocols = {
+        "load_row": cols["load_row"], "cf_row": cols["cf_row"],
+        "wholesale_row": cols["wholesale_row"], "load_kwh": cols["load_kwh"],
+        "price_mult": cols["price_mult"], "inflation": cols["inflation"], "pv_deg": cols["pv_deg"],
+        "escalator": cols["escalator"], "down_payment": cols["down_payment"],
+        "tax_rate": cols["tax_rate"], "real_discount": cols["real_discount"],
+        "itc_frac": cols["itc_frac"], "capex": cols["capex"],
+        "capex_combined": cols["capex_combined"],
+        "batt_capex_kwh_combined": cols["batt_capex_kwh"], "ccm": cols["ccm"], "vor": cols["vor"],
+        "is_res": (cols["flags"] & 1).astype(int), "is_ca": ((cols["flags"] >> 1) & 1).astype(int),
+        "econ_life": cols["econ_life"], "loan_term": cols["loan_term"], "tariff0": cols["tariff0"],
+    }
+    return orc.Population(ocols, shapes, cfs, wholesale, oracle_tariffs(tariff_records),
+                          sw_solar, sw_storage)
+
+
+def final_tariff_id(builder, agent_tariff_id, final_index, switched):
+    if switched:
+        r = builder.switches.row_of_tariff.get(int(final_index))
+        if r is not None:
+            return r["rate_id_alias"]
+    return agent_tariff_id

@@ -1,0 +1,128 @@
+"""The CPU oracle, pinned against the reference's own behaviour.
+
+* numpy summation / rounding emulation vs numpy itself;
+* the bounded-Brent replica vs scipy 1.15.3 sequences (tests/golden/brent.json);
+* the full per-agent driver vs the boundary captures produced by running the
+  reference's calc_system_size_and_performance (tests/golden/agents.*) -- these
+  must agree BIT FOR BIT, because the captures used the same SSC primitives.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from tests import helpers
+
+
+def test_np_sum_matches_numpy():
+    rng = np.random.default_rng(7)
+    for n in list(range(0, 140)) + [255, 256, 1000, 8191, 8192, 8193, 8760, 20000]:
+        for _ in range(2):
+            a = rng.standard_normal(n) * rng.uniform(1.0, 1e5)
+            assert orc.np_sum(a) == np.sum(a), n
+
+
+def test_np_sum_profiles():
+    _, arr = helpers.golden_agents()
+    for row in arr["shapes"]:
+        a = row.astype(np.float64)
+        assert orc.np_sum(a) == a.sum()
+    for row in arr["cfs"]:
+        a = np.asarray(row, dtype=float) / 1e6
+        assert orc.np_sum(a) == a.sum()
+
+
+@pytest.mark.parametrize("x", [0.05, 0.15, 0.25, 0.35, 2.45, 12.349999, 29.95, 30.1, 1e99, -0.05])
+def test_round1(x):
+    assert orc.np_round1(x) == float(np.round(x, 1))
+
+
+def test_brent_matches_scipy():
+    for c in helpers.golden_brent():
+        xs, xo, n = orc.brent_quadratic(c["low"], c["high"], c["xatol"], c["c2"], c["x0"], c["c1"])
+        assert n == c["nfev"], c
+        assert xs.tolist() == c["xs"], c
+        assert xo == c["x"], c
+
+
+def test_brent_eval_count_table():
+    """for L <~ 4.79 kW the search stops after one evaluation at
+    a + 0.3819660112501051 (b - a)."""
+    for L in (0.5, 1.0, 3.0, 4.7):
+        lo, hi = 0.8 * L, 1.25 * L
+        xs, xo, n = orc.brent_quadratic(lo, hi, 2, 1.0, L, 0.0)
+        assert n == 1
+        assert xo == lo + 0.3819660112501051 * (hi - lo)
+
+
+@pytest.fixture(scope="module")
+def oracle_run():
+    b, cols, shapes, cfs, ws = helpers.golden_population()
+    pop = helpers.oracle_population(cols, b.tariffs.array(), b.switches.array(), shapes, cfs, ws)
+    meta, arr = helpers.golden_agents()
+    res = pop.run(orc.make_cfg(**meta["cfg"]), hourly=True)
+    return b, cols, meta, arr, res
+
+
+def test_oracle_driver_scalars_bit_exact(oracle_run):
+    b, cols, meta, arr, res = oracle_run
+    for i, (g, r) in enumerate(zip(meta["agents"], res)):
+        assert r["status"] == 0, g["tag"]
+        assert r["nfev"] == len(g["evals_pv"]), g["tag"]
+        assert r["system_kw"] == g["system_kw"], g["tag"]
+        assert r["x_last"] == g["evals_pv"][-1], g["tag"]
+        for k_o, k_g in (("annual_kwh", "annual_energy_production_kwh"), ("naep", "naep"),
+                         ("capacity_factor", "capacity_factor"), ("price_per_kwh", "price_per_kwh"),
+                         ("npv", "npv"), ("payback_period", "payback_period"),
+                         ("batt_kw", "batt_kw"), ("batt_kwh", "batt_kwh")):
+            assert r[k_o] == g[k_g], (g["tag"], k_o, r[k_o], g[k_g])
+        tid = helpers.final_tariff_id(b, 900 + i, r["tariff_final"], r["switched"])
+        assert tid == g["final_tariff_id"], g["tag"]
+        nem = 1e6 if r["switched"] else 100.0
+        assert nem == g["nem_system_kw_limit"], g["tag"]
+
+
+def test_oracle_driver_arrays_bit_exact(oracle_run):
+    b, cols, meta, arr, res = oracle_run
+    pairs = (("cash_flow", "cash_flow"), ("cf_energy_value_pv_only", "cf_energy_value_pv_only"),
+             ("bill_w_pv_only", "utility_bill_w_sys_pv_only"),
+             ("bill_wo_pv_only", "utility_bill_wo_sys_pv_only"),
+             ("cf_energy_value_pv_batt", "cf_energy_value_pv_batt"),
+             ("bill_w_pv_batt", "utility_bill_w_sys_pv_batt"),
+             ("bill_wo_pv_batt", "utility_bill_wo_sys_pv_batt"))
+    for g, r in zip(meta["agents"], res):
+        for k_o, k_g in pairs:
+            assert r[k_o].tolist() == g[k_g], (g["tag"], k_o)
+
+
+def test_oracle_driver_hourly_bit_exact(oracle_run):
+    b, cols, meta, arr, res = oracle_run
+    for i, (g, r) in enumerate(zip(meta["agents"], res)):
+        for k in ("baseline_net_hourly", "adopter_net_hourly_pvonly", "adopter_net_hourly_with_batt"):
+            ref = arr[f"{i}__{k}"]
+            assert np.array_equal(r[k], ref), (g["tag"], k)
+        assert np.array_equal(arr[f"{i}__adopter_net_hourly"], arr[f"{i}__adopter_net_hourly_pvonly"])
+
+
+def test_golden_covers_edge_cases():
+    meta, _ = helpers.golden_agents()
+    tags = {a["tag"]: a for a in meta["agents"]}
+    # last-eval capture: PV-only outputs from x_last != res.x (ff:449-474)
+    assert tags["res_K1"]["evals_pv"][-1] != tags["res_K1"]["system_kw"]
+    # single-evaluation Brent for small L
+    assert len(tags["res_small"]["evals_pv"]) == 1
+    # deep searches for large commercial loads
+    assert len(tags["com_5GWh"]["evals_pv"]) >= 12
+    # sticky rate switch and storage switch happened
+    assert tags["res_sticky"]["final_tariff_id"] == "DG_201_big"
+    assert tags["res_storage_sw"]["final_tariff_id"] == "ST_203"
+    # overlapping rows never switch
+    assert tags["res_two_rows"]["nem_system_kw_limit"] == 100.0
+    # 1e99 "no payback" propagates as finite (ff:557)
+    assert tags["res_mo2_ts"]["payback_period"] == 1e99
+
+
+def test_payback_nonfinite_maps_to_30_1():
+    assert orc.np_round1(30.1) == 30.1
+    assert not math.isfinite(float("nan"))

@@ -1,0 +1,99 @@
+"""Host tariff compiler vs the reference's normalize_tariff / process_tariff
+outputs captured in tests/golden/tariffs.json (bit-exact, incl. float32
+rounding) and the SURVEY Appendix C known answers."""
+import json
+import math
+
+import numpy as np
+import pytest
+
+from dgen_amd import tariff as T
+from tests import helpers
+
+
+def _eq(a, b):
+    """Exact structural equality with NaN == NaN."""
+    if isinstance(a, float) and isinstance(b, float):
+        return (a == b) or (math.isnan(a) and math.isnan(b))
+    if isinstance(a, (list, tuple)) and isinstance(b, (list, tuple)):
+        return len(a) == len(b) and all(_eq(x, y) for x, y in zip(a, b))
+    if isinstance(a, dict) and isinstance(b, dict):
+        return a.keys() == b.keys() and all(_eq(a[k], b[k]) for k in a)
+    if isinstance(a, bool) or isinstance(b, bool):
+        return a == b and type(a) == type(b)
+    if isinstance(a, (int, float)) and isinstance(b, (int, float)):
+        return a == b
+    return a == b
+
+
+def _roundtrip(obj):
+    return json.loads(json.dumps(obj))
+
+
+@pytest.mark.parametrize("case", helpers.golden_tariffs(), ids=lambda c: c["name"])
+def test_normalize_matches_reference(case):
+    got = _roundtrip(T.normalize_tariff(case["raw"], net_sell_rate_scalar=0.0))
+    assert _eq(got, case["normalized"]), case["name"]
+
+
+@pytest.mark.parametrize("case", helpers.golden_tariffs(), ids=lambda c: c["name"])
+def test_process_matches_reference(case):
+    _, arr = helpers.golden_agents()
+    ws = arr["wholesale"][0] * 1.1
+    td = T.normalize_tariff(case["raw"], 0.0)
+    for variant, ts in (("ts_none", None), ("ts_8760", ws)):
+        got = _roundtrip(T.rate_fields(td, 0.0, ts_sell_rate=ts))
+        assert _eq(got, case["process"][variant]), (case["name"], variant)
+
+
+def test_appendix_c_known_answers():
+    g = {c["name"]: c for c in helpers.golden_tariffs()}
+    k1 = g["K1"]["normalized"]["ur_ec_tou_mat"]
+    assert k1 == [[1, 1, 9.999999680285692e+37, 0, 0.11999999731779099, 0],
+                  [2, 1, 9.999999680285692e+37, 0, 0.2800000011920929, 0]]
+    k2 = g["K2"]["normalized"]["ur_ec_tou_mat"]
+    assert k2[2][2] == 500.0           # period-2 tier-1 cap harmonised to 500
+    k3 = g["K3"]["normalized"]
+    assert all(v == 1 for row in k3["ur_ec_sched_weekday"] for v in row)   # ids > P clamp to 1
+    assert g["K5"]["normalized"]["ur_dc_enable"] == 1
+    assert g["K5"]["process"]["ts_none"]["ur_dc_enable"] == 0
+
+
+def test_record_packing_k3():
+    raw = next(c["raw"] for c in helpers.golden_tariffs() if c["name"] == "K3")
+    ct = T.compile_tariff(raw, is_ca=False)
+    r = ct.record
+    assert int(r["P"]) == 2 and int(r["T"]) == 2
+    assert (r["wkday"] == 0).all()                   # everything billed at period 1
+    assert r["cap"][0] == 300.0
+    assert r["buy"][1, 0] == np.float32(0.31)
+
+
+def test_ca_override_sell_quarter_buy():
+    raw = next(c["raw"] for c in helpers.golden_tariffs() if c["name"] == "K1")
+    ct = T.compile_tariff(raw, is_ca=True)
+    r = ct.record
+    assert int(r["mo"]) == 2
+    P, Tn = int(r["P"]), int(r["T"])
+    assert np.array_equal(r["sell"][:P, :Tn], (r["buy"][:P, :Tn] * 0.25).astype(np.float32).astype(float))
+
+
+def test_table_dedup_and_keys():
+    tt = T.TariffTable()
+    a = tt.add({"e_prices": [[0.1]]}, False)
+    b = tt.add({"e_prices": [[0.1]]}, False)
+    c = tt.add({"e_prices": [[0.1]]}, True)
+    d = tt.add({"e_prices": [[0.1]]}, False, key="switch-row:3")
+    assert a == b and c != a and d not in (a, c)
+    assert tt.array().dtype == T.TARIFF_DTYPE and len(tt) == 3
+
+
+def test_empty_tariff_flags():
+    ct = T.compile_tariff({}, is_ca=False)
+    assert int(ct.record["flags"]) & T.ST_EMPTY_EC
+
+
+def test_too_many_periods_rejected():
+    raw = {"e_prices": [[0.1] * 13], "e_wkday_12by24": [[0] * 24] * 12}
+    with pytest.raises(T.TariffError):
+        T.compile_tariff(raw, is_ca=False)
