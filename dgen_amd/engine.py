@@ -62,7 +62,7 @@ class Engine:
         torch = _torch()
         if isinstance(a, torch.Tensor):
             return a.to(device=self.dev, dtype=dtype).contiguous()
-        return torch.from_numpy(np.ascontiguousarray(a)).to(device=self.dev, dtype=dtype)
+        return torch.from_numpy(np.array(a, copy=True, order="C")).to(device=self.dev, dtype=dtype)
 
     def close(self):
         if getattr(self, "ctx", None):
