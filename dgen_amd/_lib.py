@@ -50,7 +50,7 @@ class Tables(ctypes.Structure):
         ("cfs", _vp), ("cf_naep", _vp), ("cf_slots", _vp),
         ("wholesale", _vp), ("tariffs", _vp), ("switches", _vp),
         ("n_shapes", _i64), ("n_cfs", _i64), ("n_wholesale", _i64), ("n_switches", _i64),
-        ("n_tariffs", _i32), ("pad", _i32),
+        ("n_tariffs", _i32), ("max_periods", _i32),
     ]
 
 
@@ -100,7 +100,7 @@ _LIB: Optional[ctypes.CDLL] = None
 EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
-    "dgen_kernel_times",
+    "dgen_kernel_times", "dgen_segment_sums",
 ]
 
 
@@ -141,6 +141,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.dgen_kernel_times.restype = _i32
     L.dgen_kernel_times.argtypes = [_vp, ctypes.POINTER(_f64), ctypes.POINTER(_f64),
                                     ctypes.POINTER(_f64)]
+    L.dgen_segment_sums.restype = _i32
+    L.dgen_segment_sums.argtypes = [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _vp, _i64, _vp, _vp]
     if L.dgen_abi_version() != 1:
         raise DgenError("libdgen_hip.so ABI version mismatch")
     _LIB = L

@@ -268,9 +268,18 @@ __device__ double year_bill_mo0(const dgen_tariff& t, const double* __restrict__
 // Per-thread LDS accumulators for the hourly (mo 2) bill: [k][BLOCK] layout,
 // conflict-free (each lane owns a column).
 struct LdsAcc {
-    double* base;
+    double* base;   // this lane's column of the dynamic LDS block
+    int half;       // slots per half: [0, half) imports/loads, [half, 2 half) exports/gen
     __device__ double& at(int k) const { return base[k * BLOCK]; }
+    __device__ double& hi(int k) const { return base[(half + k) * BLOCK]; }
 };
+
+// dynamic LDS: 2 * max_periods doubles per lane
+extern __shared__ double dyn_lds[];
+
+__host__ __device__ inline int lds_half(int max_periods) {
+    return (max_periods > 0 && max_periods <= MAXP) ? max_periods : MAXP;
+}
 
 // Hourly source for the net-billing year pass.
 struct HourSrc {
@@ -293,7 +302,7 @@ __device__ double year_bill_mo2(const dgen_tariff& t, const HourSrc& src, double
     double total = 0.0;
     int h = 0;
     for (int m = 0; m < 12; m++) {
-        for (int p = 0; p < MAXP; p++) { acc.at(p) = 0.0; acc.at(MAXP + p) = 0.0; }
+        for (int p = 0; p < P; p++) { acc.at(p) = 0.0; acc.hi(p) = 0.0; }
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
             for (int hod = 0; hod < 24; hod++, h++) {
@@ -310,7 +319,7 @@ __device__ double year_bill_mo2(const dgen_tariff& t, const HourSrc& src, double
                 } else {
                     double e = -dd;
                     if (src.ts) e *= (double)(float)(src.ts[h] * src.ts_mult);
-                    acc.at(MAXP + p) += e;
+                    acc.hi(p) += e;
                 }
             }
         }
@@ -321,7 +330,7 @@ __device__ double year_bill_mo2(const dgen_tariff& t, const HourSrc& src, double
             u[p] = 0.0;
             if (p < P) {
                 u[p] = acc.at(p);
-                double e = acc.at(MAXP + p);
+                double e = acc.hi(p);
                 cr += src.ts ? e : e * t.sell[p][0];
             }
         }
@@ -678,14 +687,14 @@ __host__ __device__ inline WsLayout ws_layout(void* base, int64_t n) {
 
 __global__ void __launch_bounds__(BLOCK)
 k_size(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws) {
-    __shared__ double lds[2 * MAXP * BLOCK];
     int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     WsLayout W = ws_layout(ws, n);
     SizeCtx c;
     c.T = &T; c.A = &A; c.cfg = &cfg; c.i = i; c.n = n;
     c.status = 0; c.switched = 0;
-    c.acc.base = lds + threadIdx.x;
+    c.acc.base = dyn_lds + threadIdx.x;
+    c.acc.half = lds_half(T.max_periods);
     uint8_t fl = A.flags[i];
     c.is_res = (fl & 1) != 0;
     c.is_ca = (fl & 2) != 0;
@@ -763,23 +772,75 @@ __device__ __forceinline__ void batt_size(double desired_kw, double desired_kwh,
     *power = b * (desired_kw / desired_kwh);
 }
 
-__global__ void __launch_bounds__(BLOCK)
+// Daily peak-shaving target (oracle/orc.c day_target): smallest T >= 0 with
+//   f(T) = sum_h min(max(d_h - T, 0), P) <= E,  d_h = max(load_h - pv_h, 0);
+// bisection until no breakpoint (d_h, d_h - P) is inside the bracket, then the
+// exact linear solve.  d_h is recomputed from the raw day registers.
+// An opaque copy: stops the compiler from keeping 24 hoisted products live
+// across the three per-day loops (recomputing them is cheaper than spilling).
+__device__ __forceinline__ double opaque(double x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+struct DayRaw {
+    float s[24];
+    int32_t c[24];
+};
+
+__device__ __forceinline__ double day_d(const DayRaw& r, int h, double ls, double cs6) {
+    double d = (double)r.s[h] * ls - (double)r.c[h] * cs6;
+    return d < 0.0 ? 0.0 : d;
+}
+
+__device__ __forceinline__ double day_target(const DayRaw& r, double ls, double cs6, double power, double avail,
+                             double dmax, double need0, int a_lo, int b_lo) {
+    if (need0 <= avail) return 0.0;
+    ls = opaque(ls);
+    cs6 = opaque(cs6);
+    double lo = 0.0, hi = dmax, f_hi = 0.0;
+    int a_hi = 0, b_hi = 0;
+    for (int it = 0; it < 48; it++) {
+        if (a_lo == a_hi && b_lo == b_hi) break;
+        double mid = 0.5 * (lo + hi);
+        double f = 0.0;
+        int am = 0, bm = 0;
+#pragma unroll
+        for (int h = 0; h < 24; h++) {
+            double e = day_d(r, h, ls, cs6) - mid;
+            am += e > 0.0;
+            bm += (e - power) >= 0.0;
+            if (e < 0.0) e = 0.0;
+            f += e < power ? e : power;
+        }
+        if (f <= avail) { hi = mid; f_hi = f; a_hi = am; b_hi = bm; }
+        else { lo = mid; a_lo = am; b_lo = bm; }
+    }
+    int k = a_hi - b_hi;
+    if (k <= 0) return hi;
+    double t = hi - (avail - f_hi) / (double)k;
+    if (t < lo) t = lo;
+    if (t > hi) t = hi;
+    return t;
+}
+
+__global__ void __launch_bounds__(BLOCK, 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch) {
-    __shared__ double lds[2 * MAXP * BLOCK];
     int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
     WsLayout W = ws_layout(ws, n);
-    LdsAcc acc{lds + threadIdx.x};
+    LdsAcc acc{dyn_lds + threadIdx.x, lds_half(T.max_periods)};
     const bool is_res = (A.flags[i] & 1) != 0;
     const int lr = A.load_row[i], cr = A.cf_row[i];
     const double kwh = A.load_kwh[i];
-    const double load_scale = kwh / T.shape_sum[lr];
+    const double ls = kwh / T.shape_sum[lr];                     // load = shape * ls
     const double kw_star = O.system_kw[i];
     const double x_last = O.x_last[i];
-    const double c_last = ((x_last * 1000.0) * 0.96) / 1000.0;
-    const double c_star = ((kw_star * 1000.0) * 0.96) / 1000.0;
+    // pv = cf * (c / 1e6), c = ((kW * 1000) * 0.96) / 1000   (ff:118-120)
+    const double cl6 = (((x_last * 1000.0) * 0.96) / 1000.0) / 1e6;
+    const double cs6 = (((kw_star * 1000.0) * 0.96) / 1000.0) / 1e6;
     const float* __restrict__ shp = T.shapes + (int64_t)lr * NH;
     const int32_t* __restrict__ cfp = T.cfs + (int64_t)cr * NH;
 
@@ -805,88 +866,80 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     int status = O.status[i] | t.flags;
     if (mo2 && slot < 0) status |= DGEN_ST_SCRATCH;
 
-    const double eta_in = cfg.batt_eta_in, eta_out = cfg.batt_eta_out;
+    const double eta_out = cfg.batt_eta_out;
     const double min_soc = cfg.batt_min_soc, max_soc = cfg.batt_max_soc;
+    const double inv_eta_in = 1.0 / cfg.batt_eta_in;
+    const double in_per_bank = bank > 0.0 ? cfg.batt_eta_in / bank : 0.0;
+    const double out_per_bank = bank > 0.0 ? 1.0 / (eta_out * bank) : 0.0;
     const bool has_batt = bank > 0.0;
     double soc = cfg.batt_init_soc;
     double annual = 0.0;
+    float* __restrict__ o_base = O.baseline;
+    float* __restrict__ o_pvo = O.net_pvonly;
+    float* __restrict__ o_wb = O.net_with_batt;
 
     for (int m = 0; m < 12; m++) {
-#pragma unroll
-        for (int p = 0; p < MAXP; p++) { acc.at(p) = 0.0; acc.at(MAXP + p) = 0.0; }
+        for (int p = 0; p < P; p++) { acc.at(p) = 0.0; acc.hi(p) = 0.0; }
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             const int h0 = d * 24;
             const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
-            double load[24], pv[24];
-            // 96 B of the shape row and 96 B of the cf row per day: 6 x 16 B loads each
+            DayRaw r;
+            // 96 B of the shape row and 96 B of the cf row: 6 x 16 B loads each
             const float4* s4 = reinterpret_cast<const float4*>(shp + h0);
             const int4* c4 = reinterpret_cast<const int4*>(cfp + h0);
-            double need0 = 0.0, dmax = 0.0;
 #pragma unroll
             for (int q = 0; q < 6; q++) {
                 float4 sv = s4[q];
                 int4 cv = c4[q];
-                float sa[4] = {sv.x, sv.y, sv.z, sv.w};
-                int ca[4] = {cv.x, cv.y, cv.z, cv.w};
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int hh = q * 4 + j;
-                    const int64_t h = h0 + hh;
-                    double ld = (double)sa[j] * load_scale;
-                    double g = (double)ca[j] / 1e6;
-                    double pl = g * c_last;
-                    double ps = g * c_star;
-                    load[hh] = ld;
-                    pv[hh] = ps;
-                    annual += pl;
-                    if (O.baseline) O.baseline[h * n + i] = (float)ld;
-                    if (O.net_pvonly) {
-                        double dn = ld - pl;
-                        O.net_pvonly[h * n + i] = (float)(dn > 0.0 ? dn : 0.0);
-                    }
-                    double dd = ld - ps;
-                    if (dd < 0.0) dd = 0.0;
-                    if (dd > dmax) dmax = dd;
-                    need0 += dd < power ? dd : power;
-                }
+                r.s[4 * q + 0] = sv.x; r.s[4 * q + 1] = sv.y; r.s[4 * q + 2] = sv.z; r.s[4 * q + 3] = sv.w;
+                r.c[4 * q + 0] = cv.x; r.c[4 * q + 1] = cv.y; r.c[4 * q + 2] = cv.z; r.c[4 * q + 3] = cv.w;
             }
-            // daily peak-shaving target with perfect 24 h look-ahead
+            double need0 = 0.0, dmax = 0.0;
+            int a0 = 0, b0 = 0;
+#pragma unroll
+            for (int hh = 0; hh < 24; hh++) {
+                const int64_t h = h0 + hh;
+                double ld = (double)r.s[hh] * ls;
+                double cfv = (double)r.c[hh];
+                double pl = cfv * cl6;
+                annual += pl;
+                if (o_base) o_base[h * n + i] = (float)ld;
+                if (o_pvo) {
+                    double dn = ld - pl;
+                    o_pvo[h * n + i] = (float)(dn > 0.0 ? dn : 0.0);
+                }
+                double dd = ld - cfv * cs6;
+                if (dd < 0.0) dd = 0.0;
+                if (dd > dmax) dmax = dd;
+                need0 += dd < power ? dd : power;
+                a0 += dd > 0.0;
+                b0 += (dd - power) >= 0.0;
+            }
             double target = 0.0;
             if (has_batt) {
                 double avail = (soc - min_soc) * bank * eta_out;
                 if (avail < 0.0) avail = 0.0;
-                if (need0 > avail) {
-                    double lo = 0.0, hi = dmax;
-                    for (int it = 0; it < 48; it++) {
-                        double mid = 0.5 * (lo + hi);
-                        double need = 0.0;
-#pragma unroll
-                        for (int hh = 0; hh < 24; hh++) {
-                            double dd = load[hh] - pv[hh] - mid;
-                            if (dd < 0.0) dd = 0.0;
-                            need += dd < power ? dd : power;
-                        }
-                        if (need <= avail) hi = mid; else lo = mid;
-                    }
-                    target = hi;
-                }
+                target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0);
             }
+            const double ls2 = opaque(ls), cs2 = opaque(cs6);
 #pragma unroll
             for (int hh = 0; hh < 24; hh++) {
                 const int64_t h = h0 + hh;
-                double nn = load[hh] - pv[hh];
+                double ld = (double)r.s[hh] * ls2;
+                double pv = (double)r.c[hh] * cs2;
+                double nn = ld - pv;
                 double sys, g2l;
                 if (!has_batt) {
-                    sys = pv[hh];
+                    sys = pv;
                     g2l = nn > 0.0 ? nn : 0.0;
                 } else if (nn < 0.0) {
-                    double room = (max_soc - soc) * bank / eta_in;
+                    double room = (max_soc - soc) * bank * inv_eta_in;
                     if (room < 0.0) room = 0.0;
                     double cc = -nn;
                     if (cc > power) cc = power;
                     if (cc > room) cc = room;
-                    soc = soc + cc * eta_in / bank;
-                    sys = pv[hh] - cc;
+                    soc = soc + cc * in_per_bank;
+                    sys = pv - cc;
                     g2l = 0.0;
                 } else {
                     double avail = (soc - min_soc) * bank * eta_out;
@@ -895,28 +948,25 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     if (dd < 0.0) dd = 0.0;
                     if (dd > power) dd = power;
                     if (dd > avail) dd = avail;
-                    soc = soc - dd / (eta_out * bank);
-                    sys = pv[hh] + dd;
+                    soc = soc - dd * out_per_bank;
+                    sys = pv + dd;
                     g2l = nn - dd;
                 }
-                if (O.net_with_batt) O.net_with_batt[h * n + i] = (float)g2l;
+                if (o_wb) o_wb[h * n + i] = (float)g2l;
                 if (mo2) {
                     if (scratch) scratch[h * n_scratch] = sys;    // plane [h][slot]
                 } else {
                     int p = sched[hh];
-                    acc.at(p) += load[hh];
-                    acc.at(MAXP + p) += sys;
+                    acc.at(p) += ld;
+                    acc.hi(p) += sys;
                 }
             }
         }
         if (!mo2) {
-#pragma unroll
-            for (int p = 0; p < MAXP; p++) {
-                if (p < P) {
-                    int64_t b = (int64_t)(m * MAXP + p) * n + i;
-                    W.Lb[b] = acc.at(p);
-                    W.Gb[b] = acc.at(MAXP + p);
-                }
+            for (int p = 0; p < P; p++) {
+                int64_t b = (int64_t)(m * MAXP + p) * n + i;
+                W.Lb[b] = acc.at(p);
+                W.Gb[b] = acc.hi(p);
             }
         }
     }
@@ -939,13 +989,12 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
 __global__ void __launch_bounds__(BLOCK)
 k_batt_finance(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
                int64_t n_scratch) {
-    __shared__ double lds[2 * MAXP * BLOCK];
     int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     const int st = O.status[i];
     if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH)) return;
     WsLayout W = ws_layout(ws, n);
-    LdsAcc acc{lds + threadIdx.x};
+    LdsAcc acc{dyn_lds + threadIdx.x, lds_half(T.max_periods)};
     const bool is_res = (A.flags[i] & 1) != 0;
     const bool is_ca = (A.flags[i] & 2) != 0;
     const int N = A.econ_life[i];
@@ -1024,6 +1073,36 @@ __global__ void k_brent_selftest(const double* lo, const double* hi, const doubl
         lo[i], hi[i], xatol[i], &nf, &xl);
     xopt[i] = xo;
     nfev[i] = nf;
+}
+
+// ---------------------------------------------------------------------------
+// k_segment_sums: one 256-thread block per (segment, plane)
+// ---------------------------------------------------------------------------
+template <typename V>
+__global__ void __launch_bounds__(256)
+k_segment_sums(const V* __restrict__ v1, const double* __restrict__ w1, const V* __restrict__ v2,
+               const double* __restrict__ w2, int k, int64_t n, const int64_t* __restrict__ seg_off,
+               int64_t n_seg, double* __restrict__ out) {
+    __shared__ double red[256];
+    const int64_t s = blockIdx.x;
+    const int j = blockIdx.y;
+    if (s >= n_seg || j >= k) return;
+    const int64_t lo = seg_off[s], hi = seg_off[s + 1];
+    const V* p1 = v1 + (int64_t)j * n;
+    const V* p2 = v2 ? v2 + (int64_t)j * n : nullptr;
+    double acc = 0.0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        double t = (double)p1[i] * (w1 ? w1[i] : 1.0);
+        if (p2) t += (double)p2[i] * w2[i];
+        acc += t;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[s * k + j] = red[0];
 }
 
 }  // namespace
@@ -1185,12 +1264,13 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->head = (c->head + 1) % dgen_ctx::RING;
     c->pending++;
     dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK)), block(BLOCK);
+    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK;
     HIP_TRY(hipEventRecord(c->ev[slot][0], s));
-    hipLaunchKernelGGL(k_size, grid, block, 0, s, *T, *A, *O, c->cfg, n, ws);
+    hipLaunchKernelGGL(k_size, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws);
     HIP_TRY(hipEventRecord(c->ev[slot][1], s));
-    hipLaunchKernelGGL(k_hourly_batt, grid, block, 0, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
+    hipLaunchKernelGGL(k_hourly_batt, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
     HIP_TRY(hipEventRecord(c->ev[slot][2], s));
-    hipLaunchKernelGGL(k_batt_finance, grid, block, 0, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
+    hipLaunchKernelGGL(k_batt_finance, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
     HIP_TRY(hipEventRecord(c->ev[slot][3], s));
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
@@ -1213,6 +1293,27 @@ int32_t dgen_kernel_times(dgen_ctx* c, double* ms_size, double* ms_hourly, doubl
     c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
     c->count = 0;
     return (int32_t)got;
+}
+
+int32_t dgen_segment_sums(dgen_ctx* c, const void* v1, const double* w1, const void* v2,
+                          const double* w2, int32_t values_f32, int32_t k, int64_t n,
+                          const int64_t* seg_off, int64_t n_seg, double* out, void* stream) {
+    if (!c || !v1 || !seg_off || !out || k <= 0 || n < 0 || n_seg < 0 || (v2 && !w2) ||
+        k > 65535) {
+        set_err("dgen_segment_sums: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n_seg == 0) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    dim3 grid((unsigned)n_seg, (unsigned)k), block(256);
+    if (values_f32)
+        hipLaunchKernelGGL(k_segment_sums<float>, grid, block, 0, (hipStream_t)stream,
+                           (const float*)v1, w1, (const float*)v2, w2, k, n, seg_off, n_seg, out);
+    else
+        hipLaunchKernelGGL(k_segment_sums<double>, grid, block, 0, (hipStream_t)stream,
+                           (const double*)v1, w1, (const double*)v2, w2, k, n, seg_off, n_seg, out);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
 }
 
 int32_t dgen_brent_selftest(dgen_ctx* c, const double* lo, const double* hi, const double* xatol,

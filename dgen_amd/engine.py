@@ -120,6 +120,7 @@ class Engine:
         self.tariff_records = recs
         self.tables.tariffs = _ptr(t)
         self.tables.n_tariffs = int(recs.size)
+        self.tables.max_periods = int(recs["P"].max())
 
     def set_switches(self, sw: np.ndarray):
         sw = np.ascontiguousarray(sw, dtype=SWITCH_DTYPE)
@@ -215,6 +216,35 @@ class Engine:
         cnt = _lib.check(self.lib.dgen_kernel_times(self.ctx, ctypes.byref(a), ctypes.byref(b),
                                                     ctypes.byref(c)), "dgen_kernel_times")
         return a.value, b.value, c.value, cnt
+
+    def segment_sums(self, v1, seg_off, w1=None, v2=None, w2=None):
+        """Weighted sums of k planes of n agents over contiguous segments
+        (device, deterministic order).  v1/v2: [k, n] float32/float64 device
+        tensors; seg_off: [S+1] offsets; returns a [S, k] float64 device tensor."""
+        torch = _torch()
+        if v1.dim() == 1:
+            v1 = v1.view(1, -1)
+            v2 = None if v2 is None else v2.view(1, -1)
+        k, n = v1.shape
+        f32 = v1.dtype == torch.float32
+        if v1.dtype not in (torch.float32, torch.float64) or (v2 is not None and v2.dtype != v1.dtype):
+            raise TypeError("segment_sums: values must be float32 or float64 (same dtype)")
+        so = self._to_dev(seg_off, torch.int64)
+        if so.numel() < 1 or int(so[0].item()) < 0 or int(so[-1].item()) > n or \
+                bool((so[1:] < so[:-1]).any().item()):
+            raise ValueError("segment offsets must be non-decreasing within [0, n]")
+        S = so.numel() - 1
+        out = torch.empty((S, k), dtype=torch.float64, device=self.dev)
+        f = lambda t: None if t is None else self._to_dev(t, torch.float64)
+        w1d, w2d = f(w1), f(w2)
+        keep = (v1.contiguous(), None if v2 is None else v2.contiguous(), w1d, w2d)
+        _lib.check(self.lib.dgen_segment_sums(self.ctx, _ptr(keep[0]), _ptr(w1d), _ptr(keep[1]),
+                                              _ptr(w2d), int(f32), int(k), int(n), _ptr(so), S,
+                                              _ptr(out), self.stream_handle()),
+                   "dgen_segment_sums")
+        torch.cuda.current_stream(self.dev).synchronize()
+        del keep
+        return out
 
     def brent_selftest(self, lo, hi, xatol, c2, x0, c1, maxn=64):
         torch = _torch()

@@ -116,7 +116,8 @@ typedef struct {
     const dgen_tariff* tariffs;
     const dgen_switch* switches;
     int64_t n_shapes, n_cfs, n_wholesale, n_switches;
-    int32_t n_tariffs, pad;
+    int32_t n_tariffs;
+    int32_t max_periods;           /* max P over tariffs (sizes LDS; 0 = DGEN_MAXP) */
 } dgen_tables;
 
 /* Agent batch, structure of arrays (device pointers, length n).  Column
@@ -218,6 +219,19 @@ int32_t dgen_brent_selftest(dgen_ctx* ctx, const double* lo, const double* hi,
                             const double* xatol, const double* c2, const double* x0,
                             const double* c1, int64_t n, double* xs, int32_t maxn,
                             double* xopt, int32_t* nfev, void* stream);
+
+/* Deterministic weighted segmented sums over contiguous agent ranges, for the
+ * per-(state, sector) totals and per-state 8760-h net sums that feed diffusion
+ * (replaces size_chunk's running net_sum, ff:1173-1188, and the per-state
+ * hourly export, attachment_rate_functions.py:151-206):
+ *   out[s * k + j] = sum_{i in [seg_off[s], seg_off[s+1])}
+ *                      w1[i] * v1[j * n + i] + w2[i] * v2[j * n + i]
+ * v1/v2 are k planes of n agents (plane-major, float32 or float64 by
+ * `values_f32`); v2/w2 may be NULL, w1 NULL means weight 1.  Fixed summation
+ * order (256-thread strided partials + LDS tree) => run-to-run identical.     */
+int32_t dgen_segment_sums(dgen_ctx* ctx, const void* v1, const double* w1, const void* v2,
+                          const double* w2, int32_t values_f32, int32_t k, int64_t n,
+                          const int64_t* seg_off, int64_t n_seg, double* out, void* stream);
 
 /* Per-kernel timing of the most recent dgen_size_agents call on this context
  * (HIP events recorded on the launch stream; milliseconds).                   */

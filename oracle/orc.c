@@ -355,30 +355,51 @@ void orc_batt_size(double desired_kw, double desired_kwh, double desired_v, cons
     *power_kw = bank * (desired_kw / desired_kwh);
 }
 
-/* Daily peak-shaving target with perfect 24 h look-ahead: smallest grid level T
- * such that the discharge needed to hold imports at T fits the energy stored at
- * the start of the day (48-step bisection, deterministic). */
+/* Daily peak-shaving target with perfect 24 h look-ahead: the smallest grid
+ * import level T >= 0 such that holding imports at T needs no more than the
+ * energy stored at the start of the day:
+ *     f(T) = sum_h min(max(d_h - T, 0), P) <= E,   d_h = max(load_h - pv_h, 0).
+ * f is continuous, non-increasing and piecewise linear with breakpoints at d_h
+ * and d_h - P.  Bisect [0, max d] until no breakpoint lies inside the bracket
+ * (the counts a = #{d > T} and b = #{d - P >= T} agree at both ends), then
+ * solve the linear piece exactly (slope -(a - b)).  At most 48 bisections. */
 static double day_target(const double* load, const double* pv, int h0, double power, double avail) {
     double need0 = 0.0, dmax = 0.0;
+    int a_lo = 0, b_lo = 0;
     for (int h = h0; h < h0 + 24; h++) {
         double d = load[h] - pv[h];
         if (d < 0.0) d = 0.0;
         if (d > dmax) dmax = d;
         need0 += d < power ? d : power;
+        a_lo += d > 0.0;
+        b_lo += (d - power) >= 0.0;
     }
     if (need0 <= avail) return 0.0;
-    double lo = 0.0, hi = dmax;
+    double lo = 0.0, hi = dmax, f_hi = 0.0;
+    int a_hi = 0, b_hi = 0;
     for (int it = 0; it < 48; it++) {
+        if (a_lo == a_hi && b_lo == b_hi) break;
         double mid = 0.5 * (lo + hi);
-        double need = 0.0;
+        double f = 0.0;
+        int am = 0, bm = 0;
         for (int h = h0; h < h0 + 24; h++) {
-            double d = load[h] - pv[h] - mid;
+            double d = load[h] - pv[h];
             if (d < 0.0) d = 0.0;
-            need += d < power ? d : power;
+            double e = d - mid;
+            am += e > 0.0;
+            bm += (e - power) >= 0.0;
+            if (e < 0.0) e = 0.0;
+            f += e < power ? e : power;
         }
-        if (need <= avail) hi = mid; else lo = mid;
+        if (f <= avail) { hi = mid; f_hi = f; a_hi = am; b_hi = bm; }
+        else { lo = mid; a_lo = am; b_lo = bm; }
     }
-    return hi;
+    int k = a_hi - b_hi;
+    if (k <= 0) return hi;
+    double t = hi - (avail - f_hi) / (double)k;
+    if (t < lo) t = lo;
+    if (t > hi) t = hi;
+    return t;
 }
 
 /* BTM dispatch (bdh:59-98): peak shaving with 24 h look-ahead, charge only from
@@ -387,6 +408,10 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
                        const orc_cfg* cfg, double* sysgen, double* grid_to_load) {
     double soc = cfg->batt_init_soc;
     double target = 0.0;
+    /* per-step constants (multiplications instead of divisions in the scan) */
+    const double inv_eta_in = 1.0 / cfg->batt_eta_in;
+    const double in_per_bank = bank_kwh > 0.0 ? cfg->batt_eta_in / bank_kwh : 0.0;
+    const double out_per_bank = bank_kwh > 0.0 ? 1.0 / (cfg->batt_eta_out * bank_kwh) : 0.0;
     for (int h = 0; h < ORC_NH; h++) {
         double n = load[h] - pv[h];
         if (!(bank_kwh > 0.0)) {
@@ -400,12 +425,12 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
             target = day_target(load, pv, h, power_kw, avail);
         }
         if (n < 0.0) {
-            double room = (cfg->batt_max_soc - soc) * bank_kwh / cfg->batt_eta_in;
+            double room = (cfg->batt_max_soc - soc) * bank_kwh * inv_eta_in;
             if (room < 0.0) room = 0.0;
             double c = -n;
             if (c > power_kw) c = power_kw;
             if (c > room) c = room;
-            soc = soc + c * cfg->batt_eta_in / bank_kwh;
+            soc = soc + c * in_per_bank;
             sysgen[h] = pv[h] - c;
             grid_to_load[h] = 0.0;
         } else {
@@ -415,7 +440,7 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
             if (d < 0.0) d = 0.0;
             if (d > power_kw) d = power_kw;
             if (d > avail) d = avail;
-            soc = soc - d / (cfg->batt_eta_out * bank_kwh);
+            soc = soc - d * out_per_bank;
             sysgen[h] = pv[h] + d;
             grid_to_load[h] = n - d;
         }

@@ -111,3 +111,27 @@ def final_tariff_id(builder, agent_tariff_id, final_index, switched):
         if r is not None:
             return r["rate_id_alias"]
     return agent_tariff_id
+
+
+def golden_rows():
+    """The golden agents as reference-style agent rows (pd.Series) + a
+    ProfileStore + the rate switch table, as make_golden.py built them."""
+    from dgen_amd.profiles import ProfileStore
+    meta, arr = golden_agents()
+    tariffs = {name: raw for name, raw in meta["tariff_cases"]}
+    store = ProfileStore()
+    rows = []
+    for i, a in enumerate(meta["agents"]):
+        s = dict(a["inputs"])
+        lr, cr, wr = s.pop("load_row"), s.pop("cf_row"), s.pop("wholesale_row")
+        s.pop("tag")
+        s["tariff_dict"] = tariffs[s.pop("tariff")]
+        s["agent_id"] = i
+        s["bldg_id"] = 1000 + lr
+        s["solar_re_9809_gid"] = 5000 + cr
+        s["tariff_id"] = 900 + i
+        s["wholesale_prices"] = arr["wholesale"][wr]
+        store.add_load((s["bldg_id"], s["sector_abbr"], s["state_abbr"]), arr["shapes"][lr])
+        store.add_solar((s["solar_re_9809_gid"], s["tilt"], s["azimuth"]), arr["cfs"][cr])
+        rows.append(pd.Series(s, name=i))
+    return rows, store, pd.DataFrame(meta["switch_table"])

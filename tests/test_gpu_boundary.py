@@ -1,0 +1,66 @@
+"""Drop-in boundary on the GPU: calc_system_size_and_performance / size_chunk
+with reference-style agent rows vs the golden captures of the reference's own
+function (same fields, same values within the stated tolerances)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from dgen_amd import financial_functions as ff
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+SCALARS = ["system_kw", "annual_energy_production_kwh", "naep", "capacity_factor", "price_per_kwh",
+           "npv", "batt_kw", "batt_kwh"]
+ARRAYS = ["cash_flow", "cf_energy_value_pv_only", "utility_bill_w_sys_pv_only",
+          "utility_bill_wo_sys_pv_only", "cf_energy_value_pv_batt", "utility_bill_w_sys_pv_batt",
+          "utility_bill_wo_sys_pv_batt"]
+
+
+def _check_row(out, g, i, arr, hourly=True):
+    for k in SCALARS:
+        assert np.isclose(out[k], g[k], rtol=1e-6, atol=1e-6), (g["tag"], k, out[k], g[k])
+    assert out["payback_period"] == g["payback_period"], g["tag"]
+    for k in ARRAYS:
+        assert np.allclose(out[k], g[k], rtol=1e-6, atol=1e-5), (g["tag"], k)
+    assert out["tariff_id"] == g["final_tariff_id"], g["tag"]
+    assert out["nem_system_kw_limit"] == g["nem_system_kw_limit"], g["tag"]
+    if hourly:
+        for k in ("baseline_net_hourly", "adopter_net_hourly_pvonly", "adopter_net_hourly_with_batt"):
+            ref = arr[f"{i}__{k}"]
+            assert len(out[k]) == 8760
+            assert np.allclose(out[k], ref, rtol=2e-6, atol=2e-6 * max(1.0, np.abs(ref).max())), (g["tag"], k)
+
+
+def test_calc_system_size_and_performance_single_rows():
+    rows, store, table = helpers.golden_rows()
+    meta, arr = helpers.golden_agents()
+    for i in (0, 4, 6, 9, 12):          # K1, sticky switch, storage switch, CA, 5 GWh commercial
+        out = ff.calc_system_size_and_performance(store, rows[i], None, table)
+        assert isinstance(out, pd.Series)
+        _check_row(out, meta["agents"][i], i, arr)
+        assert out["pv_per_kw_hourly"] == (np.asarray(arr["cfs"][meta["agents"][i]["inputs"]["cf_row"]],
+                                                      float) / 1e6).tolist()
+
+
+def test_size_chunk_matches_golden_and_aggregates():
+    rows, store, table = helpers.golden_rows()
+    meta, arr = helpers.golden_agents()
+    df = pd.DataFrame(rows)
+    ff._worker_conn = store
+    out, agg = ff.size_chunk(df, None, table, "simple")
+    assert list(out.index) == list(df.index)
+    assert "pv_per_kw_hourly" not in out.columns
+    for i, (aid, r) in enumerate(out.iterrows()):
+        _check_row(r, meta["agents"][i], i, arr)
+    base = sum(arr[f"{i}__baseline_net_hourly"] * 10.0 for i in range(len(rows)))
+    assert agg["n_hours"] == 8760
+    assert np.allclose(agg["net_sum_kw"], base, rtol=1e-5)
+
+
+def test_zero_load_raises_like_reference():
+    rows, store, table = helpers.golden_rows()
+    r = rows[0].copy()
+    r["load_kwh_per_customer_in_bin"] = 0.0
+    with pytest.raises(ZeroDivisionError):
+        ff.calc_system_size_and_performance(store, r, None, table)
