@@ -197,74 +197,6 @@ __global__ void k_row_slots_cf(const int32_t* __restrict__ rows, int64_t n_rows,
 // Utilityrate5 subset (semantics: DESIGN.md "SSC subset"; oracle/orc.c)
 // ---------------------------------------------------------------------------
 
-// Energy charge of one month from per-period billed kWh u[0..P): tier amounts
-// from the monthly total, each period billed its share at its own price.
-__device__ __forceinline__ double month_energy_charge(const dgen_tariff& t, int m,
-                                                      const double (&u)[MAXP]) {
-    const int P = t.P, T = t.T;
-    double U = 0.0;
-#pragma unroll
-    for (int p = 0; p < MAXP; p++)
-        if (p < P) U += u[p];
-    if (!(U > 0.0)) return 0.0;
-    double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
-    double charge = 0.0, prev = 0.0;
-    for (int k = 0; k < T; k++) {
-        double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
-        double top = U < hi ? U : hi;
-        double amt = top - prev;
-        if (amt < 0.0) amt = 0.0;
-        if (hi > prev) prev = hi;
-#pragma unroll
-        for (int p = 0; p < MAXP; p++)
-            if (p < P) charge += (u[p] / U) * amt * t.buy[p][k];
-    }
-    return charge;
-}
-
-// NEM (mo 0) bill for one year from monthly per-period net kWh:
-//   net[m][p] = L[m][p] - gscale * G[m][p], bins plane-major [bin * n + agent].
-// Per-period kWh credits roll over month to month; December true-up at the
-// year-end sell rate.  Returns the bill before the escalation factor.
-__device__ double year_bill_mo0(const dgen_tariff& t, const double* __restrict__ L,
-                                const double* __restrict__ G, int64_t stride, double gscale,
-                                double yearend_rate) {
-    const int P = t.P;
-    double credit[MAXP];
-#pragma unroll
-    for (int p = 0; p < MAXP; p++) credit[p] = 0.0;
-    double total = 0.0;
-    for (int m = 0; m < 12; m++) {
-        double u[MAXP];
-#pragma unroll
-        for (int p = 0; p < MAXP; p++) {
-            u[p] = 0.0;
-            if (p < P) {
-                int64_t b = (int64_t)(m * MAXP + p) * stride;
-                double g = G ? G[b] : 0.0;
-                double n = L[b] - gscale * g;
-                if (n >= 0.0) {
-                    double use = n < credit[p] ? n : credit[p];
-                    u[p] = n - use;
-                    credit[p] -= use;
-                } else {
-                    credit[p] += -n;
-                }
-            }
-        }
-        double bill = t.fixed + month_energy_charge(t, m, u);
-        if (m == 11) {
-            double c = 0.0;
-#pragma unroll
-            for (int p = 0; p < MAXP; p++)
-                if (p < P) c += credit[p];
-            bill -= c * yearend_rate;
-        }
-        total += bill;
-    }
-    return total;
-}
-
 // Per-thread LDS accumulators for the hourly (mo 2) bill: [k][BLOCK] layout,
 // conflict-free (each lane owns a column).
 struct LdsAcc {
@@ -279,6 +211,75 @@ extern __shared__ double dyn_lds[];
 
 __host__ __device__ inline int lds_half(int max_periods) {
     return (max_periods > 0 && max_periods <= MAXP) ? max_periods : MAXP;
+}
+
+// LDS lane layout (k = slot index, `half` = max periods of the batch):
+//   [0, half)        mo 2 imports / battery-case loads / bin build (loads)
+//   [half, 2 half)   mo 2 exports / battery-case system output / bin build (gen)
+//   [2 half, 3 half) mo 0 kWh credits
+//   [3 half, 4 half) mo 0 billed kWh of the month
+constexpr int LDS_SLOTS_PER_HALF = 4;
+
+// Energy charge of one month from per-period billed kWh u_p = acc.at(uoff + p):
+// tier amounts from the monthly total, each period billed its share at its
+// own price.
+__device__ __forceinline__ double month_energy_charge(const dgen_tariff& t, int m, const LdsAcc& acc,
+                                                      int uoff) {
+    const int P = t.P, T = t.T;
+    double U = 0.0;
+    for (int p = 0; p < P; p++) U += acc.at(uoff + p);
+    if (!(U > 0.0)) return 0.0;
+    double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
+    double charge = 0.0, prev = 0.0;
+    for (int k = 0; k < T; k++) {
+        double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
+        double top = U < hi ? U : hi;
+        double amt = top - prev;
+        if (amt < 0.0) amt = 0.0;
+        if (hi > prev) prev = hi;
+        for (int p = 0; p < P; p++) charge += (acc.at(uoff + p) / U) * amt * t.buy[p][k];
+    }
+    return charge;
+}
+
+// NEM (mo 0) bill for one year from monthly per-period net kWh:
+//   net[m][p] = L[m][p] - gscale * G[m][p], bins plane-major [bin * n + agent].
+// Per-period kWh credits roll over month to month; December true-up at the
+// year-end sell rate.  Returns the bill before the escalation factor.
+__device__ __forceinline__ double year_bill_mo0(const dgen_tariff& t, const double* __restrict__ L,
+                                                const double* __restrict__ G, int64_t stride,
+                                                double gscale, double yearend_rate,
+                                                const LdsAcc& acc) {
+    const int P = t.P;
+    const int cr = 2 * acc.half, uo = 3 * acc.half;
+    for (int p = 0; p < P; p++) acc.at(cr + p) = 0.0;
+    double total = 0.0;
+    for (int m = 0; m < 12; m++) {
+        for (int p = 0; p < P; p++) {
+            int64_t b = (int64_t)(m * MAXP + p) * stride;
+            double g = G ? G[b] : 0.0;
+            double nn = L[b] - gscale * g;
+            double credit = acc.at(cr + p);
+            double u = 0.0;
+            if (nn >= 0.0) {
+                double use = nn < credit ? nn : credit;
+                u = nn - use;
+                credit -= use;
+            } else {
+                credit += -nn;
+            }
+            acc.at(cr + p) = credit;
+            acc.at(uo + p) = u;
+        }
+        double bill = t.fixed + month_energy_charge(t, m, acc, uo);
+        if (m == 11) {
+            double cc = 0.0;
+            for (int p = 0; p < P; p++) cc += acc.at(cr + p);
+            bill -= cc * yearend_rate;
+        }
+        total += bill;
+    }
+    return total;
 }
 
 // Hourly source for the net-billing year pass.
@@ -296,7 +297,7 @@ struct HourSrc {
 // Net-billing (mo 2) bill for one year: hourly imports billed through the
 // tier/period charge, hourly exports credited at the tier-1 sell rate of the
 // hour's period or at the float32-rounded TS sell rate (ff:751-761).
-__device__ double year_bill_mo2(const dgen_tariff& t, const HourSrc& src, double s,
+__device__ __forceinline__ double year_bill_mo2(const dgen_tariff& t, const HourSrc& src, double s,
                                 bool with_gen, const LdsAcc& acc) {
     const int P = t.P;
     double total = 0.0;
@@ -323,18 +324,12 @@ __device__ double year_bill_mo2(const dgen_tariff& t, const HourSrc& src, double
                 }
             }
         }
-        double u[MAXP];
         double cr = 0.0;
-#pragma unroll
-        for (int p = 0; p < MAXP; p++) {
-            u[p] = 0.0;
-            if (p < P) {
-                u[p] = acc.at(p);
-                double e = acc.hi(p);
-                cr += src.ts ? e : e * t.sell[p][0];
-            }
+        for (int p = 0; p < P; p++) {
+            double e = acc.hi(p);
+            cr += src.ts ? e : e * t.sell[p][0];
         }
-        total += t.fixed + month_energy_charge(t, m, u) - cr;
+        total += t.fixed + month_energy_charge(t, m, acc, 0) - cr;
     }
     return total;
 }
@@ -445,31 +440,26 @@ __device__ __forceinline__ LoanParams make_loan(const dgen_agents& A, const dgen
 // ---------------------------------------------------------------------------
 // bins for the PV-only search (kW independent; rebuilt on a tariff switch)
 // ---------------------------------------------------------------------------
-__device__ void build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
-                           const double* __restrict__ gslots, double load_scale,
-                           double* __restrict__ L, double* __restrict__ G, int64_t stride) {
+__device__ __forceinline__ void build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
+                                           const double* __restrict__ gslots, double load_scale,
+                                           double* __restrict__ L, double* __restrict__ G,
+                                           int64_t stride, const LdsAcc& acc) {
+    const int P = t.P;
     for (int m = 0; m < 12; m++) {
-        double lb[MAXP], gb[MAXP];
-#pragma unroll
-        for (int p = 0; p < MAXP; p++) { lb[p] = 0.0; gb[p] = 0.0; }
+        for (int p = 0; p < P; p++) { acc.at(p) = 0.0; acc.hi(p) = 0.0; }
         for (int dt = 0; dt < 2; dt++) {
             const uint8_t* sched = dt ? t.wkend[m] : t.wkday[m];
             for (int hod = 0; hod < 24; hod++) {
-                int s = m * 48 + dt * 24 + hod;
+                int sl = m * 48 + dt * 24 + hod;
                 int p = sched[hod];
-                double lv = lslots[s], gv = gslots[s];
-#pragma unroll
-                for (int q = 0; q < MAXP; q++)
-                    if (q == p) { lb[q] += lv; gb[q] += gv; }
+                acc.at(p) += lslots[sl];
+                acc.hi(p) += gslots[sl];
             }
         }
-#pragma unroll
-        for (int p = 0; p < MAXP; p++) {
-            if (p < t.P) {
-                int64_t b = (int64_t)(m * MAXP + p) * stride;
-                L[b] = lb[p] * load_scale;
-                G[b] = gb[p];
-            }
+        for (int p = 0; p < P; p++) {
+            int64_t b = (int64_t)(m * MAXP + p) * stride;
+            L[b] = acc.at(p) * load_scale;
+            G[b] = acc.hi(p);
         }
     }
 }
@@ -478,16 +468,16 @@ __device__ void build_bins(const dgen_tariff& t, const double* __restrict__ lslo
 // k_size: PV-only bounded-Brent search, one thread per agent
 // ---------------------------------------------------------------------------
 struct SizeCtx {
-    const dgen_tables* T;
-    const dgen_agents* A;
-    const dgen_cfg* cfg;
+    const dgen_tariff* tariffs;
+    const dgen_switch* sw_rows;   // this agent's solar rate-switch candidates
+    int sw_cnt;
     int64_t i, n;
     int N;
-    bool is_res, is_ca;
+    bool is_ca;
     int tariff;
     int switched;
     int status;
-    double load_scale, kwh;
+    double load_scale, kwh, capex, ccm, yearend;
     double rate_base, sys_base;
     LoanParams lp;
     double* L;            // workspace bins [bin * n + i]
@@ -499,21 +489,27 @@ struct SizeCtx {
     const double* gslots;
 };
 
-__device__ void set_tariff(SizeCtx& c, int tix) {
-    const dgen_tariff& t = c.T->tariffs[tix];
+// Output pointers written by the final (last-x) evaluation.
+struct FinalOut {
+    double *cash_flow, *cfev, *bw, *bwo;
+    double *npv, *payback_raw, *payback_period, *first_with, *first_without, *price_per_kwh;
+};
+
+__device__ __forceinline__ void set_tariff(SizeCtx& c, int tix) {
+    const dgen_tariff& t = c.tariffs[tix];
     c.tariff = tix;
     c.status |= t.flags;
     if (t.mo == 0) {
-        build_bins(t, c.lslots, c.gslots, c.load_scale, c.L, c.G, c.n);
-        c.wo1 = year_bill_mo0(t, c.L, nullptr, c.n, 0.0, c.cfg->nm_yearend_sell_rate);
+        build_bins(t, c.lslots, c.gslots, c.load_scale, c.L, c.G, c.n, c.acc);
+        c.wo1 = year_bill_mo0(t, c.L, nullptr, c.n, 0.0, c.yearend, c.acc);
     } else {
         c.wo1 = year_bill_mo2(t, c.src, 1.0, false, c.acc);
     }
 }
 
 // apply_rate_switch (elec.py:838-863): exactly one row with min <= size < max.
-__device__ double rate_switch(SizeCtx& c, const dgen_switch* rows, int cnt, double size,
-                              int* new_tariff) {
+__device__ __forceinline__ double rate_switch(const dgen_switch* rows, int cnt, double size,
+                                              int* new_tariff) {
     int hit = -1, k = 0;
     for (int r = 0; r < cnt; r++)
         if (rows[r].min_kw <= size && rows[r].max_kw > size) { k++; hit = r; }
@@ -527,36 +523,33 @@ __device__ double rate_switch(SizeCtx& c, const dgen_switch* rows, int cnt, doub
 
 // One evaluation of calc_system_performance(kw, en_batt=False); returns -NPV.
 // With `out` set, writes the 26-long arrays and scalars of this evaluation.
-__device__ double objective(SizeCtx& c, double kw, const dgen_outputs* out) {
+__device__ __forceinline__ double objective(SizeCtx& c, double kw, const FinalOut* out) {
     double otc = 0.0;
     if (kw > 0.0) {
         int nt;
-        otc = rate_switch(c, c.T->switches + c.A->sw_solar_off[c.i], c.A->sw_solar_cnt[c.i], kw, &nt);
+        otc = rate_switch(c.sw_rows, c.sw_cnt, kw, &nt);
         if (nt >= 0) {
             c.switched = 1;
             if (nt != c.tariff) set_tariff(c, nt);
         }
     }
-    const dgen_tariff& t = c.T->tariffs[c.tariff];
+    const dgen_tariff& t = c.tariffs[c.tariff];
     double kws = ((kw * 1000.0) * 0.96) / 1000.0;       // ff:118-120 per-kW scale
-    double total = ((c.A->capex[c.i] * kw + 0.0) * c.A->ccm[c.i]) + 0.0 + otc;   // ff:263,280-282
+    double total = ((c.capex * kw + 0.0) * c.ccm) + 0.0 + otc;   // ff:263,280-282
     LoanState ls;
     loan_begin(c.lp, total, ls);
     double r = 1.0, s = 1.0, w1 = 0.0;
     const int64_t n = c.n;
     if (out) {
         out->cash_flow[c.i] = -total;
-        out->cfev_pv[c.i] = 0.0;
-        out->bill_w_pv[c.i] = 0.0;
-        out->bill_wo_pv[c.i] = 0.0;
+        out->cfev[c.i] = 0.0;
+        out->bw[c.i] = 0.0;
+        out->bwo[c.i] = 0.0;
     }
-    if (t.mo == 2) {
-        c.src.ts = (!c.is_ca && c.src.ts_mult == c.src.ts_mult) ? c.src.ts : nullptr;
-        c.src.gen_scale = kws;
-    }
+    c.src.gen_scale = kws;
     for (int y = 1; y <= c.N; y++) {
         double wb;
-        if (t.mo == 0) wb = year_bill_mo0(t, c.L, c.G, n, s * kws, c.cfg->nm_yearend_sell_rate);
+        if (t.mo == 0) wb = year_bill_mo0(t, c.L, c.G, n, s * kws, c.yearend, c.acc);
         else wb = year_bill_mo2(t, c.src, s, true, c.acc);
         double w = wb * r;
         double wo = c.wo1 * r;
@@ -565,9 +558,9 @@ __device__ double objective(SizeCtx& c, double kw, const dgen_outputs* out) {
         double pb = loan_year(c.lp, y, ev, ls);
         if (out) {
             out->cash_flow[(int64_t)y * n + c.i] = pb;
-            out->cfev_pv[(int64_t)y * n + c.i] = ev;
-            out->bill_w_pv[(int64_t)y * n + c.i] = w;
-            out->bill_wo_pv[(int64_t)y * n + c.i] = wo;
+            out->cfev[(int64_t)y * n + c.i] = ev;
+            out->bw[(int64_t)y * n + c.i] = w;
+            out->bwo[(int64_t)y * n + c.i] = wo;
         }
         r = r * c.rate_base;
         s = s * c.sys_base;
@@ -591,7 +584,7 @@ __device__ __forceinline__ double np_sign(double v) {
 
 // scipy 1.15.3 _minimize_scalar_bounded, op for op (maxfun 500).
 template <class Obj>
-__device__ double brent_bounded(Obj&& f, double x1, double x2, double xatol, int* nfev,
+__device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, double xatol, int* nfev,
                                 double* x_last) {
     const double sqrt_eps = 1.4832396974191326e-08;     // sqrt(2.2e-16)
     const double golden_mean = 0.3819660112501051;      // 0.5 * (3 - sqrt(5))
@@ -685,21 +678,27 @@ __host__ __device__ inline WsLayout ws_layout(void* base, int64_t n) {
     return w;
 }
 
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK, 3)
 k_size(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws) {
     int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     WsLayout W = ws_layout(ws, n);
     SizeCtx c;
-    c.T = &T; c.A = &A; c.cfg = &cfg; c.i = i; c.n = n;
+    c.tariffs = T.tariffs;
+    c.sw_rows = T.switches + A.sw_solar_off[i];
+    c.sw_cnt = A.sw_solar_cnt[i];
+    c.i = i; c.n = n;
     c.status = 0; c.switched = 0;
     c.acc.base = dyn_lds + threadIdx.x;
     c.acc.half = lds_half(T.max_periods);
     uint8_t fl = A.flags[i];
-    c.is_res = (fl & 1) != 0;
+    const bool is_res = (fl & 1) != 0;
     c.is_ca = (fl & 2) != 0;
     c.N = A.econ_life[i];
     c.kwh = A.load_kwh[i];
+    c.capex = A.capex[i];
+    c.ccm = A.ccm[i];
+    c.yearend = cfg.nm_yearend_sell_rate;
     int lr = A.load_row[i], cr = A.cf_row[i];
     int t0 = A.tariff0[i];
     double S = T.shape_sum[lr];
@@ -711,16 +710,15 @@ k_size(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, vo
     // ff:364-368: escalation (1 + infl + esc)^i, degradation (1 - d)^i
     c.rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
     c.sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
-    c.lp = make_loan(A, cfg, i, c.N, c.is_res);
+    c.lp = make_loan(A, cfg, i, c.N, is_res);
     c.src.shape = T.shapes + (int64_t)lr * NH;
     c.src.cf = T.cfs + (int64_t)cr * NH;
     c.src.sysgen = nullptr; c.src.sys_stride = 0;
     c.src.load_scale = c.load_scale;
     c.src.gen_scale = 0.0;
     int wr = A.wholesale_row[i];
-    c.src.ts = (wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+    c.src.ts = (!c.is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
     c.src.ts_mult = A.price_mult[i];
-    if (c.is_ca) c.src.ts = nullptr;
 
     bool bad = false;
     if (c.N < 1 || c.N > MAXY) { c.status |= DGEN_ST_YEARS; bad = true; }
@@ -744,11 +742,14 @@ k_size(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, vo
     set_tariff(c, t0);
     int nfev = 0;
     double x_last = 0.0;
-    double kw_star = brent_bounded([&](double x) { return objective(c, x, nullptr); },
-                                   low, high, xatol, &nfev, &x_last);
+    double kw_star = brent_bounded(
+        [&](double x) __attribute__((always_inline)) { return objective(c, x, nullptr); },
+        low, high, xatol, &nfev, &x_last);
     // ff:449-474: outputs of the LAST evaluation.  Re-running it is exact: the
     // sticky switch is idempotent at the same x and the state is unchanged.
-    objective(c, x_last, &O);
+    FinalOut fo{O.cash_flow, O.cfev_pv, O.bill_w_pv, O.bill_wo_pv, O.npv, O.payback_raw,
+                O.payback_period, O.first_with, O.first_without, O.price_per_kwh};
+    objective(c, x_last, &fo);
     O.system_kw[i] = kw_star;
     O.x_last[i] = x_last;
     O.nfev[i] = nfev;
@@ -788,8 +789,19 @@ struct DayRaw {
     int32_t c[24];
 };
 
+__device__ __forceinline__ float opaque_f(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ int32_t opaque_i(int32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+// load_h - pv_h clamped at 0, re-derived from the raw registers (the opaque
+// copies keep the compiler from caching 48 converted doubles across passes).
 __device__ __forceinline__ double day_d(const DayRaw& r, int h, double ls, double cs6) {
-    double d = (double)r.s[h] * ls - (double)r.c[h] * cs6;
+    double d = (double)opaque_f(r.s[h]) * ls - (double)opaque_i(r.c[h]) * cs6;
     return d < 0.0 ? 0.0 : d;
 }
 
@@ -925,8 +937,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
 #pragma unroll
             for (int hh = 0; hh < 24; hh++) {
                 const int64_t h = h0 + hh;
-                double ld = (double)r.s[hh] * ls2;
-                double pv = (double)r.c[hh] * cs2;
+                double ld = (double)opaque_f(r.s[hh]) * ls2;
+                double pv = (double)opaque_i(r.c[hh]) * cs2;
                 double nn = ld - pv;
                 double sys, g2l;
                 if (!has_batt) {
@@ -1028,7 +1040,7 @@ k_batt_finance(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64
     const double* Lb = W.Lb + i;
     const double* Gb = W.Gb + i;
 
-    double wo1 = mo2 ? year_bill_mo2(t, src, 1.0, false, acc) : year_bill_mo0(t, Lb, nullptr, n, 0.0, yr);
+    double wo1 = mo2 ? year_bill_mo2(t, src, 1.0, false, acc) : year_bill_mo0(t, Lb, nullptr, n, 0.0, yr, acc);
     LoanState ls;
     loan_begin(lp, total, ls);
     O.cfev_batt[i] = 0.0;
@@ -1036,7 +1048,7 @@ k_batt_finance(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64
     O.bill_wo_batt[i] = 0.0;
     double r = 1.0, s = 1.0;
     for (int y = 1; y <= N; y++) {
-        double wb = mo2 ? year_bill_mo2(t, src, s, true, acc) : year_bill_mo0(t, Lb, Gb, n, s, yr);
+        double wb = mo2 ? year_bill_mo2(t, src, s, true, acc) : year_bill_mo0(t, Lb, Gb, n, s, yr, acc);
         double w = wb * r;
         double wo = wo1 * r;
         double ev = (wo - w) + vor;          // ff:275: VOR added to every year
@@ -1064,7 +1076,7 @@ __global__ void k_brent_selftest(const double* lo, const double* hi, const doubl
     int nf = 0;
     double xl = 0.0;
     double xo = brent_bounded(
-        [&](double x) {
+        [&](double x) __attribute__((always_inline)) {
             if (k < maxn) rec[k] = x;
             k++;
             double d = x - b0;
@@ -1264,7 +1276,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->head = (c->head + 1) % dgen_ctx::RING;
     c->pending++;
     dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK)), block(BLOCK);
-    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK;
+    const size_t lds = sizeof(double) * LDS_SLOTS_PER_HALF * (size_t)lds_half(T->max_periods) * BLOCK;
     HIP_TRY(hipEventRecord(c->ev[slot][0], s));
     hipLaunchKernelGGL(k_size, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws);
     HIP_TRY(hipEventRecord(c->ev[slot][1], s));
