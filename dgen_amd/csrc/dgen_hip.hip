@@ -773,10 +773,12 @@ __device__ __forceinline__ void batt_size(double desired_kw, double desired_kwh,
     *power = b * (desired_kw / desired_kwh);
 }
 
-// Daily peak-shaving target (oracle/orc.c day_target): smallest T >= 0 with
-//   f(T) = sum_h min(max(d_h - T, 0), P) <= E,  d_h = max(load_h - pv_h, 0);
-// bisection until no breakpoint (d_h, d_h - P) is inside the bracket, then the
-// exact linear solve.  d_h is recomputed from the raw day registers.
+// Daily peak-shaving target (same algorithm as the oracle's day_target):
+// smallest T >= 0 with f(T) = sum_h min(max(d_h - T, 0), P) <= E,
+// d_h = max(load_h - pv_h, 0).  No saturated hour: Newton from 0 on the convex
+// water-filling function.  Otherwise bisection until no breakpoint (d_h,
+// d_h - P) is inside the bracket, then the exact linear solve.  d_h is
+// recomputed from the raw day registers.
 // An opaque copy: stops the compiler from keeping 24 hoisted products live
 // across the three per-day loops (recomputing them is cheaper than spilling).
 __device__ __forceinline__ double opaque(double x) {
@@ -810,6 +812,28 @@ __device__ __forceinline__ double day_target(const DayRaw& r, double ls, double 
     if (need0 <= avail) return 0.0;
     ls = opaque(ls);
     cs6 = opaque(cs6);
+    if (dmax <= power) {
+        // no hour saturates: convex water-filling, Newton from T = 0 (exact once
+        // the active count stops changing)
+        double t = 0.0, f = need0;
+        int a = a_lo;
+        for (int it = 0; it < 48; it++) {
+            double tn = t + (f - avail) / (double)a;
+            double fn = 0.0;
+            int an = 0;
+#pragma unroll
+            for (int h = 0; h < 24; h++) {
+                double e = day_d(r, h, ls, cs6) - tn;
+                an += e > 0.0;
+                fn += e > 0.0 ? e : 0.0;
+            }
+            t = tn;
+            if (an == a || fn <= avail || an == 0) break;
+            f = fn;
+            a = an;
+        }
+        return t;
+    }
     double lo = 0.0, hi = dmax, f_hi = 0.0;
     int a_hi = 0, b_hi = 0;
     for (int it = 0; it < 48; it++) {

@@ -360,21 +360,46 @@ void orc_batt_size(double desired_kw, double desired_kwh, double desired_v, cons
  * energy stored at the start of the day:
  *     f(T) = sum_h min(max(d_h - T, 0), P) <= E,   d_h = max(load_h - pv_h, 0).
  * f is continuous, non-increasing and piecewise linear with breakpoints at d_h
- * and d_h - P.  Bisect [0, max d] until no breakpoint lies inside the bracket
- * (the counts a = #{d > T} and b = #{d - P >= T} agree at both ends), then
- * solve the linear piece exactly (slope -(a - b)).  At most 48 bisections. */
+ * and d_h - P.  If no d_h exceeds P, f is convex and Newton from T = 0 is
+ * exact in a few steps.  Otherwise bisect [0, max d] until no breakpoint lies
+ * inside the bracket (the counts a = #{d > T} and b = #{d - P >= T} agree at
+ * both ends), then solve the linear piece exactly (slope -(a - b)). */
 static double day_target(const double* load, const double* pv, int h0, double power, double avail) {
+    double d[24];
     double need0 = 0.0, dmax = 0.0;
     int a_lo = 0, b_lo = 0;
-    for (int h = h0; h < h0 + 24; h++) {
-        double d = load[h] - pv[h];
-        if (d < 0.0) d = 0.0;
-        if (d > dmax) dmax = d;
-        need0 += d < power ? d : power;
-        a_lo += d > 0.0;
-        b_lo += (d - power) >= 0.0;
+    for (int k = 0; k < 24; k++) {
+        double v = load[h0 + k] - pv[h0 + k];
+        if (v < 0.0) v = 0.0;
+        d[k] = v;
+        if (v > dmax) dmax = v;
+        need0 += v < power ? v : power;
+        a_lo += v > 0.0;
+        b_lo += (v - power) >= 0.0;
     }
     if (need0 <= avail) return 0.0;
+    if (dmax <= power) {
+        /* no hour saturates: f(T) = sum max(d - T, 0) is convex and decreasing,
+         * so Newton from T = 0 stays left of the root and is exact once the
+         * active count stops changing. */
+        double t = 0.0, f = need0;
+        int a = a_lo;
+        for (int it = 0; it < 48; it++) {
+            double tn = t + (f - avail) / (double)a;
+            double fn = 0.0;
+            int an = 0;
+            for (int k = 0; k < 24; k++) {
+                double e = d[k] - tn;
+                an += e > 0.0;
+                fn += e > 0.0 ? e : 0.0;
+            }
+            t = tn;
+            if (an == a || fn <= avail || an == 0) break;
+            f = fn;
+            a = an;
+        }
+        return t;
+    }
     double lo = 0.0, hi = dmax, f_hi = 0.0;
     int a_hi = 0, b_hi = 0;
     for (int it = 0; it < 48; it++) {
@@ -382,10 +407,8 @@ static double day_target(const double* load, const double* pv, int h0, double po
         double mid = 0.5 * (lo + hi);
         double f = 0.0;
         int am = 0, bm = 0;
-        for (int h = h0; h < h0 + 24; h++) {
-            double d = load[h] - pv[h];
-            if (d < 0.0) d = 0.0;
-            double e = d - mid;
+        for (int k = 0; k < 24; k++) {
+            double e = d[k] - mid;
             am += e > 0.0;
             bm += (e - power) >= 0.0;
             if (e < 0.0) e = 0.0;

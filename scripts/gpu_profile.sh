@@ -14,7 +14,7 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 fi
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_trace -o run -- python3 $BENCH > gpurun_out/prof_${TAG}_trace.log 2>&1; rc=$?
 echo "trace rc=$rc"; tail -2 gpurun_out/prof_${TAG}_trace.log; stop $rc
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU"; do
+for grp in ${PMC_GROUPS:-"FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU" "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY"}; do
   name=$(echo $grp | cut -d' ' -f1)
   timeout -k 10 400 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/prof_${TAG}_pmc_$name -o run -- python3 $BENCH > gpurun_out/prof_${TAG}_pmc_$name.log 2>&1; rc=$?
   echo "pmc $grp rc=$rc"; tail -2 gpurun_out/prof_${TAG}_pmc_$name.log; stop $rc
