@@ -350,9 +350,16 @@ struct LoanState {
 };
 
 __device__ __forceinline__ double depr_frac(int type, int year, int sl) {
-    if (type == 1) {
-        const double m5[6] = {0.20, 0.32, 0.192, 0.1152, 0.1152, 0.0576};
-        return (year >= 1 && year <= 6) ? m5[year - 1] : 0.0;
+    if (type == 1) {   // MACRS 5-year half-year table (no local array: keeps it out of scratch)
+        switch (year) {
+            case 1: return 0.20;
+            case 2: return 0.32;
+            case 3: return 0.192;
+            case 4: return 0.1152;
+            case 5: return 0.1152;
+            case 6: return 0.0576;
+            default: return 0.0;
+        }
     }
     if (type == 2) return (year >= 1 && year <= sl) ? 1.0 / (double)sl : 0.0;
     return 0.0;
@@ -1086,6 +1093,521 @@ k_batt_finance(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64
     O.npv_pv_batt[i] = ls.npv_acc;
 }
 
+// ===========================================================================
+// Year-lane engine: one 64-lane wave per agent, lane = analysis year.
+// Every per-agent quantity (tariff state, Brent state, cost, bins) is
+// wave-uniform, so it lives in scalar registers / LDS; each lane owns one
+// year's bill and cash-flow line; NPV is a deterministic wave sum and the
+// payback year a wave prefix scan + ballot.
+// ===========================================================================
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ double wave_sum(double v) {
+    // fixed butterfly, then lane 0's value for every lane (wave-uniform result)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return __shfl(v, 0, WAVE);
+}
+
+__device__ __forceinline__ double wave_incl_scan(double v, int lane) {
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        double t = __shfl_up(v, o, WAVE);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ double pow_seq(double b, int e) {   // 1 * b * b ... (e times)
+    double r = 1.0;
+    for (int k = 0; k < e; k++) r = r * b;
+    return r;
+}
+
+// Per-block LDS (one wave):
+//   bins  L[12 * half], G[12 * half]         (wave-uniform, broadcast reads)
+//   lane  [4 * half][WAVE]                    (per-lane per-period state)
+struct YLds {
+    double* L;
+    double* G;
+    double* lane;   // lane column base (already offset by lane)
+    int half;
+    __device__ double& at(int k) const { return lane[k * WAVE]; }
+};
+
+__host__ __device__ inline size_t ylds_bytes(int half) {
+    return sizeof(double) * ((size_t)24 * half + (size_t)4 * half * WAVE);
+}
+
+__device__ __forceinline__ YLds ylds_make(double* base, int half, int lane) {
+    YLds y;
+    y.L = base;
+    y.G = base + 12 * half;
+    y.lane = base + 24 * half + lane;
+    y.half = half;
+    return y;
+}
+
+// month energy charge from the lane's billed kWh u_p = at(uoff + p)
+__device__ __forceinline__ double yl_month_charge(const dgen_tariff& t, int m, const YLds& S, int uoff) {
+    const int P = t.P, T = t.T;
+    double U = 0.0;
+    for (int p = 0; p < P; p++) U += S.at(uoff + p);
+    if (!(U > 0.0)) return 0.0;
+    double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
+    double charge = 0.0, prev = 0.0;
+    for (int k = 0; k < T; k++) {
+        double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
+        double top = U < hi ? U : hi;
+        double amt = top - prev;
+        if (amt < 0.0) amt = 0.0;
+        if (hi > prev) prev = hi;
+        for (int p = 0; p < P; p++) charge += (S.at(uoff + p) / U) * amt * t.buy[p][k];
+    }
+    return charge;
+}
+
+// NEM (mo 0) bill of the lane's year: net = L - gscale * G per (month, period)
+// from the LDS bins; per-period kWh credits; December true-up.
+__device__ __forceinline__ double yl_bill_mo0(const dgen_tariff& t, const YLds& S, double gscale,
+                                              double yearend) {
+    const int P = t.P, half = S.half;
+    const int cr = 0, uo = half;
+    for (int p = 0; p < P; p++) S.at(cr + p) = 0.0;
+    double total = 0.0;
+    for (int m = 0; m < 12; m++) {
+        for (int p = 0; p < P; p++) {
+            double nn = S.L[m * half + p] - gscale * S.G[m * half + p];
+            double credit = S.at(cr + p);
+            double u = 0.0;
+            if (nn >= 0.0) {
+                double use = nn < credit ? nn : credit;
+                u = nn - use;
+                credit -= use;
+            } else {
+                credit += -nn;
+            }
+            S.at(cr + p) = credit;
+            S.at(uo + p) = u;
+        }
+        double bill = t.fixed + yl_month_charge(t, m, S, uo);
+        if (m == 11) {
+            double cc = 0.0;
+            for (int p = 0; p < P; p++) cc += S.at(cr + p);
+            bill -= cc * yearend;
+        }
+        total += bill;
+    }
+    return total;
+}
+
+// Wave-uniform hourly source for net billing.
+struct YSrc {
+    const float* shape;
+    const int32_t* cf;        // PV-only (or nullptr)
+    const double* sysgen;     // battery scratch [h * stride] (or nullptr)
+    int64_t sys_stride;
+    double load_scale, gen_scale;
+    const double* ts;
+    double ts_mult;
+};
+
+// Net-billing (mo 2) bill of the lane's year (system output x s).
+__device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& src, double s,
+                                              bool with_gen, const YLds& S) {
+    const int P = t.P, half = S.half;
+    double total = 0.0;
+    int h = 0;
+    for (int m = 0; m < 12; m++) {
+        for (int p = 0; p < P; p++) { S.at(p) = 0.0; S.at(half + p) = 0.0; }
+        for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
+            const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
+            for (int hod = 0; hod < 24; hod++, h++) {
+                double load = (double)src.shape[h] * src.load_scale;
+                double g = 0.0;
+                if (with_gen) {
+                    if (src.sysgen) g = src.sysgen[(int64_t)h * src.sys_stride];
+                    else g = ((double)src.cf[h] / 1e6) * src.gen_scale;
+                }
+                double dd = load - g * s;
+                int p = sched[hod];
+                if (dd > 0.0) {
+                    S.at(p) += dd;
+                } else {
+                    double e = -dd;
+                    if (src.ts) e *= (double)(float)(src.ts[h] * src.ts_mult);
+                    S.at(half + p) += e;
+                }
+            }
+        }
+        double cr = 0.0;
+        for (int p = 0; p < P; p++) {
+            double e = S.at(half + p);
+            cr += src.ts ? e : e * t.sell[p][0];
+        }
+        total += t.fixed + yl_month_charge(t, m, S, 0) - cr;
+    }
+    return total;
+}
+
+// bins of a tariff from a row's slot sums, one (month, period) cell per lane
+__device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
+                                              const double* __restrict__ gslots, double load_scale,
+                                              const YLds& S, int lane) {
+    const int P = t.P;
+    for (int cell = lane; cell < 12 * P; cell += WAVE) {
+        int m = cell / P, p = cell % P;
+        double la = 0.0, ga = 0.0;
+        for (int dt = 0; dt < 2; dt++) {
+            const uint8_t* sched = dt ? t.wkend[m] : t.wkday[m];
+            for (int hod = 0; hod < 24; hod++) {
+                if (sched[hod] == p) {
+                    int sl = m * 48 + dt * 24 + hod;
+                    la += lslots[sl];
+                    ga += gslots[sl];
+                }
+            }
+        }
+        S.L[m * S.half + p] = la * load_scale;
+        S.G[m * S.half + p] = ga;
+    }
+    __syncthreads();
+}
+
+// Per-agent loan constants (wave-uniform) + per-lane year factors.
+struct YLoan {
+    int N, term, market, sl_years, depr_type;
+    double r_loan, loan_f, itc_pct, itc_max, ins_rate, debt_frac, fed, sta, rr;
+    // lane (year y = lane + 1) factors
+    double df;        // rr^y
+    double ins_esc;   // (1 + infl)^(y - 1)
+};
+
+__device__ __forceinline__ YLoan yl_make_loan(const dgen_agents& A, const dgen_cfg& cfg, int64_t i,
+                                              int N, bool is_res, int y) {
+    YLoan L;
+    L.N = N;
+    L.term = A.loan_term[i];
+    L.market = is_res ? 0 : 1;
+    double infl = (A.inflation[i] * 100.0) * 0.01;
+    double real = (A.real_discount[i] * 100.0) * 0.01;
+    double nom = (1.0 + real) * (1.0 + infl) - 1.0;
+    L.rr = 1.0 / (1.0 + nom);
+    double tax_pct = A.tax_rate[i] * 100.0;
+    L.fed = (tax_pct * 0.7) * 0.01;
+    L.sta = (tax_pct * 0.3) * 0.01;
+    L.r_loan = cfg.loan_rate_pct * 0.01;
+    L.loan_f = pow_seq(1.0 + L.r_loan, L.term);
+    L.itc_pct = A.itc_frac[i];                 // ff:285: the fraction passed as the percent
+    L.itc_max = cfg.itc_fed_max;
+    L.ins_rate = cfg.insurance_rate_pct * 0.01;
+    L.debt_frac = (100.0 - (A.down_payment[i] * 100.0)) * 0.01;
+    L.sl_years = cfg.depr_sl_years;
+    L.depr_type = is_res ? 0 : 2;
+    L.df = pow_seq(L.rr, y);
+    L.ins_esc = pow_seq(1.0 + infl, y - 1);
+    return L;
+}
+
+struct YFlow {
+    double npv, payback, pb;   // pb: this lane's cf_payback_with_expenses
+};
+
+// Cash flow of one lane's year + the wave reductions (Cashloan subset).
+__device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev, int y, int lane,
+                                             bool active) {
+    double debt = L.debt_frac * C;
+    double pmt = 0.0;
+    if (L.term > 0 && debt != 0.0) {
+        if (L.r_loan != 0.0) pmt = debt * L.r_loan / (1.0 - 1.0 / L.loan_f);
+        else pmt = debt / (double)L.term;
+    }
+    double itc = L.itc_pct * 0.01 * C;
+    if (itc > L.itc_max) itc = L.itc_max;
+    double basis = C - 0.5 * itc;
+    double oe = (L.ins_rate * C) * L.ins_esc;
+    // loan balance entering year y: the same recursion as a sequential pass
+    double bal = debt;
+    for (int k = 1; k < y; k++)
+        if (k <= L.term && pmt != 0.0) bal = bal - (pmt - bal * L.r_loan);
+    double interest = 0.0, payment = 0.0;
+    if (y <= L.term && pmt != 0.0) { interest = bal * L.r_loan; payment = pmt; }
+    double itc_y = (y == 1) ? itc : 0.0;
+    double sta_tax = 0.0, fed_tax = 0.0;
+    if (L.market != 0) {
+        double dep = depr_frac(L.depr_type, y, L.sl_years) * basis;
+        sta_tax = L.sta * (ev - oe - interest - dep);
+        fed_tax = L.fed * (ev - oe - interest - dep - sta_tax);
+    }
+    double taxsav = itc_y - sta_tax - fed_tax;
+    double atcf = ev - oe - payment + taxsav;
+    double pb = ev - oe + taxsav;
+    if (!active) { atcf = 0.0; pb = 0.0; }
+    YFlow f;
+    f.npv = -(C - debt) + wave_sum(atcf * L.df);
+    double cum = -C + wave_incl_scan(pb, lane);
+    unsigned long long hit = __ballot(active && cum > 0.0);
+    f.payback = 1e99;
+    if (hit) {
+        int k = __ffsll((long long)hit) - 1;              // first paying lane
+        double cum_k = __shfl(cum, k, WAVE), pb_k = __shfl(pb, k, WAVE);
+        f.payback = (pb_k != 0.0) ? (double)(k + 1) - cum_k / pb_k : (double)(k + 1) - 0.5;
+    }
+    f.pb = pb;
+    return f;
+}
+
+struct YCtx {
+    const dgen_tariff* tariffs;
+    const dgen_switch* sw_rows;
+    int sw_cnt;
+    int tariff, switched, status;
+    double capex, ccm, kwh, yearend, load_scale;
+    double r_y, s_y;      // lane factors (1 + infl + esc)^(y-1), (1 - deg)^(y-1)
+    double wo1;           // year-1 no-system bill, current tariff
+    const double* lslots;
+    const double* gslots;
+    YSrc src;
+    YLds S;
+    YLoan loan;
+    int lane, y, N;
+    bool active;
+};
+
+__device__ __forceinline__ void yl_set_tariff(YCtx& c, int tix) {
+    const dgen_tariff& t = c.tariffs[tix];
+    c.tariff = tix;
+    c.status |= t.flags;
+    if (t.mo == 0) {
+        __syncthreads();
+        yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.lane);
+        c.wo1 = yl_bill_mo0(t, c.S, 0.0, c.yearend);
+    } else {
+        c.wo1 = yl_bill_mo2(t, c.src, 1.0, false, c.S);
+    }
+}
+
+struct YOut {   // written by the final evaluation; agent-major [agent][MAXY+1]
+    double *cash_flow, *cfev, *bw, *bwo;
+};
+
+// calc_system_performance(kw, en_batt=False) with lanes = years; returns -NPV
+// (wave-uniform).  With `out`, writes the arrays of this evaluation.
+__device__ __forceinline__ double yl_objective(YCtx& c, double kw, const YOut* out, int64_t i,
+                                               double* w1_out, YFlow* flow_out) {
+    double otc = 0.0;
+    if (kw > 0.0) {
+        int nt;
+        otc = rate_switch(c.sw_rows, c.sw_cnt, kw, &nt);
+        if (nt >= 0) {
+            c.switched = 1;
+            if (nt != c.tariff) yl_set_tariff(c, nt);
+        }
+    }
+    const dgen_tariff& t = c.tariffs[c.tariff];
+    double kws = ((kw * 1000.0) * 0.96) / 1000.0;                  // ff:118-120
+    double total = ((c.capex * kw + 0.0) * c.ccm) + 0.0 + otc;     // ff:263,280-282
+    double wb;
+    if (t.mo == 0) {
+        wb = yl_bill_mo0(t, c.S, c.s_y * kws, c.yearend);
+    } else {
+        c.src.gen_scale = kws;
+        wb = yl_bill_mo2(t, c.src, c.s_y, true, c.S);
+    }
+    double w = wb * c.r_y;
+    double wo = c.wo1 * c.r_y;
+    double ev = wo - w;
+    YFlow f = yl_cashflow(c.loan, total, ev, c.y, c.lane, c.active);
+    if (out) {
+        double* base = out->cash_flow + i * (MAXY + 1);
+        if (c.lane == 0) {
+            base[0] = -total;
+            out->cfev[i * (MAXY + 1)] = 0.0;
+            out->bw[i * (MAXY + 1)] = 0.0;
+            out->bwo[i * (MAXY + 1)] = 0.0;
+        }
+        if (c.active) {
+            base[c.y] = f.pb;
+            out->cfev[i * (MAXY + 1) + c.y] = ev;
+            out->bw[i * (MAXY + 1) + c.y] = w;
+            out->bwo[i * (MAXY + 1) + c.y] = wo;
+        }
+    }
+    if (w1_out) *w1_out = __shfl(w, 0, WAVE);
+    if (flow_out) *flow_out = f;
+    return -f.npv;
+}
+
+__global__ void __launch_bounds__(WAVE)
+k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n) {
+    const int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const int lane = threadIdx.x;
+    const int half = lds_half(T.max_periods);
+    YCtx c;
+    c.lane = lane;
+    c.y = lane + 1;
+    c.S = ylds_make(dyn_lds, half, lane);
+    c.tariffs = T.tariffs;
+    c.sw_rows = T.switches + A.sw_solar_off[i];
+    c.sw_cnt = A.sw_solar_cnt[i];
+    c.status = 0;
+    c.switched = 0;
+    const uint8_t fl = A.flags[i];
+    const bool is_res = (fl & 1) != 0, is_ca = (fl & 2) != 0;
+    c.N = A.econ_life[i];
+    c.active = c.y <= c.N;
+    c.kwh = A.load_kwh[i];
+    c.capex = A.capex[i];
+    c.ccm = A.ccm[i];
+    c.yearend = cfg.nm_yearend_sell_rate;
+    const int lr = A.load_row[i], cr = A.cf_row[i];
+    const int t0 = A.tariff0[i];
+    const double naep0 = T.cf_naep[cr];
+    c.load_scale = c.kwh / T.shape_sum[lr];
+    c.lslots = T.shape_slots + (int64_t)lr * NSLOT;
+    c.gslots = T.cf_slots + (int64_t)cr * NSLOT;
+    const double rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
+    const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+    c.r_y = pow_seq(rate_base, c.y - 1);
+    c.s_y = pow_seq(sys_base, c.y - 1);
+    c.loan = yl_make_loan(A, cfg, i, c.N, is_res, c.y);
+    c.src.shape = T.shapes + (int64_t)lr * NH;
+    c.src.cf = T.cfs + (int64_t)cr * NH;
+    c.src.sysgen = nullptr;
+    c.src.sys_stride = 0;
+    c.src.load_scale = c.load_scale;
+    c.src.gen_scale = 0.0;
+    const int wr = A.wholesale_row[i];
+    c.src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+    c.src.ts_mult = A.price_mult[i];
+
+    bool bad = false;
+    if (c.N < 1 || c.N > MAXY) { c.status |= DGEN_ST_YEARS; bad = true; }
+    if (t0 < 0 || t0 >= T.n_tariffs) { c.status |= DGEN_ST_TARIFF; bad = true; }
+    const double max_load = c.kwh / naep0;                         // ff:440-444
+    const double low = max_load * 0.8, high = max_load * 1.25;
+    const double span = high - low;
+    const double tl = (span > 1.0 ? span : 1.0) * 1e-3;
+    const double fl_tl = floor(tl);
+    const double xatol = fl_tl < 2.0 ? 2.0 : fl_tl;
+    if (!isfinite(low) || !isfinite(high)) { c.status |= DGEN_ST_BOUNDS; bad = true; }
+    if (c.kwh == 0.0) c.status |= DGEN_ST_ZERO_LOAD;
+    if (bad) {
+        if (lane == 0) {
+            O.status[i] = c.status;
+            O.nfev[i] = 0;
+            O.system_kw[i] = NAN; O.x_last[i] = NAN; O.npv[i] = NAN;
+            O.tariff_final[i] = t0; O.switched[i] = 0;
+        }
+        return;
+    }
+    yl_set_tariff(c, t0);
+    int nfev = 0;
+    double x_last = 0.0;
+    double kw_star = brent_bounded(
+        [&](double x) __attribute__((always_inline)) {
+            return yl_objective(c, x, nullptr, i, nullptr, nullptr);
+        },
+        low, high, xatol, &nfev, &x_last);
+    // ff:449-474: outputs of the LAST evaluation (re-run: deterministic, and the
+    // sticky switch is idempotent at the same x)
+    YOut yo{O.cash_flow, O.cfev_pv, O.bill_w_pv, O.bill_wo_pv};
+    double w1 = 0.0;
+    YFlow f;
+    double negnpv = yl_objective(c, x_last, &yo, i, &w1, &f);
+    if (lane == 0) {
+        O.npv[i] = -negnpv;
+        O.payback_raw[i] = f.payback;
+        double pb = isfinite(f.payback) ? f.payback : 30.1;
+        O.payback_period[i] = rint(pb * 10.0) / 10.0;
+        O.first_with[i] = w1;
+        O.first_without[i] = c.wo1;
+        O.price_per_kwh[i] = c.wo1 / c.kwh;
+        O.system_kw[i] = kw_star;
+        O.x_last[i] = x_last;
+        O.nfev[i] = nfev;
+        O.tariff_final[i] = c.tariff;
+        O.switched[i] = c.switched;
+        O.status[i] = c.status;
+    }
+}
+
+// Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
+__global__ void __launch_bounds__(WAVE)
+k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
+                 int64_t n_scratch) {
+    const int64_t i = blockIdx.x;
+    if (i >= n) return;
+    const int st = O.status[i];
+    if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH)) return;
+    const int lane = threadIdx.x;
+    const int y = lane + 1;
+    const int half = lds_half(T.max_periods);
+    YLds S = ylds_make(dyn_lds, half, lane);
+    WsLayout W = ws_layout(ws, n);
+    const bool is_res = (A.flags[i] & 1) != 0;
+    const bool is_ca = (A.flags[i] & 2) != 0;
+    const int N = A.econ_life[i];
+    const bool active = y <= N;
+    const dgen_tariff& t = T.tariffs[O.tariff_final[i]];
+    const double kw = O.system_kw[i];
+    const double bank = O.batt_kwh[i];
+    const double otc = W.otc_b[i];
+    const double rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
+    const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+    const double r_y = pow_seq(rate_base, y - 1), s_y = pow_seq(sys_base, y - 1);
+    const YLoan L = yl_make_loan(A, cfg, i, N, is_res, y);
+    double system_costs = (kw > 0.0) ? A.capex_combined[i] * kw : A.capex[i] * kw;   // ff:203-216
+    double batt_costs = A.batt_capex_kwh[i] * bank * 0.7;                           // ff:219
+    double total = ((system_costs + batt_costs) * A.ccm[i]) + 0.0 + otc;
+    const double vor = A.vor[i];
+    const bool mo2 = t.mo == 2;
+    double wo1, wb;
+    if (!mo2) {
+        for (int cell = lane; cell < 12 * t.P; cell += WAVE) {
+            int m = cell / t.P, p = cell % t.P;
+            int64_t b = (int64_t)(m * MAXP + p) * n + i;
+            S.L[m * half + p] = W.Lb[b];
+            S.G[m * half + p] = W.Gb[b];
+        }
+        __syncthreads();
+        wo1 = yl_bill_mo0(t, S, 0.0, cfg.nm_yearend_sell_rate);
+        wb = yl_bill_mo0(t, S, s_y, cfg.nm_yearend_sell_rate);
+    } else {
+        YSrc src;
+        const int lr = A.load_row[i];
+        src.shape = T.shapes + (int64_t)lr * NH;
+        src.cf = nullptr;
+        src.load_scale = A.load_kwh[i] / T.shape_sum[lr];
+        src.gen_scale = 0.0;
+        src.sys_stride = n_scratch;
+        const int slot = A.scratch_slot[i];
+        src.sysgen = (slot >= 0) ? W.scratch + slot : nullptr;
+        const int wr = A.wholesale_row[i];
+        src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+        src.ts_mult = A.price_mult[i];
+        wo1 = yl_bill_mo2(t, src, 1.0, false, S);
+        wb = yl_bill_mo2(t, src, s_y, true, S);
+    }
+    double w = wb * r_y;
+    double wo = wo1 * r_y;
+    double ev = (wo - w) + vor;                                    // ff:275
+    YFlow f = yl_cashflow(L, total, ev, y, lane, active);
+    const int64_t row = i * (MAXY + 1);
+    if (lane == 0) {
+        O.cfev_batt[row] = 0.0;
+        O.bill_w_batt[row] = 0.0;
+        O.bill_wo_batt[row] = 0.0;
+        O.npv_pv_batt[i] = f.npv;
+    }
+    if (active) {
+        O.cfev_batt[row + y] = ev;
+        O.bill_w_batt[row + y] = w;
+        O.bill_wo_batt[row + y] = wo;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Brent self-test kernel (closed-form objective; tests the search alone)
 // ---------------------------------------------------------------------------
@@ -1302,11 +1824,13 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK)), block(BLOCK);
     const size_t lds = sizeof(double) * LDS_SLOTS_PER_HALF * (size_t)lds_half(T->max_periods) * BLOCK;
     HIP_TRY(hipEventRecord(c->ev[slot][0], s));
-    hipLaunchKernelGGL(k_size, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws);
+    const size_t ylds = ylds_bytes(lds_half(T->max_periods));
+    hipLaunchKernelGGL(k_size_w, dim3((unsigned)n), dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n);
     HIP_TRY(hipEventRecord(c->ev[slot][1], s));
     hipLaunchKernelGGL(k_hourly_batt, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
     HIP_TRY(hipEventRecord(c->ev[slot][2], s));
-    hipLaunchKernelGGL(k_batt_finance, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
+    hipLaunchKernelGGL(k_batt_finance_w, dim3((unsigned)n), dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n,
+                       ws, n_scratch);
     HIP_TRY(hipEventRecord(c->ev[slot][3], s));
     HIP_TRY(hipGetLastError());
     return DGEN_OK;

@@ -186,7 +186,7 @@ class Engine:
             out[name] = torch.empty(n, dtype=torch.float64 if dt == "float64" else torch.int32,
                                     device=self.dev)
         for name in _lib.OUTPUT_YEARLY:
-            out[name] = torch.zeros((_lib.MAXY + 1, n), dtype=torch.float64, device=self.dev)
+            out[name] = torch.zeros((n, _lib.MAXY + 1), dtype=torch.float64, device=self.dev)
         for name in _lib.OUTPUT_HOURLY:
             out[name] = (torch.empty((_lib.NH, n), dtype=torch.float32, device=self.dev)
                          if hourly else None)
@@ -263,12 +263,12 @@ class Engine:
 
 
 def outputs_to_host(out: Dict[str, object]) -> Dict[str, np.ndarray]:
-    """Device outputs -> host numpy (yearly planes transposed to [agent][year])."""
+    """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly)."""
     res = {}
     for name, _ in _lib.OUTPUT_SCALARS:
         res[name] = out[name].cpu().numpy()
     for name in _lib.OUTPUT_YEARLY:
-        res[name] = out[name].cpu().numpy().T.copy()
+        res[name] = out[name].cpu().numpy()
     for name in _lib.OUTPUT_HOURLY:
         t = out.get(name)
         res[name] = None if t is None else t.cpu().numpy().T.copy()

@@ -23,8 +23,9 @@
  *     (dgen_model.py:382).
  *   - Calls are stream-ordered on the given hipStream_t (NULL = default stream)
  *     and asynchronous unless stated otherwise.
- *   - Array outputs are plane-major: value (y, agent) at [y * n + agent]; hourly
- *     outputs are time-major: (hour, agent) at [hour * n + agent].
+ *   - Yearly array outputs are agent-major: value (agent, y) at
+ *     [agent * (DGEN_MAXY + 1) + y]; hourly outputs are time-major:
+ *     (hour, agent) at [hour * n + agent].
  */
 #ifndef DGEN_HIP_H
 #define DGEN_HIP_H
@@ -172,13 +173,13 @@ typedef struct {
     int32_t* tariff_final;         /* sticky tariff state after both runs             */
     int32_t* switched;             /* any rate switch happened (nem limit -> 1e6)     */
     int32_t* status;               /* DGEN_ST_* bits                                  */
-    double* cash_flow;             /* [(MAXY+1)][n] cf_payback_with_expenses          */
-    double* cfev_pv;               /* [(MAXY+1)][n] cf_energy_value_pv_only           */
-    double* bill_w_pv;             /* [(MAXY+1)][n] utility_bill_w_sys_pv_only        */
-    double* bill_wo_pv;            /* [(MAXY+1)][n] utility_bill_wo_sys_pv_only       */
-    double* cfev_batt;             /* [(MAXY+1)][n] cf_energy_value_pv_batt           */
-    double* bill_w_batt;           /* [(MAXY+1)][n] utility_bill_w_sys_pv_batt        */
-    double* bill_wo_batt;          /* [(MAXY+1)][n] utility_bill_wo_sys_pv_batt       */
+    double* cash_flow;             /* [n][MAXY+1] cf_payback_with_expenses            */
+    double* cfev_pv;               /* [n][MAXY+1] cf_energy_value_pv_only             */
+    double* bill_w_pv;             /* [n][MAXY+1] utility_bill_w_sys_pv_only          */
+    double* bill_wo_pv;            /* [n][MAXY+1] utility_bill_wo_sys_pv_only         */
+    double* cfev_batt;             /* [n][MAXY+1] cf_energy_value_pv_batt             */
+    double* bill_w_batt;           /* [n][MAXY+1] utility_bill_w_sys_pv_batt          */
+    double* bill_wo_batt;          /* [n][MAXY+1] utility_bill_wo_sys_pv_batt         */
     float*  baseline;              /* [8760][n] baseline_net_hourly (may be NULL)     */
     float*  net_pvonly;            /* [8760][n] adopter_net_hourly_pvonly             */
     float*  net_with_batt;         /* [8760][n] adopter_net_hourly_with_batt          */
