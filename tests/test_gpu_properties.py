@@ -1,0 +1,81 @@
+"""Full-size (bench workload: 1M residential agents) properties that do not
+need the oracle to finish: bracket containment, evaluation-count bound, energy
+balance of the hourly planes, sign constraints, run-to-run determinism, plus
+an oracle spot check on a random sample of the same population."""
+import numpy as np
+import pytest
+import torch
+
+from dgen_amd.synth import make_population
+from oracle import oracle as orc
+from tests import helpers
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+N = 1_000_000
+
+
+@pytest.fixture(scope="module")
+def full(engine):
+    pop = make_population("res_1m_nem_tou", N)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    out = engine.alloc_outputs(batch.n, hourly=True)
+    engine.size(batch, out)
+    torch.cuda.synchronize()
+    return pop, batch, out
+
+
+def test_status_and_bracket(full, engine):
+    pop, batch, out = full
+    st = out["status"].cpu().numpy()
+    assert (st == 0).all()
+    s_sum, naep = engine.profile_sums()
+    kwh = pop.cols["load_kwh"]
+    L = kwh / naep[pop.cols["cf_row"]]
+    kw = out["system_kw"].cpu().numpy()
+    assert (kw >= 0.8 * L - 1e-9).all() and (kw <= 1.25 * L + 1e-9).all()
+    nf = out["nfev"].cpu().numpy()
+    assert nf.min() >= 1 and nf.max() <= 16
+
+
+def test_hourly_energy_balance(full):
+    pop, batch, out = full
+    base = out["baseline"].double().sum(0).cpu().numpy()
+    assert np.allclose(base, pop.cols["load_kwh"], rtol=2e-5)
+    assert float(out["net_pvonly"].min()) >= 0.0
+    assert float(out["net_with_batt"].min()) >= 0.0
+    # the battery never raises imports above the PV-only imports
+    pv_imp = out["net_pvonly"].double().sum(0)
+    wb_imp = out["net_with_batt"].double().sum(0)
+    assert bool((wb_imp <= pv_imp * (1 + 1e-6) + 1e-3).all())
+
+
+def test_run_to_run_bit_identical(full, engine):
+    pop, batch, out = full
+    out2 = engine.alloc_outputs(batch.n, hourly=True)
+    engine.size(batch, out2)
+    torch.cuda.synchronize()
+    for k in ("system_kw", "npv", "payback_period", "batt_kwh", "cash_flow", "bill_w_batt"):
+        assert torch.equal(out[k], out2[k]), k
+    for k in ("baseline", "net_pvonly", "net_with_batt"):
+        assert torch.equal(out[k], out2[k]), k
+
+
+def test_random_sample_vs_oracle(full):
+    pop, batch, out = full
+    rng = np.random.default_rng(11)
+    idx = np.sort(rng.choice(N, 150, replace=False))
+    opop = helpers.oracle_population({k: v[idx] for k, v in pop.cols.items()}, pop.tariffs,
+                                     pop.switches, pop.shapes, pop.cfs, pop.wholesale)
+    ref = opop.run(orc.make_cfg())
+    o = {k: out[k].cpu().numpy() for k in ("system_kw", "npv", "nfev", "payback_period",
+                                           "batt_kwh", "annual_kwh")}
+    for j, r in zip(idx, ref):
+        assert o["nfev"][j] == r["nfev"]
+        assert abs(o["system_kw"][j] - r["system_kw"]) <= 1e-9 * r["system_kw"]
+        assert np.isclose(o["npv"][j], r["npv"], rtol=1e-6, atol=1e-6)
+        assert np.isclose(o["annual_kwh"][j], r["annual_kwh"], rtol=1e-9)
+        assert o["payback_period"][j] == r["payback_period"]

@@ -1,0 +1,63 @@
+"""GPU vs CPU oracle on seeded synthetic populations of every configuration
+(SURVEY 8d generator): random legacy / ur_* tariffs with tiers, NEM and net
+billing, CA NEM3, DG rate-switch rows, residential and commercial loads.
+
+Sizes are chosen so the oracle (single-thread C) finishes in seconds; the
+full-size properties run on the 1M-agent bench population in
+test_gpu_properties.py."""
+import numpy as np
+import pytest
+import torch
+
+from dgen_amd.engine import outputs_to_host
+from dgen_amd.synth import make_population
+from oracle import oracle as orc
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("res_1m_nem_tou", 600), ("ca_res_storage", 300), ("com_8m", 200), ("national_mixed", 400)]
+
+
+def _small_pop(cfg, n):
+    return make_population(cfg, n, n_res_shapes=64, n_com_shapes=32, n_cf=32, n_counties=16,
+                           n_tariffs=48)
+
+
+@pytest.mark.parametrize("cfg,n", CASES)
+def test_synthetic_population_matches_oracle(engine, cfg, n):
+    pop = _small_pop(cfg, n)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    out = engine.alloc_outputs(batch.n, hourly=True)
+    engine.size(batch, out)
+    torch.cuda.synchronize()
+    o = outputs_to_host(out)
+    opop = helpers.oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs,
+                                     pop.wholesale)
+    ref = opop.run(orc.make_cfg(), hourly=True)
+    n_switch = 0
+    for i, r in enumerate(ref):
+        assert o["status"][i] == 0 and r["status"] == 0, i
+        assert o["nfev"][i] == r["nfev"], (i, o["nfev"][i], r["nfev"])
+        assert o["tariff_final"][i] == r["tariff_final"], i
+        assert o["switched"][i] == r["switched"], i
+        n_switch += int(r["switched"])
+        assert abs(o["system_kw"][i] - r["system_kw"]) <= 1e-9 * max(1.0, r["system_kw"]), i
+        for k in ("npv", "annual_kwh", "first_with", "first_without", "batt_kwh", "batt_kw",
+                  "npv_pv_batt"):
+            assert np.isclose(o[k][i], r[k], rtol=1e-6, atol=1e-6), (i, k, o[k][i], r[k])
+        assert o["payback_period"][i] == r["payback_period"], (i, o["payback_raw"][i], r["payback_raw"])
+        N1 = 26
+        for k_o, k_r in (("cash_flow", "cash_flow"), ("cfev_pv", "cf_energy_value_pv_only"),
+                         ("bill_w_pv", "bill_w_pv_only"), ("cfev_batt", "cf_energy_value_pv_batt"),
+                         ("bill_w_batt", "bill_w_pv_batt")):
+            assert np.allclose(o[k_o][i, :N1], r[k_r], rtol=1e-6, atol=1e-5), (i, k_o)
+        for k_o, k_r in (("net_pvonly", "adopter_net_hourly_pvonly"),
+                         ("net_with_batt", "adopter_net_hourly_with_batt")):
+            ref_h = r[k_r]
+            assert np.allclose(o[k_o][i], ref_h, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(ref_h).max())), (i, k_o)
+    if cfg != "ca_res_storage":
+        assert n_switch > 0          # the population exercises the DG switch
