@@ -1663,6 +1663,79 @@ k_segment_sums(const V* __restrict__ v1, const double* __restrict__ w1, const V*
     if (threadIdx.x == 0) out[s * k + j] = red[0];
 }
 
+
+// ---------------------------------------------------------------------------
+// Diffusion step, thread per agent
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double np_maximum(double a, double b) {   // propagates NaN
+    if (a != a || b != b) return NAN;
+    return a > b ? a : b;
+}
+
+// financial_functions.calc_max_market_share (ff:1264-1310): clip payback to the
+// curve's range (NaN -> min, pandas Series.where), round to 0.1 (half-even),
+// factor = round(100 x), left-merge on (sector, factor).
+__global__ void k_max_market_share(dgen_mms_table tb, const double* __restrict__ payback,
+                                   const int32_t* __restrict__ row, int64_t n,
+                                   double* __restrict__ bounded, int64_t* __restrict__ factor,
+                                   double* __restrict__ mms) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double pb = payback[i];
+    if (!(pb >= tb.min_pb)) pb = tb.min_pb;
+    if (!(pb <= tb.max_pb)) pb = tb.max_pb;
+    double r1 = rint(pb * 10.0) / 10.0;
+    double fac = rint(r1 * 100.0);
+    bounded[i] = r1;
+    int64_t fi = (int64_t)fac;
+    factor[i] = fi;
+    int r = row[i];
+    int64_t k = fi - tb.factor_min;
+    double v = NAN;
+    if (r >= 0 && r < tb.n_rows && k >= 0 && k < tb.n_factors) v = tb.mms[(int64_t)r * tb.n_factors + k];
+    mms[i] = v;
+}
+
+// calc_equiv_time -> calc_diffusion_market_share -> bass_diffusion -> the
+// market-share floor / cap and cumulative updates of calc_diffusion_solar.
+__global__ void k_diffusion(dgen_diffusion_in in, dgen_diffusion_out out, int64_t n, int first) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double mms = in.max_market_share[i];
+    const double msly = in.market_share_last_year[i];
+    const double p = in.bass_p[i], q = in.bass_q[i];
+    const double mfix = (mms == 0.0) ? 1e-9 : mms;
+    const double ratio = (msly > mfix) ? 0.0 : msly / mfix;
+    const double teq = log((1.0 - ratio) / (1.0 + ratio * (q / p))) / (-1.0 * (p + q));
+    const double teq2 = first ? teq + in.teq_yr1[i] : teq + 2.0;
+    const double f = pow(M_E, -1.0 * (p + q) * teq2);               // np.e ** (...)
+    const double naf = (1.0 - f) / (1.0 + (q / p) * f);
+    const double bms = mms * naf;
+    const double dms = (msly > bms) ? msly : bms;
+    const double ms = np_maximum(dms, msly);
+    double nms = ms - msly;
+    if (ms > mms) nms = 0.0;
+    const double na = nms * in.developable_agent_weight[i];
+    const double skw = in.system_kw[i];
+    const double nmv = (na * skw) * in.system_capex_per_kw[i];
+    const double nskw = na * skw;
+    out.mms_fix_zeros[i] = mfix;
+    out.ratio[i] = ratio;
+    out.bass_params_teq[i] = teq;
+    out.teq2[i] = teq2;
+    out.f[i] = f;
+    out.new_adopt_fraction[i] = naf;
+    out.bass_market_share[i] = bms;
+    out.diffusion_market_share[i] = dms;
+    out.market_share[i] = ms;
+    out.new_market_share[i] = nms;
+    out.new_adopters[i] = na;
+    out.new_market_value[i] = nmv;
+    out.new_system_kw[i] = nskw;
+    out.number_of_adopters[i] = in.adopters_cum_last_year[i] + na;
+    out.market_value[i] = in.market_value_last_year[i] + nmv;
+    out.system_kw_cum[i] = in.system_kw_cum_last_year[i] + nskw;
+}
 }  // namespace
 
 // ===========================================================================
@@ -1872,6 +1945,44 @@ int32_t dgen_segment_sums(dgen_ctx* c, const void* v1, const double* w1, const v
     else
         hipLaunchKernelGGL(k_segment_sums<double>, grid, block, 0, (hipStream_t)stream,
                            (const double*)v1, w1, (const double*)v2, w2, k, n, seg_off, n_seg, out);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_max_market_share(dgen_ctx* c, const dgen_mms_table* tb, const double* payback,
+                              const int32_t* mms_row, int64_t n, double* bounded, int64_t* factor,
+                              double* mms, void* stream) {
+    if (!c || !tb || !tb->mms || !payback || !mms_row || !bounded || !factor || !mms || n < 0 ||
+        tb->n_rows < 0 || tb->n_factors < 0) {
+        set_err("dgen_max_market_share: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n == 0) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_max_market_share, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, *tb, payback, mms_row, n, bounded, factor, mms);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_diffusion(dgen_ctx* c, const dgen_diffusion_in* in, const dgen_diffusion_out* out,
+                       int64_t n, int32_t is_first_year, void* stream) {
+    if (!c || !in || !out || n < 0) { set_err("dgen_diffusion: bad argument"); return DGEN_E_ARG; }
+    const void* req[] = {in->max_market_share, in->market_share_last_year, in->bass_p, in->bass_q,
+                         in->teq_yr1, in->developable_agent_weight, in->system_kw,
+                         in->system_capex_per_kw, in->adopters_cum_last_year,
+                         in->market_value_last_year, in->system_kw_cum_last_year,
+                         out->mms_fix_zeros, out->ratio, out->bass_params_teq, out->teq2, out->f,
+                         out->new_adopt_fraction, out->bass_market_share,
+                         out->diffusion_market_share, out->market_share, out->new_market_share,
+                         out->new_adopters, out->new_market_value, out->new_system_kw,
+                         out->number_of_adopters, out->market_value, out->system_kw_cum};
+    for (const void* p : req)
+        if (!p) { set_err("dgen_diffusion: missing column"); return DGEN_E_ARG; }
+    if (n == 0) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_diffusion, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, *in, *out, n, (int)is_first_year);
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
 }

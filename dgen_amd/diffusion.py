@@ -1,0 +1,185 @@
+"""Diffusion step on the device: drop-ins for
+
+    financial_functions.calc_max_market_share(dataframe, max_market_share_df)   ff:1264-1310
+    diffusion_functions_elec.calc_diffusion_solar(df, is_first_year, bass_params, year, ...)
+                                                                                 diffusion_functions_elec.py:24-156
+
+The pandas merges that attach per-(state, sector) Bass parameters and the curve
+keys stay on the host, exactly as the reference writes them; the per-agent
+arithmetic (payback clip / round / curve lookup, equivalent time, Bass step,
+market-share floor and cap, cumulative updates) runs in k_max_market_share /
+k_diffusion through the C-ABI.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Tuple
+
+import numpy as np
+import pandas as pd
+
+from . import _lib
+
+ANCHOR_YEARS = (2014, 2016, 2018)
+
+_LAST_YEAR_COLS = ['agent_id', 'market_share', 'max_market_share', 'number_of_adopters',
+                   'market_value', 'initial_number_of_adopters', 'initial_pv_kw', 'initial_batt_kw',
+                   'initial_batt_kwh', 'initial_market_share', 'initial_market_value',
+                   'system_kw_cum', 'new_system_kw', 'batt_kw_cum', 'new_batt_kw', 'batt_kwh_cum',
+                   'new_batt_kwh']
+_LAST_YEAR_RENAME = {'market_share': 'market_share_last_year',
+                     'max_market_share': 'max_market_share_last_year',
+                     'number_of_adopters': 'adopters_cum_last_year',
+                     'market_value': 'market_value_last_year',
+                     'system_kw_cum': 'system_kw_cum_last_year',
+                     'batt_kw_cum': 'batt_kw_cum_last_year',
+                     'batt_kwh_cum': 'batt_kwh_cum_last_year'}
+DIFF_IN = ["max_market_share", "market_share_last_year", "bass_p", "bass_q", "teq_yr1",
+           "developable_agent_weight", "system_kw", "system_capex_per_kw", "adopters_cum_last_year",
+           "market_value_last_year", "system_kw_cum_last_year"]
+DIFF_OUT = ["mms_fix_zeros", "ratio", "bass_params_teq", "teq2", "f", "new_adopt_fraction",
+            "bass_market_share", "diffusion_market_share", "market_share", "new_market_share",
+            "new_adopters", "new_market_value", "new_system_kw", "number_of_adopters",
+            "market_value", "system_kw_cum"]
+
+
+class MmsTable(ctypes.Structure):
+    _fields_ = [("mms", ctypes.c_void_p), ("n_rows", ctypes.c_int32), ("n_factors", ctypes.c_int32),
+                ("factor_min", ctypes.c_int32), ("pad", ctypes.c_int32), ("min_pb", ctypes.c_double),
+                ("max_pb", ctypes.c_double)]
+
+
+class DiffIn(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in DIFF_IN]
+
+
+class DiffOut(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in DIFF_OUT]
+
+
+def _bind(L):
+    if getattr(L, "_dgen_diff_bound", False):
+        return L
+    L.dgen_max_market_share.restype = ctypes.c_int32
+    L.dgen_max_market_share.argtypes = [ctypes.c_void_p, ctypes.POINTER(MmsTable), ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.dgen_diffusion.restype = ctypes.c_int32
+    L.dgen_diffusion.argtypes = [ctypes.c_void_p, ctypes.POINTER(DiffIn), ctypes.POINTER(DiffOut),
+                                 ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
+    L._dgen_diff_bound = True
+    return L
+
+
+def mms_table(max_market_share_df: pd.DataFrame):
+    """Dense (sector -> row) x (factor) table of the rows the reference's merge
+    can hit: metric 'payback_period', business_model 'host_owned' (ff:1299-1307).
+    Returns (table [rows, F], {sector: row}, factor_min, min_pb, max_pb)."""
+    pb_rows = max_market_share_df.loc[max_market_share_df.metric == 'payback_period', 'payback_period']
+    max_pb, min_pb = float(pb_rows.max()), float(pb_rows.min())
+    sub = max_market_share_df[(max_market_share_df['metric'] == 'payback_period') &
+                              (max_market_share_df['business_model'] == 'host_owned')].copy()
+    fac = (sub['payback_period'] * 100).round()
+    fac = fac.replace([np.inf, -np.inf], np.nan)
+    sub = sub.assign(_f=fac).dropna(subset=['_f'])
+    if sub.duplicated(subset=['sector_abbr', '_f']).any():
+        raise NotImplementedError("duplicate (sector, payback) curve points: the reference's merge "
+                                  "would duplicate agent rows")
+    sectors = list(dict.fromkeys(sub['sector_abbr'].tolist()))
+    rows = {s: k for k, s in enumerate(sectors)}
+    if len(sub):
+        fmin, fmax = int(sub['_f'].min()), int(sub['_f'].max())
+    else:
+        fmin, fmax = 0, -1
+    F = fmax - fmin + 1
+    tab = np.full((max(len(sectors), 1), max(F, 1)), np.nan)
+    for s, f, v in zip(sub['sector_abbr'], sub['_f'].astype(np.int64), sub['max_market_share']):
+        tab[rows[s], int(f) - fmin] = float(v)
+    return tab, rows, fmin, min_pb, max_pb
+
+
+def _dev(engine, a, dtype):
+    return engine._to_dev(np.asarray(a), dtype)
+
+
+def calc_max_market_share(dataframe: pd.DataFrame, max_market_share_df: pd.DataFrame,
+                          engine=None) -> pd.DataFrame:
+    """ff:1264 -- attach max_market_share by (sector_abbr, payback factor)."""
+    import torch
+    from .financial_functions import get_engine
+    eng = engine or get_engine()
+    L = _bind(eng.lib)
+    in_cols = list(dataframe.columns)
+    df = dataframe.reset_index()
+    df['business_model'] = 'host_owned'
+    df['metric'] = 'payback_period'
+    tab, rows, fmin, min_pb, max_pb = mms_table(max_market_share_df)
+    n = len(df)
+    row = np.array([rows.get(s, -1) for s in df['sector_abbr']], dtype=np.int32)
+    pb = df['payback_period'].to_numpy(dtype=np.float64)
+    t_tab = _dev(eng, tab, torch.float64)
+    t_pb, t_row = _dev(eng, pb, torch.float64), _dev(eng, row, torch.int32)
+    b = torch.empty(n, dtype=torch.float64, device=eng.dev)
+    fct = torch.empty(n, dtype=torch.int64, device=eng.dev)
+    mms = torch.empty(n, dtype=torch.float64, device=eng.dev)
+    tb = MmsTable(mms=t_tab.data_ptr(), n_rows=tab.shape[0], n_factors=tab.shape[1],
+                  factor_min=fmin, pad=0, min_pb=min_pb, max_pb=max_pb)
+    _lib.check(L.dgen_max_market_share(eng.ctx, ctypes.byref(tb), t_pb.data_ptr(), t_row.data_ptr(),
+                                       n, b.data_ptr(), fct.data_ptr(), mms.data_ptr(),
+                                       eng.stream_handle()), "dgen_max_market_share")
+    torch.cuda.synchronize(eng.dev)
+    df['payback_period_bounded'] = b.cpu().numpy()
+    df['payback_period_as_factor'] = pd.array(fct.cpu().numpy(), dtype='Int64')
+    df['max_market_share'] = mms.cpu().numpy()
+    return df[in_cols + ['max_market_share', 'metric']]
+
+
+def diffusion_arrays(engine, cols: Dict[str, np.ndarray], is_first_year: bool) -> Dict[str, np.ndarray]:
+    """Run k_diffusion on host columns (DIFF_IN names) -> DIFF_OUT arrays."""
+    import torch
+    L = _bind(engine.lib)
+    n = len(cols["system_kw"])
+    keep = {k: _dev(engine, np.asarray(cols[k], dtype=np.float64), torch.float64) for k in DIFF_IN}
+    outs = {k: torch.empty(n, dtype=torch.float64, device=engine.dev) for k in DIFF_OUT}
+    din = DiffIn(**{k: keep[k].data_ptr() for k in DIFF_IN})
+    dout = DiffOut(**{k: outs[k].data_ptr() for k in DIFF_OUT})
+    _lib.check(L.dgen_diffusion(engine.ctx, ctypes.byref(din), ctypes.byref(dout), n,
+                                int(bool(is_first_year)), engine.stream_handle()), "dgen_diffusion")
+    torch.cuda.synchronize(engine.dev)
+    return {k: v.cpu().numpy() for k, v in outs.items()}
+
+
+def calc_diffusion_solar(df, is_first_year, bass_params, year, override_p_value=None,
+                         override_q_value=None, override_teq_yr1_value=None, engine=None):
+    """diffusion_functions_elec.py:24 -- PV Bass diffusion for the solve year.
+    (The reference accepts but does not apply the override_* arguments.)"""
+    from .financial_functions import get_engine
+    if year in ANCHOR_YEARS:
+        raise NotImplementedError("historical anchoring years (2014/2016/2018) read "
+                                  "config.OBSERVED_DEPLOYMENT_BY_STATE; model years start in 2026")
+    eng = engine or get_engine()
+    df = df.reset_index()
+    bass_params = bass_params[bass_params['tech'] == 'solar']
+    df = pd.merge(df, bass_params[['state_abbr', 'bass_param_p', 'bass_param_q', 'teq_yr1',
+                                   'sector_abbr']], how='left', on=['state_abbr', 'sector_abbr'])
+    cols = {"max_market_share": df['max_market_share'], "market_share_last_year": df['market_share_last_year'],
+            "bass_p": df['bass_param_p'], "bass_q": df['bass_param_q'], "teq_yr1": df['teq_yr1'],
+            "developable_agent_weight": df['developable_agent_weight'], "system_kw": df['system_kw'],
+            "system_capex_per_kw": df['system_capex_per_kw'],
+            "adopters_cum_last_year": df['adopters_cum_last_year'],
+            "market_value_last_year": df['market_value_last_year'],
+            "system_kw_cum_last_year": df['system_kw_cum_last_year']}
+    o = diffusion_arrays(eng, {k: v.to_numpy(dtype=np.float64) for k, v in cols.items()}, is_first_year)
+    for k in ("mms_fix_zeros", "ratio", "bass_params_teq", "teq2", "f", "new_adopt_fraction",
+              "bass_market_share", "diffusion_market_share", "market_share", "new_market_share",
+              "new_adopters", "new_market_value", "new_system_kw"):
+        df[k] = o[k]
+    df['new_batt_kw'] = 0.0
+    df['new_batt_kwh'] = 0.0
+    df['number_of_adopters'] = o['number_of_adopters']
+    df['market_value'] = o['market_value']
+    df['system_kw_cum'] = o['system_kw_cum']
+    df['batt_kw_cum'] = df['batt_kw_cum_last_year']
+    df['batt_kwh_cum'] = df['batt_kwh_cum_last_year']
+    market_last_year = df[_LAST_YEAR_COLS].rename(columns=_LAST_YEAR_RENAME)
+    return df, market_last_year

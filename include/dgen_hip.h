@@ -234,6 +234,57 @@ int32_t dgen_segment_sums(dgen_ctx* ctx, const void* v1, const double* w1, const
                           const double* w2, int32_t values_f32, int32_t k, int64_t n,
                           const int64_t* seg_off, int64_t n_seg, double* out, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Diffusion step: the per-agent arithmetic of
+ *   financial_functions.calc_max_market_share      ff:1264-1310 (payback -> max market share)
+ *   diffusion_functions_elec.calc_diffusion_solar   diffusion_functions_elec.py:24-156
+ *     (calc_equiv_time :343-372, calc_diffusion_market_share :251-292,
+ *      bass_diffusion :323-338).
+ * The pandas merges (bass p/q/teq_yr1 by state x sector, table keys) stay on
+ * the host; every per-agent number is computed here.
+ * ---------------------------------------------------------------------- */
+
+/* max_market_curves_to_model (metric 'payback_period', business model
+ * 'host_owned') as a dense table: value(row, factor) at
+ * mms[row * n_factors + (factor - factor_min)], factor = round(100 * payback)
+ * on the 0.1-year grid; NaN = no curve point (left-merge miss).              */
+typedef struct {
+    const double* mms;
+    int32_t n_rows, n_factors, factor_min, pad;
+    double min_pb, max_pb;          /* clip range (min / max over the curve)    */
+} dgen_mms_table;
+
+/* payback_period_bounded, payback_period_as_factor, max_market_share.
+ * mms_row: curve row of the agent's sector (-1: no curve -> NaN).            */
+int32_t dgen_max_market_share(dgen_ctx* ctx, const dgen_mms_table* table, const double* payback,
+                              const int32_t* mms_row, int64_t n, double* payback_bounded,
+                              int64_t* factor, double* max_market_share, void* stream);
+
+typedef struct {
+    const double* max_market_share;
+    const double* market_share_last_year;
+    const double* bass_p;
+    const double* bass_q;
+    const double* teq_yr1;
+    const double* developable_agent_weight;
+    const double* system_kw;
+    const double* system_capex_per_kw;
+    const double* adopters_cum_last_year;
+    const double* market_value_last_year;
+    const double* system_kw_cum_last_year;
+} dgen_diffusion_in;
+
+typedef struct {
+    double *mms_fix_zeros, *ratio, *bass_params_teq, *teq2, *f, *new_adopt_fraction;
+    double *bass_market_share, *diffusion_market_share, *market_share, *new_market_share;
+    double *new_adopters, *new_market_value, *new_system_kw, *number_of_adopters;
+    double *market_value, *system_kw_cum;
+} dgen_diffusion_out;
+
+/* One Bass diffusion step for every agent (is_first_year selects teq_yr1). */
+int32_t dgen_diffusion(dgen_ctx* ctx, const dgen_diffusion_in* in, const dgen_diffusion_out* out,
+                       int64_t n, int32_t is_first_year, void* stream);
+
 /* Per-kernel timing of the most recent dgen_size_agents call on this context
  * (HIP events recorded on the launch stream; milliseconds).                   */
 int32_t dgen_kernel_times(dgen_ctx* ctx, double* ms_size, double* ms_hourly, double* ms_finance);

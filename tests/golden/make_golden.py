@@ -528,6 +528,77 @@ def run_agents(ff, elec, shapes, cfs, ws, tariffs):
     return recs, hourly, rst
 
 
+# ----------------------------------------------------------------------------
+# diffusion
+# ----------------------------------------------------------------------------
+MMS_CSV = "/root/reference/dgen_os/data_share/NREL_max_market_share.csv"
+
+
+def diffusion_inputs(rng, n=1500):
+    """Synthetic agent frame + max-market-share curves + Bass parameters."""
+    raw = pd.read_csv(MMS_CSV)
+    cur = raw[(raw.metric == "payback_period") & (raw.business_model == "host_owned_retrofit")]
+    rows = []
+    for sec, scale in (("res", 1.0), ("com", 0.8), ("ind", 0.6)):
+        for pb, v in zip(cur.metric_value, cur.max_market_share):
+            rows.append((float(pb), sec, float(v) * scale, "payback_period", "NREL", "host_owned"))
+        rows.append((30.1, sec, 0.0, "payback_period", "NREL", "host_owned"))   # SQL union row
+        rows.append((5.0, sec, 0.5, "payback_period", "NREL", "tpo"))           # filtered by the merge
+    for pb in np.arange(0, 50, 0.5):
+        rows.append((float(pb), "res", 0.3, "monthly_bill_savings", "NREL", "host_owned"))
+    mms_df = pd.DataFrame(rows, columns=["payback_period", "sector_abbr", "max_market_share",
+                                         "metric", "source", "business_model"])
+    states = ["DE", "CA", "NY", "TX", "ZZ"]
+    bp = []
+    for st in states[:-1]:
+        for sec in ("res", "com", "ind"):
+            bp.append((st, sec, "solar", float(rng.uniform(0.0005, 0.003)), float(rng.uniform(0.3, 0.5)),
+                       float(rng.uniform(2.0, 12.0))))
+            bp.append((st, sec, "storage", 0.01, 0.2, 1.0))
+    bass = pd.DataFrame(bp, columns=["state_abbr", "sector_abbr", "tech", "bass_param_p",
+                                     "bass_param_q", "teq_yr1"])
+    st = rng.choice(states, n)
+    sec = rng.choice(["res", "com", "ind"], n)
+    pb = np.round(rng.uniform(-2, 35, n), 3)
+    special = [np.nan, 1e99, 30.1, 15.05, 0.0, 30.0, -1.0, 29.95, 0.04999999]
+    pb[:len(special)] = special
+    msly = rng.uniform(0, 0.2, n)
+    msly[::37] = 0.0
+    df = pd.DataFrame({
+        "state_abbr": st, "sector_abbr": sec, "payback_period": pb,
+        "market_share_last_year": msly,
+        "developable_agent_weight": np.where(rng.random(n) < 0.05, 0.0, rng.uniform(0, 500, n)),
+        "system_kw": rng.uniform(0, 200, n), "system_capex_per_kw": rng.uniform(1500, 5000, n),
+        "adopters_cum_last_year": rng.uniform(0, 50, n), "market_value_last_year": rng.uniform(0, 1e5, n),
+        "system_kw_cum_last_year": rng.uniform(0, 300, n), "batt_kw_cum_last_year": rng.uniform(0, 30, n),
+        "batt_kwh_cum_last_year": rng.uniform(0, 60, n),
+        "initial_number_of_adopters": rng.uniform(0, 5, n), "initial_pv_kw": rng.uniform(0, 10, n),
+        "initial_batt_kw": 0.0, "initial_batt_kwh": 0.0, "initial_market_share": 0.0,
+        "initial_market_value": 0.0,
+    }, index=pd.Index(np.arange(100, 100 + n), name="agent_id"))
+    return df, mms_df, bass
+
+
+def run_diffusion(ff, rng):
+    import diffusion_functions_elec as dfe
+    df, mms_df, bass = diffusion_inputs(rng)
+    out_mms = ff.calc_max_market_share(df, mms_df)
+    d2 = out_mms.copy()
+    d2.index = df.index
+    res = {}
+    for first in (True, False):
+        out, mly = dfe.calc_diffusion_solar(d2, first, bass, 2026 if first else 2027)
+        res["first" if first else "later"] = {"df": out.to_dict(orient="list"),
+                                              "columns": list(out.columns),
+                                              "market_last_year": mly.to_dict(orient="list"),
+                                              "mly_columns": list(mly.columns)}
+    return {"inputs": df.reset_index().to_dict(orient="list"), "mms_df": mms_df.to_dict(orient="list"),
+            "bass": bass.to_dict(orient="list"),
+            "mms_out": {"columns": list(out_mms.columns),
+                        "max_market_share": out_mms["max_market_share"].tolist()},
+            "diffusion": res}
+
+
 def _jsonable(o):
     if isinstance(o, dict):
         return {str(k): _jsonable(v) for k, v in o.items()}
@@ -565,6 +636,9 @@ def main():
             "tariff_cases": _jsonable([[n, r] for n, r in tariffs])}
     with open(os.path.join(HERE, "agents.json"), "w") as f:
         json.dump(_jsonable(meta), f)
+    dif = run_diffusion(ff, np.random.default_rng(20260004))
+    with open(os.path.join(HERE, "diffusion.json"), "w") as f:
+        json.dump(_jsonable(dif), f)
     np.savez_compressed(os.path.join(HERE, "agents.npz"), shapes=shapes, cfs=cfs, wholesale=ws,
                         **{k.replace(":", "__"): v for k, v in hourly.items()})
     print(f"tariffs={len(tar)} brent={len(br)} agents={len(recs)}")
