@@ -105,7 +105,8 @@ EXPORTED = [
 
 
 def lib_path() -> str:
-    return _build.OUT
+    # DGEN_LIB: load an alternative build (ablation / A-B timing of kernel variants)
+    return os.environ.get("DGEN_LIB") or _build.OUT
 
 
 def load(build_if_missing: bool = True) -> ctypes.CDLL:
