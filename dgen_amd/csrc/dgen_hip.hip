@@ -197,158 +197,18 @@ __global__ void k_row_slots_cf(const int32_t* __restrict__ rows, int64_t n_rows,
 // Utilityrate5 subset (semantics: DESIGN.md "SSC subset"; oracle/orc.c)
 // ---------------------------------------------------------------------------
 
-// Per-thread LDS accumulators for the hourly (mo 2) bill: [k][BLOCK] layout,
-// conflict-free (each lane owns a column).
-struct LdsAcc {
-    double* base;   // this lane's column of the dynamic LDS block
-    int half;       // slots per half: [0, half) imports/loads, [half, 2 half) exports/gen
-    __device__ double& at(int k) const { return base[k * BLOCK]; }
-    __device__ double& hi(int k) const { return base[(half + k) * BLOCK]; }
-};
-
-// dynamic LDS: 2 * max_periods doubles per lane
+// Dynamic LDS.  k_hourly_batt: per-lane (load, system) bin pairs [p][BLOCK];
+// the year-lane kernels: YLds (below).
 extern __shared__ double dyn_lds[];
 
+// periods the LDS layouts are sized for (batch maximum, clamped to MAXP)
 __host__ __device__ inline int lds_half(int max_periods) {
     return (max_periods > 0 && max_periods <= MAXP) ? max_periods : MAXP;
-}
-
-// LDS lane layout (k = slot index, `half` = max periods of the batch):
-//   [0, half)        mo 2 imports / battery-case loads / bin build (loads)
-//   [half, 2 half)   mo 2 exports / battery-case system output / bin build (gen)
-//   [2 half, 3 half) mo 0 kWh credits
-//   [3 half, 4 half) mo 0 billed kWh of the month
-constexpr int LDS_SLOTS_PER_HALF = 4;
-
-// Energy charge of one month from per-period billed kWh u_p = acc.at(uoff + p):
-// tier amounts from the monthly total, each period billed its share at its
-// own price.
-__device__ __forceinline__ double month_energy_charge(const dgen_tariff& t, int m, const LdsAcc& acc,
-                                                      int uoff) {
-    const int P = t.P, T = t.T;
-    double U = 0.0;
-    for (int p = 0; p < P; p++) U += acc.at(uoff + p);
-    if (!(U > 0.0)) return 0.0;
-    double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
-    double charge = 0.0, prev = 0.0;
-    for (int k = 0; k < T; k++) {
-        double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
-        double top = U < hi ? U : hi;
-        double amt = top - prev;
-        if (amt < 0.0) amt = 0.0;
-        if (hi > prev) prev = hi;
-        for (int p = 0; p < P; p++) charge += (acc.at(uoff + p) / U) * amt * t.buy[p][k];
-    }
-    return charge;
-}
-
-// NEM (mo 0) bill for one year from monthly per-period net kWh:
-//   net[m][p] = L[m][p] - gscale * G[m][p], bins plane-major [bin * n + agent].
-// Per-period kWh credits roll over month to month; December true-up at the
-// year-end sell rate.  Returns the bill before the escalation factor.
-__device__ __forceinline__ double year_bill_mo0(const dgen_tariff& t, const double* __restrict__ L,
-                                                const double* __restrict__ G, int64_t stride,
-                                                double gscale, double yearend_rate,
-                                                const LdsAcc& acc) {
-    const int P = t.P;
-    const int cr = 2 * acc.half, uo = 3 * acc.half;
-    for (int p = 0; p < P; p++) acc.at(cr + p) = 0.0;
-    double total = 0.0;
-    for (int m = 0; m < 12; m++) {
-        for (int p = 0; p < P; p++) {
-            int64_t b = (int64_t)(m * MAXP + p) * stride;
-            double g = G ? G[b] : 0.0;
-            double nn = L[b] - gscale * g;
-            double credit = acc.at(cr + p);
-            double u = 0.0;
-            if (nn >= 0.0) {
-                double use = nn < credit ? nn : credit;
-                u = nn - use;
-                credit -= use;
-            } else {
-                credit += -nn;
-            }
-            acc.at(cr + p) = credit;
-            acc.at(uo + p) = u;
-        }
-        double bill = t.fixed + month_energy_charge(t, m, acc, uo);
-        if (m == 11) {
-            double cc = 0.0;
-            for (int p = 0; p < P; p++) cc += acc.at(cr + p);
-            bill -= cc * yearend_rate;
-        }
-        total += bill;
-    }
-    return total;
-}
-
-// Hourly source for the net-billing year pass.
-struct HourSrc {
-    const float* shape;     // load row
-    const int32_t* cf;      // cf row (PV-only) or nullptr
-    const double* sysgen;   // battery scratch [h * stride] or nullptr
-    int64_t sys_stride;
-    double load_scale;      // load_kwh / row_sum
-    double gen_scale;       // kW scale for cf (PV-only)
-    const double* ts;       // wholesale row or nullptr
-    double ts_mult;
-};
-
-// Net-billing (mo 2) bill for one year: hourly imports billed through the
-// tier/period charge, hourly exports credited at the tier-1 sell rate of the
-// hour's period or at the float32-rounded TS sell rate (ff:751-761).
-__device__ __forceinline__ double year_bill_mo2(const dgen_tariff& t, const HourSrc& src, double s,
-                                bool with_gen, const LdsAcc& acc) {
-    const int P = t.P;
-    double total = 0.0;
-    int h = 0;
-    for (int m = 0; m < 12; m++) {
-        for (int p = 0; p < P; p++) { acc.at(p) = 0.0; acc.hi(p) = 0.0; }
-        for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
-            const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
-            for (int hod = 0; hod < 24; hod++, h++) {
-                double load = (double)src.shape[h] * src.load_scale;
-                double g = 0.0;
-                if (with_gen) {
-                    if (src.sysgen) g = src.sysgen[(int64_t)h * src.sys_stride];
-                    else g = ((double)src.cf[h] / 1e6) * src.gen_scale;
-                }
-                double dd = load - g * s;
-                int p = sched[hod];
-                if (dd > 0.0) {
-                    acc.at(p) += dd;
-                } else {
-                    double e = -dd;
-                    if (src.ts) e *= (double)(float)(src.ts[h] * src.ts_mult);
-                    acc.hi(p) += e;
-                }
-            }
-        }
-        double cr = 0.0;
-        for (int p = 0; p < P; p++) {
-            double e = acc.hi(p);
-            cr += src.ts ? e : e * t.sell[p][0];
-        }
-        total += t.fixed + month_energy_charge(t, m, acc, 0) - cr;
-    }
-    return total;
 }
 
 // ---------------------------------------------------------------------------
 // Cashloan subset: one year's step of the after-tax cash flow
 // ---------------------------------------------------------------------------
-struct LoanParams {
-    int N, term, market;
-    double infl, rr, fed, sta, r_loan, loan_f;  // loan_f = (1+r)^term
-    double itc_pct, itc_max, ins_rate, debt_frac;
-    int sl_years, depr_type;
-};
-
-struct LoanState {
-    double C, debt, pmt, itc, basis, ins0, balance, ins_esc, df, npv_acc, cum, payback;
-    bool paid;
-};
-
 __device__ __forceinline__ double depr_frac(int type, int year, int sl) {
     if (type == 1) {   // MACRS 5-year half-year table (no local array: keeps it out of scratch)
         switch (year) {
@@ -365,155 +225,6 @@ __device__ __forceinline__ double depr_frac(int type, int year, int sl) {
     return 0.0;
 }
 
-__device__ __forceinline__ void loan_begin(const LoanParams& lp, double C, LoanState& s) {
-    s.C = C;
-    s.debt = lp.debt_frac * C;
-    s.pmt = 0.0;
-    if (lp.term > 0 && s.debt != 0.0) {
-        if (lp.r_loan != 0.0) s.pmt = s.debt * lp.r_loan / (1.0 - 1.0 / lp.loan_f);
-        else s.pmt = s.debt / (double)lp.term;
-    }
-    double itc = lp.itc_pct * 0.01 * C;
-    s.itc = itc > lp.itc_max ? lp.itc_max : itc;
-    s.basis = C - 0.5 * s.itc;
-    s.ins0 = lp.ins_rate * C;
-    s.balance = s.debt;
-    s.ins_esc = 1.0;
-    s.df = 1.0;
-    s.npv_acc = -(C - s.debt);
-    s.cum = -C;
-    s.payback = 1e99;
-    s.paid = false;
-}
-
-// Returns cf_payback_with_expenses[i]; accumulates NPV (forward discounting)
-// and the payback interpolation of SSC compute_payback.
-__device__ __forceinline__ double loan_year(const LoanParams& lp, int i, double ev, LoanState& s) {
-    double oe = s.ins0 * s.ins_esc;
-    s.ins_esc = s.ins_esc * (1.0 + lp.infl);
-    double interest = 0.0, payment = 0.0;
-    if (i <= lp.term && s.pmt != 0.0) {
-        interest = s.balance * lp.r_loan;
-        payment = s.pmt;
-        s.balance = s.balance - (s.pmt - interest);
-    }
-    double itc_i = (i == 1) ? s.itc : 0.0;
-    double sta_tax = 0.0, fed_tax = 0.0;
-    if (lp.market != 0) {
-        double dep = depr_frac(lp.depr_type, i, lp.sl_years) * s.basis;
-        sta_tax = lp.sta * (ev - oe - interest - dep);
-        fed_tax = lp.fed * (ev - oe - interest - dep - sta_tax);
-    }
-    double taxsav = itc_i - sta_tax - fed_tax;
-    double atcf = ev - oe - payment + taxsav;
-    double pb = ev - oe + taxsav;
-    s.df = s.df * lp.rr;
-    s.npv_acc += atcf * s.df;
-    s.cum += pb;
-    if (!s.paid && s.cum > 0.0) {
-        s.paid = true;
-        s.payback = (pb != 0.0) ? (double)i - s.cum / pb : (double)i - 0.5;
-    }
-    return pb;
-}
-
-__device__ __forceinline__ LoanParams make_loan(const dgen_agents& A, const dgen_cfg& cfg, int64_t i,
-                                                int N, bool is_res) {
-    LoanParams lp;
-    lp.N = N;
-    lp.term = A.loan_term[i];
-    lp.market = is_res ? 0 : 1;
-    double infl_pct = A.inflation[i] * 100.0;
-    lp.infl = infl_pct * 0.01;
-    double real = (A.real_discount[i] * 100.0) * 0.01;
-    double nom = (1.0 + real) * (1.0 + lp.infl) - 1.0;
-    lp.rr = 1.0 / (1.0 + nom);
-    double tax_pct = A.tax_rate[i] * 100.0;
-    lp.fed = (tax_pct * 0.7) * 0.01;
-    lp.sta = (tax_pct * 0.3) * 0.01;
-    lp.r_loan = cfg.loan_rate_pct * 0.01;
-    double f = 1.0;
-    for (int k = 0; k < lp.term; k++) f = f * (1.0 + lp.r_loan);
-    lp.loan_f = f;
-    lp.itc_pct = A.itc_frac[i];          // ff:285 passes the fraction as the percent
-    lp.itc_max = cfg.itc_fed_max;
-    lp.ins_rate = cfg.insurance_rate_pct * 0.01;
-    lp.debt_frac = (100.0 - (A.down_payment[i] * 100.0)) * 0.01;
-    lp.sl_years = cfg.depr_sl_years;
-    lp.depr_type = is_res ? 0 : 2;
-    return lp;
-}
-
-// ---------------------------------------------------------------------------
-// bins for the PV-only search (kW independent; rebuilt on a tariff switch)
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
-                                           const double* __restrict__ gslots, double load_scale,
-                                           double* __restrict__ L, double* __restrict__ G,
-                                           int64_t stride, const LdsAcc& acc) {
-    const int P = t.P;
-    for (int m = 0; m < 12; m++) {
-        for (int p = 0; p < P; p++) { acc.at(p) = 0.0; acc.hi(p) = 0.0; }
-        for (int dt = 0; dt < 2; dt++) {
-            const uint8_t* sched = dt ? t.wkend[m] : t.wkday[m];
-            for (int hod = 0; hod < 24; hod++) {
-                int sl = m * 48 + dt * 24 + hod;
-                int p = sched[hod];
-                acc.at(p) += lslots[sl];
-                acc.hi(p) += gslots[sl];
-            }
-        }
-        for (int p = 0; p < P; p++) {
-            int64_t b = (int64_t)(m * MAXP + p) * stride;
-            L[b] = acc.at(p) * load_scale;
-            G[b] = acc.hi(p);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_size: PV-only bounded-Brent search, one thread per agent
-// ---------------------------------------------------------------------------
-struct SizeCtx {
-    const dgen_tariff* tariffs;
-    const dgen_switch* sw_rows;   // this agent's solar rate-switch candidates
-    int sw_cnt;
-    int64_t i, n;
-    int N;
-    bool is_ca;
-    int tariff;
-    int switched;
-    int status;
-    double load_scale, kwh, capex, ccm, yearend;
-    double rate_base, sys_base;
-    LoanParams lp;
-    double* L;            // workspace bins [bin * n + i]
-    double* G;
-    double wo1;           // year-1 no-system bill for the current tariff
-    HourSrc src;          // for mo 2
-    LdsAcc acc;
-    const double* lslots;
-    const double* gslots;
-};
-
-// Output pointers written by the final (last-x) evaluation.
-struct FinalOut {
-    double *cash_flow, *cfev, *bw, *bwo;
-    double *npv, *payback_raw, *payback_period, *first_with, *first_without, *price_per_kwh;
-};
-
-__device__ __forceinline__ void set_tariff(SizeCtx& c, int tix) {
-    const dgen_tariff& t = c.tariffs[tix];
-    c.tariff = tix;
-    c.status |= t.flags;
-    if (t.mo == 0) {
-        build_bins(t, c.lslots, c.gslots, c.load_scale, c.L, c.G, c.n, c.acc);
-        c.wo1 = year_bill_mo0(t, c.L, nullptr, c.n, 0.0, c.yearend, c.acc);
-    } else {
-        c.wo1 = year_bill_mo2(t, c.src, 1.0, false, c.acc);
-    }
-}
-
 // apply_rate_switch (elec.py:838-863): exactly one row with min <= size < max.
 __device__ __forceinline__ double rate_switch(const dgen_switch* rows, int cnt, double size,
                                               int* new_tariff) {
@@ -526,63 +237,6 @@ __device__ __forceinline__ double rate_switch(const dgen_switch* rows, int cnt, 
         return rows[hit].one_time_charge;
     }
     return 0.0;
-}
-
-// One evaluation of calc_system_performance(kw, en_batt=False); returns -NPV.
-// With `out` set, writes the 26-long arrays and scalars of this evaluation.
-__device__ __forceinline__ double objective(SizeCtx& c, double kw, const FinalOut* out) {
-    double otc = 0.0;
-    if (kw > 0.0) {
-        int nt;
-        otc = rate_switch(c.sw_rows, c.sw_cnt, kw, &nt);
-        if (nt >= 0) {
-            c.switched = 1;
-            if (nt != c.tariff) set_tariff(c, nt);
-        }
-    }
-    const dgen_tariff& t = c.tariffs[c.tariff];
-    double kws = ((kw * 1000.0) * 0.96) / 1000.0;       // ff:118-120 per-kW scale
-    double total = ((c.capex * kw + 0.0) * c.ccm) + 0.0 + otc;   // ff:263,280-282
-    LoanState ls;
-    loan_begin(c.lp, total, ls);
-    double r = 1.0, s = 1.0, w1 = 0.0;
-    const int64_t n = c.n;
-    if (out) {
-        out->cash_flow[c.i] = -total;
-        out->cfev[c.i] = 0.0;
-        out->bw[c.i] = 0.0;
-        out->bwo[c.i] = 0.0;
-    }
-    c.src.gen_scale = kws;
-    for (int y = 1; y <= c.N; y++) {
-        double wb;
-        if (t.mo == 0) wb = year_bill_mo0(t, c.L, c.G, n, s * kws, c.yearend, c.acc);
-        else wb = year_bill_mo2(t, c.src, s, true, c.acc);
-        double w = wb * r;
-        double wo = c.wo1 * r;
-        double ev = wo - w;
-        if (y == 1) w1 = w;
-        double pb = loan_year(c.lp, y, ev, ls);
-        if (out) {
-            out->cash_flow[(int64_t)y * n + c.i] = pb;
-            out->cfev[(int64_t)y * n + c.i] = ev;
-            out->bw[(int64_t)y * n + c.i] = w;
-            out->bwo[(int64_t)y * n + c.i] = wo;
-        }
-        r = r * c.rate_base;
-        s = s * c.sys_base;
-    }
-    double npv = ls.npv_acc;
-    if (out) {
-        out->npv[c.i] = npv;
-        out->payback_raw[c.i] = ls.payback;
-        double pb = isfinite(ls.payback) ? ls.payback : 30.1;
-        out->payback_period[c.i] = rint(pb * 10.0) / 10.0;
-        out->first_with[c.i] = w1;
-        out->first_without[c.i] = c.wo1;
-        out->price_per_kwh[c.i] = c.wo1 / c.kwh;
-    }
-    return -npv;
 }
 
 __device__ __forceinline__ double np_sign(double v) {
@@ -685,86 +339,6 @@ __host__ __device__ inline WsLayout ws_layout(void* base, int64_t n) {
     return w;
 }
 
-__global__ void __launch_bounds__(BLOCK, 3)
-k_size(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws) {
-    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    WsLayout W = ws_layout(ws, n);
-    SizeCtx c;
-    c.tariffs = T.tariffs;
-    c.sw_rows = T.switches + A.sw_solar_off[i];
-    c.sw_cnt = A.sw_solar_cnt[i];
-    c.i = i; c.n = n;
-    c.status = 0; c.switched = 0;
-    c.acc.base = dyn_lds + threadIdx.x;
-    c.acc.half = lds_half(T.max_periods);
-    uint8_t fl = A.flags[i];
-    const bool is_res = (fl & 1) != 0;
-    c.is_ca = (fl & 2) != 0;
-    c.N = A.econ_life[i];
-    c.kwh = A.load_kwh[i];
-    c.capex = A.capex[i];
-    c.ccm = A.ccm[i];
-    c.yearend = cfg.nm_yearend_sell_rate;
-    int lr = A.load_row[i], cr = A.cf_row[i];
-    int t0 = A.tariff0[i];
-    double S = T.shape_sum[lr];
-    double naep0 = T.cf_naep[cr];
-    c.load_scale = c.kwh / S;
-    c.lslots = T.shape_slots + (int64_t)lr * NSLOT;
-    c.gslots = T.cf_slots + (int64_t)cr * NSLOT;
-    c.L = W.L + i; c.G = W.G + i;
-    // ff:364-368: escalation (1 + infl + esc)^i, degradation (1 - d)^i
-    c.rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
-    c.sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
-    c.lp = make_loan(A, cfg, i, c.N, is_res);
-    c.src.shape = T.shapes + (int64_t)lr * NH;
-    c.src.cf = T.cfs + (int64_t)cr * NH;
-    c.src.sysgen = nullptr; c.src.sys_stride = 0;
-    c.src.load_scale = c.load_scale;
-    c.src.gen_scale = 0.0;
-    int wr = A.wholesale_row[i];
-    c.src.ts = (!c.is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
-    c.src.ts_mult = A.price_mult[i];
-
-    bool bad = false;
-    if (c.N < 1 || c.N > MAXY) { c.status |= DGEN_ST_YEARS; bad = true; }
-    if (t0 < 0 || t0 >= T.n_tariffs) { c.status |= DGEN_ST_TARIFF; bad = true; }
-    // ff:440-444 bracket and xatol
-    double max_load = c.kwh / naep0;
-    double low = max_load * 0.8, high = max_load * 1.25;
-    double span = high - low;
-    double tl = (span > 1.0 ? span : 1.0) * 1e-3;      // max(1, high - low) * 1e-3
-    double fl_tl = floor(tl);
-    double xatol = fl_tl < 2.0 ? 2.0 : fl_tl;           // max(2, int(...))
-    if (!isfinite(low) || !isfinite(high)) { c.status |= DGEN_ST_BOUNDS; bad = true; }
-    if (c.kwh == 0.0) c.status |= DGEN_ST_ZERO_LOAD;
-    if (bad) {
-        O.status[i] = c.status;
-        O.nfev[i] = 0;
-        O.system_kw[i] = NAN; O.x_last[i] = NAN; O.npv[i] = NAN;
-        O.tariff_final[i] = t0; O.switched[i] = 0;
-        return;
-    }
-    set_tariff(c, t0);
-    int nfev = 0;
-    double x_last = 0.0;
-    double kw_star = brent_bounded(
-        [&](double x) __attribute__((always_inline)) { return objective(c, x, nullptr); },
-        low, high, xatol, &nfev, &x_last);
-    // ff:449-474: outputs of the LAST evaluation.  Re-running it is exact: the
-    // sticky switch is idempotent at the same x and the state is unchanged.
-    FinalOut fo{O.cash_flow, O.cfev_pv, O.bill_w_pv, O.bill_wo_pv, O.npv, O.payback_raw,
-                O.payback_period, O.first_with, O.first_without, O.price_per_kwh};
-    objective(c, x_last, &fo);
-    O.system_kw[i] = kw_star;
-    O.x_last[i] = x_last;
-    O.nfev[i] = nfev;
-    O.tariff_final[i] = c.tariff;
-    O.switched[i] = c.switched;
-    O.status[i] = c.status;
-}
-
 // ---------------------------------------------------------------------------
 // k_hourly_batt: one sequential scan over the year per agent
 // ---------------------------------------------------------------------------
@@ -815,29 +389,36 @@ __device__ __forceinline__ double day_d(const DayRaw& r, int h, double ls, doubl
 }
 
 __device__ __forceinline__ double day_target(const DayRaw& r, double ls, double cs6, double power, double avail,
-                             double dmax, double need0, int a_lo, int b_lo) {
+                             double dmax, double need0, int a_lo, int b_lo, double dmin_pos) {
     if (need0 <= avail) return 0.0;
     ls = opaque(ls);
     cs6 = opaque(cs6);
     if (dmax <= power) {
-        // no hour saturates: convex water-filling, Newton from T = 0 (exact once
-        // the active count stops changing)
-        double t = 0.0, f = need0;
+        // no hour saturates: convex water-filling, Newton from T = 0, exact once
+        // the active count stops changing.  `mact` = min{d_h : d_h > t}: the
+        // count at tn equals the count at t iff mact > tn, so the confirming
+        // pass of the plain iteration is skipped (same iterates, same result).
+        double t = 0.0, f = need0, mact = dmin_pos;
         int a = a_lo;
         for (int it = 0; it < 48; it++) {
             double tn = t + (f - avail) / (double)a;
-            double fn = 0.0;
+            t = tn;
+            if (mact > tn) break;
+            double fn = 0.0, mn = INFINITY;
             int an = 0;
 #pragma unroll
             for (int h = 0; h < 24; h++) {
-                double e = day_d(r, h, ls, cs6) - tn;
-                an += e > 0.0;
-                fn += e > 0.0 ? e : 0.0;
+                const double dh = day_d(r, h, ls, cs6);
+                double e = dh - tn;
+                const bool on = e > 0.0;
+                an += on;
+                fn += on ? e : 0.0;
+                mn = (on && dh < mn) ? dh : mn;
             }
-            t = tn;
             if (an == a || fn <= avail || an == 0) break;
             f = fn;
             a = an;
+            mact = mn;
         }
         return t;
     }
@@ -867,6 +448,48 @@ __device__ __forceinline__ double day_target(const DayRaw& r, double ls, double 
     return t;
 }
 
+// Byte-addressed store into one hour row: `row` is wave-uniform (SGPRs), the
+// lane's 32-bit offset zero-extends (global_store ... v_off, s[base]).
+__device__ __forceinline__ void st_f32(char* row, uint32_t off, float v) {
+    *reinterpret_cast<float*>(row + off) = v;
+}
+__device__ __forceinline__ void st_f64(char* row, uint32_t off, double v) {
+    *reinterpret_cast<double*>(row + off) = v;
+}
+
+// One hour of the dispatch (same arithmetic as the oracle's branchy
+// orc_batt_dispatch, written without divergence): charge when the net load is
+// negative, discharge towards the day's target otherwise.  With no battery
+// (bank = power = 0) every clamp is 0 and sys = pv, g2l = max(nn, 0).
+struct HourStep {
+    double sys, g2l;
+};
+__device__ __forceinline__ HourStep batt_hour(double nn, double pv, double target, double power,
+                                              double bank, double& soc, const dgen_cfg& cfg,
+                                              double inv_eta_in, double in_per_bank,
+                                              double out_per_bank) {
+    const bool chg = nn < 0.0;
+    double room = (cfg.batt_max_soc - soc) * bank * inv_eta_in;
+    room = room < 0.0 ? 0.0 : room;
+    double avail = (soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out;
+    avail = avail < 0.0 ? 0.0 : avail;
+    double cc = -nn;
+    cc = cc > power ? power : cc;
+    cc = cc > room ? room : cc;
+    double dd = nn - target;
+    dd = dd < 0.0 ? 0.0 : dd;
+    dd = dd > power ? power : dd;
+    dd = dd > avail ? avail : dd;
+    // soc + cc*k  ==  soc + (-(dd*k')) exactly for the discharge branch
+    const double dsoc = chg ? cc * in_per_bank : -(dd * out_per_bank);
+    soc = soc + dsoc;
+    HourStep r;
+    r.sys = pv + (chg ? -cc : dd);
+    r.g2l = chg ? 0.0 : nn - dd;
+    return r;
+}
+
+template <bool HOURLY>
 __global__ void __launch_bounds__(BLOCK, 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch) {
@@ -874,7 +497,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     if (i >= n) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
     WsLayout W = ws_layout(ws, n);
-    LdsAcc acc{dyn_lds + threadIdx.x, lds_half(T.max_periods)};
+    // battery-case bins: (load, system output) pairs per period, [p][BLOCK]
+    double2* bins = reinterpret_cast<double2*>(dyn_lds) + threadIdx.x;
     const bool is_res = (A.flags[i] & 1) != 0;
     const int lr = A.load_row[i], cr = A.cf_row[i];
     const double kwh = A.load_kwh[i];
@@ -905,27 +529,36 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const int P = t.P;
     const bool mo2 = (t.mo == 2);
     const int slot = A.scratch_slot[i];
-    double* scratch = (mo2 && slot >= 0) ? W.scratch + slot : nullptr;
+    const bool put_sys = mo2 && slot >= 0;
     int status = O.status[i] | t.flags;
     if (mo2 && slot < 0) status |= DGEN_ST_SCRATCH;
 
-    const double eta_out = cfg.batt_eta_out;
-    const double min_soc = cfg.batt_min_soc, max_soc = cfg.batt_max_soc;
     const double inv_eta_in = 1.0 / cfg.batt_eta_in;
     const double in_per_bank = bank > 0.0 ? cfg.batt_eta_in / bank : 0.0;
-    const double out_per_bank = bank > 0.0 ? 1.0 / (eta_out * bank) : 0.0;
+    const double out_per_bank = bank > 0.0 ? 1.0 / (cfg.batt_eta_out * bank) : 0.0;
     const bool has_batt = bank > 0.0;
+    if (!has_batt) power = 0.0;
     double soc = cfg.batt_init_soc;
     double annual = 0.0;
-    float* __restrict__ o_base = O.baseline;
-    float* __restrict__ o_pvo = O.net_pvonly;
-    float* __restrict__ o_wb = O.net_with_batt;
+    // hour rows: wave-uniform bases advanced by one row per hour; per-lane
+    // 32-bit byte offsets (host guarantees n < 2^29, n_scratch < 2^28)
+    const uint32_t off4 = (uint32_t)i * 4u;
+    const uint32_t off8 = (uint32_t)(put_sys ? slot : 0) * 8u;
+    const size_t row4 = (size_t)n * 4u, row8 = (size_t)n_scratch * 8u;
+    char* const ob = reinterpret_cast<char*>(O.baseline);
+    char* const op = reinterpret_cast<char*>(O.net_pvonly);
+    char* const ow = reinterpret_cast<char*>(O.net_with_batt);
+    char* const osc = reinterpret_cast<char*>(W.scratch);
+    size_t ho4 = 0, ho8 = 0;
 
     for (int m = 0; m < 12; m++) {
-        for (int p = 0; p < P; p++) { acc.at(p) = 0.0; acc.hi(p) = 0.0; }
+        for (int p = 0; p < P; p++) bins[p * BLOCK] = make_double2(0.0, 0.0);
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             const int h0 = d * 24;
-            const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
+            // the day's period schedule: 24 bytes (8-aligned rows) in 3 registers
+            const uint64_t* sr =
+                reinterpret_cast<const uint64_t*>(((d % 7) >= 5) ? t.wkend[m] : t.wkday[m]);
+            const uint64_t sched[3] = {sr[0], sr[1], sr[2]};
             DayRaw r;
             // 96 B of the shape row and 96 B of the cf row: 6 x 16 B loads each
             const float4* s4 = reinterpret_cast<const float4*>(shp + h0);
@@ -937,79 +570,61 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 r.s[4 * q + 0] = sv.x; r.s[4 * q + 1] = sv.y; r.s[4 * q + 2] = sv.z; r.s[4 * q + 3] = sv.w;
                 r.c[4 * q + 0] = cv.x; r.c[4 * q + 1] = cv.y; r.c[4 * q + 2] = cv.z; r.c[4 * q + 3] = cv.w;
             }
-            double need0 = 0.0, dmax = 0.0;
-            int a0 = 0, b0 = 0;
-#pragma unroll
-            for (int hh = 0; hh < 24; hh++) {
-                const int64_t h = h0 + hh;
-                double ld = (double)r.s[hh] * ls;
-                double cfv = (double)r.c[hh];
-                double pl = cfv * cl6;
-                annual += pl;
-                if (o_base) o_base[h * n + i] = (float)ld;
-                if (o_pvo) {
-                    double dn = ld - pl;
-                    o_pvo[h * n + i] = (float)(dn > 0.0 ? dn : 0.0);
-                }
-                double dd = ld - cfv * cs6;
-                if (dd < 0.0) dd = 0.0;
-                if (dd > dmax) dmax = dd;
-                need0 += dd < power ? dd : power;
-                a0 += dd > 0.0;
-                b0 += (dd - power) >= 0.0;
-            }
             double target = 0.0;
             if (has_batt) {
-                double avail = (soc - min_soc) * bank * eta_out;
+                // day statistics of d_h = max(load_h - pv_h, 0) for the target
+                double need0 = 0.0, dmax = 0.0, dmin_pos = INFINITY;
+                int a0 = 0, b0 = 0;
+#pragma unroll
+                for (int hh = 0; hh < 24; hh++) {
+                    double dd = (double)r.s[hh] * ls - (double)r.c[hh] * cs6;
+                    if (dd < 0.0) dd = 0.0;
+                    if (dd > dmax) dmax = dd;
+                    need0 += dd < power ? dd : power;
+                    a0 += dd > 0.0;
+                    b0 += (dd - power) >= 0.0;
+                    dmin_pos = (dd > 0.0 && dd < dmin_pos) ? dd : dmin_pos;
+                }
+                double avail = (soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out;
                 if (avail < 0.0) avail = 0.0;
-                target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0);
+                target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0, dmin_pos);
             }
-            const double ls2 = opaque(ls), cs2 = opaque(cs6);
+            const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);
 #pragma unroll
             for (int hh = 0; hh < 24; hh++) {
-                const int64_t h = h0 + hh;
-                double ld = (double)opaque_f(r.s[hh]) * ls2;
-                double pv = (double)opaque_i(r.c[hh]) * cs2;
-                double nn = ld - pv;
-                double sys, g2l;
-                if (!has_batt) {
-                    sys = pv;
-                    g2l = nn > 0.0 ? nn : 0.0;
-                } else if (nn < 0.0) {
-                    double room = (max_soc - soc) * bank * inv_eta_in;
-                    if (room < 0.0) room = 0.0;
-                    double cc = -nn;
-                    if (cc > power) cc = power;
-                    if (cc > room) cc = room;
-                    soc = soc + cc * in_per_bank;
-                    sys = pv - cc;
-                    g2l = 0.0;
-                } else {
-                    double avail = (soc - min_soc) * bank * eta_out;
-                    if (avail < 0.0) avail = 0.0;
-                    double dd = nn - target;
-                    if (dd < 0.0) dd = 0.0;
-                    if (dd > power) dd = power;
-                    if (dd > avail) dd = avail;
-                    soc = soc - dd * out_per_bank;
-                    sys = pv + dd;
-                    g2l = nn - dd;
+                const double ld = (double)opaque_f(r.s[hh]) * ls2;
+                const double cfv = (double)opaque_i(r.c[hh]);
+                const double pl = cfv * cl2;                 // PV-only run (x_last)
+                annual += pl;
+                const double pv = cfv * cs2;                 // battery run (kW*)
+                const double nn = ld - pv;
+                HourStep st = batt_hour(nn, pv, target, power, bank, soc, cfg, inv_eta_in,
+                                        in_per_bank, out_per_bank);
+                if constexpr (HOURLY) {
+                    const double dn = ld - pl;
+                    st_f32(ob + ho4, off4, (float)ld);
+                    st_f32(op + ho4, off4, (float)(dn > 0.0 ? dn : 0.0));
+                    st_f32(ow + ho4, off4, (float)st.g2l);
                 }
-                if (o_wb) o_wb[h * n + i] = (float)g2l;
-                if (mo2) {
-                    if (scratch) scratch[h * n_scratch] = sys;    // plane [h][slot]
-                } else {
-                    int p = sched[hh];
-                    acc.at(p) += ld;
-                    acc.hi(p) += sys;
+                ho4 += row4;
+                if (put_sys) {
+                    st_f64(osc + ho8, off8, st.sys);         // plane [h][slot]
+                } else if (!mo2) {
+                    const int p = (int)((sched[hh >> 3] >> (8 * (hh & 7))) & 0xffu);
+                    double2 b = bins[p * BLOCK];
+                    b.x += ld;
+                    b.y += st.sys;
+                    bins[p * BLOCK] = b;
                 }
+                ho8 += row8;
             }
         }
         if (!mo2) {
             for (int p = 0; p < P; p++) {
-                int64_t b = (int64_t)(m * MAXP + p) * n + i;
-                W.Lb[b] = acc.at(p);
-                W.Gb[b] = acc.hi(p);
+                const double2 b = bins[p * BLOCK];
+                int64_t k = (int64_t)(m * MAXP + p) * n + i;
+                W.Lb[k] = b.x;
+                W.Gb[k] = b.y;
             }
         }
     }
@@ -1018,79 +633,12 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     double naep = annual / den;
     O.naep[i] = naep;
     O.capacity_factor[i] = naep / 8760.0;
-    O.batt_kw[i] = power;
+    O.batt_kw[i] = has_batt ? power : 0.0;
     O.batt_kwh[i] = bank;
     O.tariff_final[i] = tariff;
     O.switched[i] = switched;
     O.status[i] = status;
     W.otc_b[i] = otc;
-}
-
-// ---------------------------------------------------------------------------
-// k_batt_finance: Utilityrate5 + Cashloan of the PV+battery run (ff:178-288)
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(BLOCK)
-k_batt_finance(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-               int64_t n_scratch) {
-    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const int st = O.status[i];
-    if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH)) return;
-    WsLayout W = ws_layout(ws, n);
-    LdsAcc acc{dyn_lds + threadIdx.x, lds_half(T.max_periods)};
-    const bool is_res = (A.flags[i] & 1) != 0;
-    const bool is_ca = (A.flags[i] & 2) != 0;
-    const int N = A.econ_life[i];
-    const dgen_tariff& t = T.tariffs[O.tariff_final[i]];
-    const double kw = O.system_kw[i];
-    const double bank = O.batt_kwh[i];
-    const double otc = W.otc_b[i];
-    const double rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
-    const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
-    const LoanParams lp = make_loan(A, cfg, i, N, is_res);
-    // ff:203-219 costs of the PV+battery system
-    double system_costs = (kw > 0.0) ? A.capex_combined[i] * kw : A.capex[i] * kw;
-    double batt_costs = A.batt_capex_kwh[i] * bank * 0.7;
-    double total = ((system_costs + batt_costs) * A.ccm[i]) + 0.0 + otc;
-    const double vor = A.vor[i];
-
-    HourSrc src;
-    const int lr = A.load_row[i];
-    src.shape = T.shapes + (int64_t)lr * NH;
-    src.cf = nullptr;
-    src.load_scale = A.load_kwh[i] / T.shape_sum[lr];
-    src.gen_scale = 0.0;
-    src.sys_stride = n_scratch;
-    const int slot = A.scratch_slot[i];
-    src.sysgen = (slot >= 0) ? W.scratch + slot : nullptr;
-    int wr = A.wholesale_row[i];
-    src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
-    src.ts_mult = A.price_mult[i];
-    const bool mo2 = t.mo == 2;
-    const double yr = cfg.nm_yearend_sell_rate;
-    const double* Lb = W.Lb + i;
-    const double* Gb = W.Gb + i;
-
-    double wo1 = mo2 ? year_bill_mo2(t, src, 1.0, false, acc) : year_bill_mo0(t, Lb, nullptr, n, 0.0, yr, acc);
-    LoanState ls;
-    loan_begin(lp, total, ls);
-    O.cfev_batt[i] = 0.0;
-    O.bill_w_batt[i] = 0.0;
-    O.bill_wo_batt[i] = 0.0;
-    double r = 1.0, s = 1.0;
-    for (int y = 1; y <= N; y++) {
-        double wb = mo2 ? year_bill_mo2(t, src, s, true, acc) : year_bill_mo0(t, Lb, Gb, n, s, yr, acc);
-        double w = wb * r;
-        double wo = wo1 * r;
-        double ev = (wo - w) + vor;          // ff:275: VOR added to every year
-        loan_year(lp, y, ev, ls);
-        O.cfev_batt[(int64_t)y * n + i] = ev;
-        O.bill_w_batt[(int64_t)y * n + i] = w;
-        O.bill_wo_batt[(int64_t)y * n + i] = wo;
-        r = r * rate_base;
-        s = s * sys_base;
-    }
-    O.npv_pv_batt[i] = ls.npv_acc;
 }
 
 // ===========================================================================
@@ -1879,6 +1427,15 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                            O->bill_w_batt, O->bill_wo_batt};
     for (const void* p : req_o)
         if (!p) { set_err("dgen_size_agents: missing output column"); return DGEN_E_ARG; }
+    const bool hourly = O->baseline != nullptr;
+    if ((O->net_pvonly != nullptr) != hourly || (O->net_with_batt != nullptr) != hourly) {
+        set_err("dgen_size_agents: hourly planes must be all set or all NULL");
+        return DGEN_E_ARG;
+    }
+    if (n >= ((int64_t)1 << 29) || n_scratch >= ((int64_t)1 << 28)) {
+        set_err("dgen_size_agents: batch too large (n < 2^29, n_scratch < 2^28 per call)");
+        return DGEN_E_ARG;
+    }
     if (!ws || ws_bytes < dgen_workspace_bytes(n, n_scratch)) {
         set_err("dgen_size_agents: workspace too small (%zu < %zu)", ws_bytes,
                 dgen_workspace_bytes(n, n_scratch));
@@ -1895,12 +1452,15 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->head = (c->head + 1) % dgen_ctx::RING;
     c->pending++;
     dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK)), block(BLOCK);
-    const size_t lds = sizeof(double) * LDS_SLOTS_PER_HALF * (size_t)lds_half(T->max_periods) * BLOCK;
+    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK;
     HIP_TRY(hipEventRecord(c->ev[slot][0], s));
     const size_t ylds = ylds_bytes(lds_half(T->max_periods));
     hipLaunchKernelGGL(k_size_w, dim3((unsigned)n), dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n);
     HIP_TRY(hipEventRecord(c->ev[slot][1], s));
-    hipLaunchKernelGGL(k_hourly_batt, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
+    if (hourly)
+        hipLaunchKernelGGL(k_hourly_batt<true>, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
+    else
+        hipLaunchKernelGGL(k_hourly_batt<false>, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
     HIP_TRY(hipEventRecord(c->ev[slot][2], s));
     hipLaunchKernelGGL(k_batt_finance_w, dim3((unsigned)n), dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n,
                        ws, n_scratch);

@@ -12,3 +12,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; ok $rc
 timeout -k 10 400 python bench.py --agents $AGENTS --steps 3 --warmup 1 --cpu-seconds 5 > gpurun_out/bench_small.log 2>&1; rc=$?
 echo "bench rc=$rc"; tail -3 gpurun_out/bench_small.log; ok $rc
+if [ -n "$FULL" ]; then
+  timeout -k 10 500 python bench.py > gpurun_out/bench_full.log 2>&1; rc=$?
+  echo "bench full rc=$rc"; tail -3 gpurun_out/bench_full.log; ok $rc
+fi
