@@ -749,6 +749,67 @@ __device__ __forceinline__ double yl_bill_mo0(const dgen_tariff& t, const YLds& 
     return total;
 }
 
+// Same bill with the per-period credits and billed kWh in registers (P <= 4,
+// the common case): loops run to the compile-time bound under the uniform
+// guard p < P, so the order of every sum is the LDS version's.
+constexpr int PREG = 4;
+__device__ __forceinline__ double yl_bill_mo0_reg(const dgen_tariff& t, const YLds& S, double gscale,
+                                                  double yearend) {
+    const int P = t.P, T = t.T, half = S.half;
+    double credit[PREG], u[PREG];
+#pragma unroll
+    for (int p = 0; p < PREG; p++) { credit[p] = 0.0; u[p] = 0.0; }
+    double total = 0.0;
+    for (int m = 0; m < 12; m++) {
+#pragma unroll
+        for (int p = 0; p < PREG; p++) {
+            if (p < P) {
+                double nn = S.L[m * half + p] - gscale * S.G[m * half + p];
+                double use = nn < credit[p] ? nn : credit[p];
+                double un = nn - use;
+                double cn = credit[p] - use;
+                const bool pos = nn >= 0.0;
+                u[p] = pos ? un : 0.0;
+                credit[p] = pos ? cn : credit[p] + -nn;
+            }
+        }
+        double U = 0.0;
+#pragma unroll
+        for (int p = 0; p < PREG; p++)
+            if (p < P) U += u[p];
+        double charge = 0.0;
+        if (U > 0.0) {
+            double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
+            double prev = 0.0;
+            for (int k = 0; k < T; k++) {
+                double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
+                double top = U < hi ? U : hi;
+                double amt = top - prev;
+                if (amt < 0.0) amt = 0.0;
+                if (hi > prev) prev = hi;
+#pragma unroll
+                for (int p = 0; p < PREG; p++)
+                    if (p < P) charge += (u[p] / U) * amt * t.buy[p][k];
+            }
+        }
+        double bill = t.fixed + charge;
+        if (m == 11) {
+            double cc = 0.0;
+#pragma unroll
+            for (int p = 0; p < PREG; p++)
+                if (p < P) cc += credit[p];
+            bill -= cc * yearend;
+        }
+        total += bill;
+    }
+    return total;
+}
+
+__device__ __forceinline__ double yl_bill_nem(const dgen_tariff& t, const YLds& S, double gscale,
+                                              double yearend) {
+    return (t.P <= PREG) ? yl_bill_mo0_reg(t, S, gscale, yearend) : yl_bill_mo0(t, S, gscale, yearend);
+}
+
 // Wave-uniform hourly source for net billing.
 struct YSrc {
     const float* shape;
@@ -874,15 +935,19 @@ __device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev
     if (itc > L.itc_max) itc = L.itc_max;
     double basis = C - 0.5 * itc;
     double oe = (L.ins_rate * C) * L.ins_esc;
-    // loan balance entering year y: the same recursion as a sequential pass
-    double bal = debt;
-    for (int k = 1; k < y; k++)
-        if (k <= L.term && pmt != 0.0) bal = bal - (pmt - bal * L.r_loan);
-    double interest = 0.0, payment = 0.0;
-    if (y <= L.term && pmt != 0.0) { interest = bal * L.r_loan; payment = pmt; }
+    const bool paying = y <= L.term && pmt != 0.0;
+    const double payment = paying ? pmt : 0.0;
     double itc_y = (y == 1) ? itc : 0.0;
     double sta_tax = 0.0, fed_tax = 0.0;
     if (L.market != 0) {
+        // interest is deductible for commercial agents only; the balance
+        // entering year y follows the same sequential recursion (years past the
+        // term or the analysis period leave it unchanged or are unused)
+        double bal = debt;
+        const int kend = min(min(y, L.term + 1), L.N + 1);
+        if (pmt != 0.0)
+            for (int k = 1; k < kend; k++) bal = bal - (pmt - bal * L.r_loan);
+        const double interest = paying ? bal * L.r_loan : 0.0;
         double dep = depr_frac(L.depr_type, y, L.sl_years) * basis;
         sta_tax = L.sta * (ev - oe - interest - dep);
         fed_tax = L.fed * (ev - oe - interest - dep - sta_tax);
@@ -905,6 +970,11 @@ __device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev
     return f;
 }
 
+struct YLast {   // per-lane results of the most recent evaluation
+    double total, ev, w, wo;
+    YFlow flow;
+};
+
 struct YCtx {
     const dgen_tariff* tariffs;
     const dgen_switch* sw_rows;
@@ -918,6 +988,7 @@ struct YCtx {
     YSrc src;
     YLds S;
     YLoan loan;
+    YLast last;
     int lane, y, N;
     bool active;
 };
@@ -929,20 +1000,16 @@ __device__ __forceinline__ void yl_set_tariff(YCtx& c, int tix) {
     if (t.mo == 0) {
         __syncthreads();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.lane);
-        c.wo1 = yl_bill_mo0(t, c.S, 0.0, c.yearend);
+        c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);
     } else {
         c.wo1 = yl_bill_mo2(t, c.src, 1.0, false, c.S);
     }
 }
 
-struct YOut {   // written by the final evaluation; agent-major [agent][MAXY+1]
-    double *cash_flow, *cfev, *bw, *bwo;
-};
-
 // calc_system_performance(kw, en_batt=False) with lanes = years; returns -NPV
-// (wave-uniform).  With `out`, writes the arrays of this evaluation.
-__device__ __forceinline__ double yl_objective(YCtx& c, double kw, const YOut* out, int64_t i,
-                                               double* w1_out, YFlow* flow_out) {
+// (wave-uniform).  Every evaluation leaves its per-lane results in `c.last`:
+// after the search they are the outputs of the last evaluation (ff:449-474).
+__device__ __forceinline__ double yl_objective(YCtx& c, double kw) {
     double otc = 0.0;
     if (kw > 0.0) {
         int nt;
@@ -957,7 +1024,7 @@ __device__ __forceinline__ double yl_objective(YCtx& c, double kw, const YOut* o
     double total = ((c.capex * kw + 0.0) * c.ccm) + 0.0 + otc;     // ff:263,280-282
     double wb;
     if (t.mo == 0) {
-        wb = yl_bill_mo0(t, c.S, c.s_y * kws, c.yearend);
+        wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
     } else {
         c.src.gen_scale = kws;
         wb = yl_bill_mo2(t, c.src, c.s_y, true, c.S);
@@ -966,23 +1033,11 @@ __device__ __forceinline__ double yl_objective(YCtx& c, double kw, const YOut* o
     double wo = c.wo1 * c.r_y;
     double ev = wo - w;
     YFlow f = yl_cashflow(c.loan, total, ev, c.y, c.lane, c.active);
-    if (out) {
-        double* base = out->cash_flow + i * (MAXY + 1);
-        if (c.lane == 0) {
-            base[0] = -total;
-            out->cfev[i * (MAXY + 1)] = 0.0;
-            out->bw[i * (MAXY + 1)] = 0.0;
-            out->bwo[i * (MAXY + 1)] = 0.0;
-        }
-        if (c.active) {
-            base[c.y] = f.pb;
-            out->cfev[i * (MAXY + 1) + c.y] = ev;
-            out->bw[i * (MAXY + 1) + c.y] = w;
-            out->bwo[i * (MAXY + 1) + c.y] = wo;
-        }
-    }
-    if (w1_out) *w1_out = __shfl(w, 0, WAVE);
-    if (flow_out) *flow_out = f;
+    c.last.total = total;
+    c.last.ev = ev;
+    c.last.w = w;
+    c.last.wo = wo;
+    c.last.flow = f;
     return -f.npv;
 }
 
@@ -1055,17 +1110,27 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n) 
     double x_last = 0.0;
     double kw_star = brent_bounded(
         [&](double x) __attribute__((always_inline)) {
-            return yl_objective(c, x, nullptr, i, nullptr, nullptr);
+            return yl_objective(c, x);
         },
         low, high, xatol, &nfev, &x_last);
-    // ff:449-474: outputs of the LAST evaluation (re-run: deterministic, and the
-    // sticky switch is idempotent at the same x)
-    YOut yo{O.cash_flow, O.cfev_pv, O.bill_w_pv, O.bill_wo_pv};
-    double w1 = 0.0;
-    YFlow f;
-    double negnpv = yl_objective(c, x_last, &yo, i, &w1, &f);
+    const YLast& l = c.last;
+    const YFlow& f = l.flow;
+    const double w1 = __shfl(l.w, 0, WAVE);
+    const int64_t row = i * (MAXY + 1);
     if (lane == 0) {
-        O.npv[i] = -negnpv;
+        O.cash_flow[row] = -l.total;
+        O.cfev_pv[row] = 0.0;
+        O.bill_w_pv[row] = 0.0;
+        O.bill_wo_pv[row] = 0.0;
+    }
+    if (c.active) {
+        O.cash_flow[row + c.y] = f.pb;
+        O.cfev_pv[row + c.y] = l.ev;
+        O.bill_w_pv[row + c.y] = l.w;
+        O.bill_wo_pv[row + c.y] = l.wo;
+    }
+    if (lane == 0) {
+        O.npv[i] = f.npv;
         O.payback_raw[i] = f.payback;
         double pb = isfinite(f.payback) ? f.payback : 30.1;
         O.payback_period[i] = rint(pb * 10.0) / 10.0;
@@ -1120,8 +1185,8 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             S.G[m * half + p] = W.Gb[b];
         }
         __syncthreads();
-        wo1 = yl_bill_mo0(t, S, 0.0, cfg.nm_yearend_sell_rate);
-        wb = yl_bill_mo0(t, S, s_y, cfg.nm_yearend_sell_rate);
+        wo1 = yl_bill_nem(t, S, 0.0, cfg.nm_yearend_sell_rate);
+        wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
     } else {
         YSrc src;
         const int lr = A.load_row[i];
