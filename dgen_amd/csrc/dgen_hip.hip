@@ -384,15 +384,12 @@ __device__ __forceinline__ int32_t opaque_i(int32_t x) {
 // load_h - pv_h clamped at 0, re-derived from the raw registers (the opaque
 // copies keep the compiler from caching 48 converted doubles across passes).
 __device__ __forceinline__ double day_d(const DayRaw& r, int h, double ls, double cs6) {
-    double d = (double)opaque_f(r.s[h]) * ls - (double)opaque_i(r.c[h]) * cs6;
-    return d < 0.0 ? 0.0 : d;
+    return fmax((double)r.s[h] * ls - (double)r.c[h] * cs6, 0.0);
 }
 
 __device__ __forceinline__ double day_target(const DayRaw& r, double ls, double cs6, double power, double avail,
                              double dmax, double need0, int a_lo, int b_lo, double dmin_pos) {
     if (need0 <= avail) return 0.0;
-    ls = opaque(ls);
-    cs6 = opaque(cs6);
     if (dmax <= power) {
         // no hour saturates: convex water-filling, Newton from T = 0, exact once
         // the active count stops changing.  `mact` = min{d_h : d_h > t}: the
@@ -409,11 +406,11 @@ __device__ __forceinline__ double day_target(const DayRaw& r, double ls, double 
 #pragma unroll
             for (int h = 0; h < 24; h++) {
                 const double dh = day_d(r, h, ls, cs6);
-                double e = dh - tn;
+                const double e = dh - tn;
                 const bool on = e > 0.0;
                 an += on;
-                fn += on ? e : 0.0;
-                mn = (on && dh < mn) ? dh : mn;
+                fn += fmax(e, 0.0);
+                mn = fmin(mn, on ? dh : INFINITY);
             }
             if (an == a || fn <= avail || an == 0) break;
             f = fn;
@@ -431,11 +428,10 @@ __device__ __forceinline__ double day_target(const DayRaw& r, double ls, double 
         int am = 0, bm = 0;
 #pragma unroll
         for (int h = 0; h < 24; h++) {
-            double e = day_d(r, h, ls, cs6) - mid;
+            const double e = day_d(r, h, ls, cs6) - mid;
             am += e > 0.0;
             bm += (e - power) >= 0.0;
-            if (e < 0.0) e = 0.0;
-            f += e < power ? e : power;
+            f += fmin(fmax(e, 0.0), power);
         }
         if (f <= avail) { hi = mid; f_hi = f; a_hi = am; b_hi = bm; }
         else { lo = mid; a_lo = am; b_lo = bm; }
@@ -469,17 +465,12 @@ __device__ __forceinline__ HourStep batt_hour(double nn, double pv, double targe
                                               double inv_eta_in, double in_per_bank,
                                               double out_per_bank) {
     const bool chg = nn < 0.0;
-    double room = (cfg.batt_max_soc - soc) * bank * inv_eta_in;
-    room = room < 0.0 ? 0.0 : room;
-    double avail = (soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out;
-    avail = avail < 0.0 ? 0.0 : avail;
-    double cc = -nn;
-    cc = cc > power ? power : cc;
-    cc = cc > room ? room : cc;
-    double dd = nn - target;
-    dd = dd < 0.0 ? 0.0 : dd;
-    dd = dd > power ? power : dd;
-    dd = dd > avail ? avail : dd;
+    // clamps as v_min/v_max (they can differ from the oracle's ternaries only in
+    // the sign of a zero result, which no later sum or product can see)
+    const double room = fmax((cfg.batt_max_soc - soc) * bank * inv_eta_in, 0.0);
+    const double avail = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
+    const double cc = fmin(fmin(-nn, power), room);
+    const double dd = fmin(fmin(fmax(nn - target, 0.0), power), avail);
     // soc + cc*k  ==  soc + (-(dd*k')) exactly for the discharge branch
     const double dsoc = chg ? cc * in_per_bank : -(dd * out_per_bank);
     soc = soc + dsoc;
@@ -577,16 +568,15 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 int a0 = 0, b0 = 0;
 #pragma unroll
                 for (int hh = 0; hh < 24; hh++) {
-                    double dd = (double)r.s[hh] * ls - (double)r.c[hh] * cs6;
-                    if (dd < 0.0) dd = 0.0;
-                    if (dd > dmax) dmax = dd;
-                    need0 += dd < power ? dd : power;
-                    a0 += dd > 0.0;
+                    const double dd = fmax((double)r.s[hh] * ls - (double)r.c[hh] * cs6, 0.0);
+                    dmax = fmax(dmax, dd);
+                    need0 += fmin(dd, power);
+                    const bool on = dd > 0.0;
+                    a0 += on;
                     b0 += (dd - power) >= 0.0;
-                    dmin_pos = (dd > 0.0 && dd < dmin_pos) ? dd : dmin_pos;
+                    dmin_pos = fmin(dmin_pos, on ? dd : INFINITY);
                 }
-                double avail = (soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out;
-                if (avail < 0.0) avail = 0.0;
+                const double avail = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
                 target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0, dmin_pos);
             }
             const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);
@@ -603,7 +593,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 if constexpr (HOURLY) {
                     const double dn = ld - pl;
                     st_f32(ob + ho4, off4, (float)ld);
-                    st_f32(op + ho4, off4, (float)(dn > 0.0 ? dn : 0.0));
+                    st_f32(op + ho4, off4, (float)fmax(dn, 0.0));
                     st_f32(ow + ho4, off4, (float)st.g2l);
                 }
                 ho4 += row4;
