@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="size() pipeline depth (default: the library's DGEN_DEFAULT_CHUNKS)")
+    ap.add_argument("--caller-order", action="store_true",
+                    help="keep the generator's agent order on device (no profile_order grouping)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_bytes_per_agent.json"))
     return ap.parse_args()
 
@@ -100,15 +104,18 @@ def main():
     if ws > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from dgen_amd.engine import Engine
+    from dgen_amd.engine import Engine, profile_order
     from dgen_amd.synth import make_population
 
     pop = make_population(args.config, args.agents, seed=20260000 + 3 + 7919 * rank)
     eng = Engine(local if ws > 1 else 0)
+    if args.chunks is not None:
+        eng.set_pipeline(args.chunks)
     eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     eng.set_tariffs(pop.tariffs)
     eng.set_switches(pop.switches)
-    batch = eng.upload_agents(pop.cols, pop.n_scratch)
+    order = None if args.caller_order else profile_order(pop.cols)
+    batch = eng.upload_agents(pop.cols, pop.n_scratch, order=order)
     out = eng.alloc_outputs(batch.n, hourly=not args.no_hourly)
     c_out = eng.c_outputs(out)
     torch.cuda.synchronize()
@@ -176,6 +183,8 @@ def main():
             "config": {"workload": args.config, "agents_per_gpu": args.agents,
                        "global_agents": args.agents * ws,
                        "hourly_outputs": not args.no_hourly,
+                       "pipeline_chunks": eng.chunks,
+                       "device_order": "caller" if args.caller_order else "profile (cf_row, load_row)",
                        "parallelism": f"dp{ws} (agent shards, no collective in the step)",
                        "agents_with_status_errors": n_bad},
             "roofline": roof, "cpu_baseline": cpu,

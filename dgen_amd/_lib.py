@@ -97,10 +97,14 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
+ABI_VERSION = 2   # include/dgen_hip.h DGEN_ABI_VERSION
+DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
+
 EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
     "dgen_kernel_times", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
+    "dgen_set_pipeline",
 ]
 
 
@@ -142,9 +146,11 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.dgen_kernel_times.restype = _i32
     L.dgen_kernel_times.argtypes = [_vp, ctypes.POINTER(_f64), ctypes.POINTER(_f64),
                                     ctypes.POINTER(_f64)]
+    L.dgen_set_pipeline.restype = _i32
+    L.dgen_set_pipeline.argtypes = [_vp, _i32]
     L.dgen_segment_sums.restype = _i32
     L.dgen_segment_sums.argtypes = [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _vp, _i64, _vp, _vp]
-    if L.dgen_abi_version() != 1:
+    if L.dgen_abi_version() != ABI_VERSION:
         raise DgenError("libdgen_hip.so ABI version mismatch")
     _LIB = L
     return L

@@ -483,9 +483,10 @@ __device__ __forceinline__ HourStep batt_hour(double nn, double pv, double targe
 template <bool HOURLY>
 __global__ void __launch_bounds__(BLOCK, 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-              int64_t n_scratch) {
-    int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
+              int64_t n_scratch, int64_t i0, int64_t i1) {
+    // agents [i0, i1) of a batch of n (row stride of every plane stays n)
+    int64_t i = i0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= i1) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
     WsLayout W = ws_layout(ws, n);
     // battery-case bins: (load, system output) pairs per period, [p][BLOCK]
@@ -1032,8 +1033,8 @@ __device__ __forceinline__ double yl_objective(YCtx& c, double kw) {
 }
 
 __global__ void __launch_bounds__(WAVE)
-k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n) {
-    const int64_t i = blockIdx.x;
+k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0) {
+    const int64_t i = i0 + (int64_t)blockIdx.x;
     if (i >= n) return;
     const int lane = threadIdx.x;
     const int half = lds_half(T.max_periods);
@@ -1139,8 +1140,8 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n) 
 // Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
 __global__ void __launch_bounds__(WAVE)
 k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-                 int64_t n_scratch) {
-    const int64_t i = blockIdx.x;
+                 int64_t n_scratch, int64_t i0) {
+    const int64_t i = i0 + (int64_t)blockIdx.x;
     if (i >= n) return;
     const int st = O.status[i];
     if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH)) return;
@@ -1344,11 +1345,19 @@ __global__ void k_diffusion(dgen_diffusion_in in, dgen_diffusion_out out, int64_
 // ===========================================================================
 // C-ABI
 // ===========================================================================
+// Each dgen_size_agents call records, per chunk, five events: around k_size
+// on the caller's stream (0, 1) and around k_hourly_batt / k_batt_finance on
+// the ctx's second stream (2, 3, 4).  Kernel time = sum over chunks.
 struct dgen_ctx {
     int device;
     dgen_cfg cfg;
-    static constexpr int RING = 64;
-    hipEvent_t ev[RING][4];
+    static constexpr int RING = 16;
+    static constexpr int MAXCH = 16;
+    hipEvent_t ev[RING][MAXCH][5];
+    int nch[RING];     // chunks recorded in the slot
+    hipEvent_t fork, join;
+    hipStream_t s2;    // hourly + finance stream of the chunk pipeline
+    int chunks;        // pipeline depth (dgen_set_pipeline)
     int head;          // next ring slot to record
     int pending;       // recorded, not yet folded
     double sum_ms[3];
@@ -1356,11 +1365,17 @@ struct dgen_ctx {
 };
 
 static int fold_one(dgen_ctx* c, int slot) {
-    HIP_TRY(hipEventSynchronize(c->ev[slot][3]));
-    for (int k = 0; k < 3; k++) {
-        float ms = 0.f;
-        HIP_TRY(hipEventElapsedTime(&ms, c->ev[slot][k], c->ev[slot][k + 1]));
-        c->sum_ms[k] += ms;
+    const int k = c->nch[slot];
+    HIP_TRY(hipEventSynchronize(c->ev[slot][k - 1][4]));
+    for (int j = 0; j < k; j++) {
+        hipEvent_t* e = c->ev[slot][j];
+        float a = 0.f, b = 0.f, f = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]));
+        HIP_TRY(hipEventElapsedTime(&b, e[2], e[3]));
+        HIP_TRY(hipEventElapsedTime(&f, e[3], e[4]));
+        c->sum_ms[0] += a;
+        c->sum_ms[1] += b;
+        c->sum_ms[2] += f;
     }
     c->count++;
     return 0;
@@ -1394,16 +1409,21 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     c->device = device;
     c->cfg = *cfg;
     c->head = 0; c->pending = 0; c->count = 0;
+    c->chunks = DGEN_DEFAULT_CHUNKS;
     c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
-    for (int r = 0; r < dgen_ctx::RING; r++)
-        for (int k = 0; k < 4; k++) {
-            hipError_t e = hipEventCreate(&c->ev[r][k]);
-            if (e != hipSuccess) {
-                set_err("hipEventCreate failed: %s", hipGetErrorString(e));
-                delete c;
-                return DGEN_E_HIP;
-            }
-        }
+    hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
+    for (int r = 0; r < dgen_ctx::RING && e == hipSuccess; r++) {
+        c->nch[r] = 0;
+        for (int j = 0; j < dgen_ctx::MAXCH && e == hipSuccess; j++)
+            for (int k = 0; k < 5 && e == hipSuccess; k++) e = hipEventCreate(&c->ev[r][j][k]);
+    }
+    if (e != hipSuccess) {
+        set_err("dgen_open: stream/event creation failed: %s", hipGetErrorString(e));
+        delete c;   // leaks the handles created so far; the process is failing anyway
+        return DGEN_E_HIP;
+    }
     *out = c;
     return DGEN_OK;
 }
@@ -1411,8 +1431,13 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
 int32_t dgen_close(dgen_ctx* c) {
     if (!c) return DGEN_OK;
     (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->s2);
     for (int r = 0; r < dgen_ctx::RING; r++)
-        for (int k = 0; k < 4; k++) (void)hipEventDestroy(c->ev[r][k]);
+        for (int j = 0; j < dgen_ctx::MAXCH; j++)
+            for (int k = 0; k < 5; k++) (void)hipEventDestroy(c->ev[r][j][k]);
+    (void)hipEventDestroy(c->fork);
+    (void)hipEventDestroy(c->join);
+    (void)hipStreamDestroy(c->s2);
     delete c;
     return DGEN_OK;
 }
@@ -1503,24 +1528,57 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         if (r) return r;
         c->pending--;
     }
+    // chunk pipeline: k_size of chunk j+1 (fp64 VALU / latency bound) runs on
+    // the caller's stream while k_hourly_batt + k_batt_finance of chunk j (HBM
+    // bound) run on s2; chunk boundaries are multiples of BLOCK so every wave's
+    // hour-row stores stay one contiguous 256 B segment.
+    int nch = c->chunks;
+    if (nch < 1) nch = 1;
+    if (nch > dgen_ctx::MAXCH) nch = dgen_ctx::MAXCH;
+    int64_t csz = (n + nch - 1) / nch;
+    csz = ((csz + BLOCK - 1) / BLOCK) * BLOCK;
+    nch = (int)((n + csz - 1) / csz);
     int slot = c->head;
     c->head = (c->head + 1) % dgen_ctx::RING;
     c->pending++;
-    dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK)), block(BLOCK);
+    c->nch[slot] = nch;
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK;
-    HIP_TRY(hipEventRecord(c->ev[slot][0], s));
     const size_t ylds = ylds_bytes(lds_half(T->max_periods));
-    hipLaunchKernelGGL(k_size_w, dim3((unsigned)n), dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n);
-    HIP_TRY(hipEventRecord(c->ev[slot][1], s));
-    if (hourly)
-        hipLaunchKernelGGL(k_hourly_batt<true>, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
-    else
-        hipLaunchKernelGGL(k_hourly_batt<false>, grid, block, lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch);
-    HIP_TRY(hipEventRecord(c->ev[slot][2], s));
-    hipLaunchKernelGGL(k_batt_finance_w, dim3((unsigned)n), dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n,
-                       ws, n_scratch);
-    HIP_TRY(hipEventRecord(c->ev[slot][3], s));
+    hipStream_t s2 = c->s2;
+    HIP_TRY(hipEventRecord(c->fork, s));
+    HIP_TRY(hipStreamWaitEvent(s2, c->fork, 0));
+    for (int j = 0; j < nch; j++) {
+        const int64_t i0 = (int64_t)j * csz, i1 = (i0 + csz < n) ? i0 + csz : n, m = i1 - i0;
+        hipEvent_t* e = c->ev[slot][j];
+        HIP_TRY(hipEventRecord(e[0], s));
+        hipLaunchKernelGGL(k_size_w, dim3((unsigned)m), dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0);
+        HIP_TRY(hipEventRecord(e[1], s));
+        HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
+        HIP_TRY(hipEventRecord(e[2], s2));
+        dim3 grid((unsigned)((m + BLOCK - 1) / BLOCK)), block(BLOCK);
+        if (hourly)
+            hipLaunchKernelGGL(k_hourly_batt<true>, grid, block, lds, s2, *T, *A, *O, c->cfg, n, ws,
+                               n_scratch, i0, i1);
+        else
+            hipLaunchKernelGGL(k_hourly_batt<false>, grid, block, lds, s2, *T, *A, *O, c->cfg, n, ws,
+                               n_scratch, i0, i1);
+        HIP_TRY(hipEventRecord(e[3], s2));
+        hipLaunchKernelGGL(k_batt_finance_w, dim3((unsigned)m), dim3(WAVE), ylds, s2, *T, *A, *O,
+                           c->cfg, n, ws, n_scratch, i0);
+        HIP_TRY(hipEventRecord(e[4], s2));
+    }
+    HIP_TRY(hipEventRecord(c->join, s2));
+    HIP_TRY(hipStreamWaitEvent(s, c->join, 0));
     HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_set_pipeline(dgen_ctx* c, int32_t chunks) {
+    if (!c || chunks < 1 || chunks > dgen_ctx::MAXCH) {
+        set_err("dgen_set_pipeline: chunks must be in [1, %d]", dgen_ctx::MAXCH);
+        return DGEN_E_ARG;
+    }
+    c->chunks = chunks;
     return DGEN_OK;
 }
 

@@ -35,6 +35,20 @@ class AgentBatch:
     cols: Dict[str, object]          # name -> device tensor
     workspace: object                # uint8 device tensor
     c_agents: _lib.Agents = field(default=None)
+    # device row j holds caller agent perm[j] (None: caller order)
+    perm: Optional[np.ndarray] = None
+
+
+def profile_order(cols: Dict[str, np.ndarray]) -> np.ndarray:
+    """Device order for a batch: agents grouped by (cf_row, load_row).
+
+    k_hourly_batt runs one agent per lane and streams the agent's two profile
+    rows day by day; when the 64 lanes of a wave share a cf row its loads are
+    one broadcast line instead of 64, and the load-shape lines of a group stay
+    hot in L2.  The reference's agent order carries no
+    meaning (size_chunk returns rows keyed by agent_id, ff:1149-1218), so the
+    host columnarizer is free to choose it.  Stable, so ties keep caller order."""
+    return np.lexsort((np.asarray(cols["load_row"]), np.asarray(cols["cf_row"]))).astype(np.int64)
 
 
 class Engine:
@@ -52,6 +66,7 @@ class Engine:
         _lib.check(self.lib.dgen_open(self.device, ctypes.byref(c), ctypes.byref(h)), "dgen_open")
         self.ctx = h
         self.tables = _lib.Tables()
+        self.chunks = _lib.DEFAULT_CHUNKS
         self._keep: Dict[str, object] = {}
 
     # ------------------------------------------------------------------ utils
@@ -137,9 +152,18 @@ class Engine:
         return (self._keep["shape_sum"].cpu().numpy(), self._keep["cf_naep"].cpu().numpy())
 
     # ------------------------------------------------------------------ batch
-    def upload_agents(self, cols: Dict[str, np.ndarray], n_scratch: Optional[int] = None) -> AgentBatch:
+    def upload_agents(self, cols: Dict[str, np.ndarray], n_scratch: Optional[int] = None,
+                      order: Optional[np.ndarray] = None) -> AgentBatch:
+        """Upload agent columns.  `order` (a permutation, e.g. profile_order(cols))
+        lays the batch out on device as cols[...][order]; outputs then come back in
+        that order and outputs_to_host(out, batch.perm) restores caller order."""
         torch = _torch()
         n = len(cols["load_kwh"])
+        if order is not None:
+            order = np.asarray(order, dtype=np.int64)
+            if order.shape != (n,) or not np.array_equal(np.sort(order), np.arange(n)):
+                raise ValueError("order must be a permutation of range(n)")
+            cols = {k: np.asarray(v)[order] for k, v in cols.items()}
         dev = {}
         tmap = {"int32": torch.int32, "uint8": torch.uint8, "float64": torch.float64}
         for name, dt in _lib.AGENT_COLUMNS:
@@ -158,7 +182,7 @@ class Engine:
         wsb = int(self.lib.dgen_workspace_bytes(n, n_scratch))
         ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
         ca = _lib.Agents(**{name: _ptr(dev[name]) for name, _ in _lib.AGENT_COLUMNS})
-        return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca)
+        return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order)
 
     def validate_agents(self, dev, n):
         """Host-side bounds checks before any kernel indexes a table."""
@@ -208,6 +232,11 @@ class Engine:
                                              batch.workspace.numel(), batch.n_scratch,
                                              self.stream_handle()),
                    "dgen_size_agents")
+
+    def set_pipeline(self, chunks: int):
+        """Chunk-pipeline depth of size() (dgen_set_pipeline; 1 = no overlap)."""
+        _lib.check(self.lib.dgen_set_pipeline(self.ctx, int(chunks)), "dgen_set_pipeline")
+        self.chunks = int(chunks)
 
     def kernel_times(self):
         """Average per-launch device time (ms) of the three sizing kernels over
@@ -262,8 +291,9 @@ class Engine:
         return xs.cpu().numpy(), xo.cpu().numpy(), nf.cpu().numpy()
 
 
-def outputs_to_host(out: Dict[str, object]) -> Dict[str, np.ndarray]:
-    """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly)."""
+def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
+    """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly),
+    in caller order when `perm` (AgentBatch.perm) is given."""
     res = {}
     for name, _ in _lib.OUTPUT_SCALARS:
         res[name] = out[name].cpu().numpy()
@@ -272,4 +302,10 @@ def outputs_to_host(out: Dict[str, object]) -> Dict[str, np.ndarray]:
     for name in _lib.OUTPUT_HOURLY:
         t = out.get(name)
         res[name] = None if t is None else t.cpu().numpy().T.copy()
+    if perm is not None:
+        for k, v in res.items():
+            if v is not None:
+                u = np.empty_like(v)
+                u[perm] = v
+                res[k] = u
     return res

@@ -139,16 +139,16 @@ def size_rows(rows, con, rate_switch_table, hourly: str = "list"):
     b = _columnarize(rows, src, rate_switch_table)
     cols = b.columns()
     eng = get_engine()
-    from .engine import outputs_to_host
+    from .engine import outputs_to_host, profile_order
     import torch
     eng.load_profiles(src.shapes, src.cfs, b.wholesale.array())
     eng.set_tariffs(b.tariffs.array())
     eng.set_switches(b.switches.array())
-    batch = eng.upload_agents(cols)
+    batch = eng.upload_agents(cols, order=profile_order(cols))
     out = eng.alloc_outputs(batch.n, hourly=True)
     eng.size(batch, out)
     torch.cuda.synchronize(eng.dev)
-    o = outputs_to_host(out)
+    o = outputs_to_host(out, batch.perm)
     ids = [r.get("agent_id", r.name) for r in rows]
     _raise_for_status(o["status"], ids)
     cfs = src.cfs

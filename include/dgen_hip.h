@@ -37,7 +37,8 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 1
+#define DGEN_ABI_VERSION 2
+#define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_NH    8760   /* hours per year                                    */
 #define DGEN_NSLOT 576    /* 12 months x {weekday, weekend} x 24 hours         */
 #define DGEN_MAXP  12     /* TOU periods                                        */
@@ -285,9 +286,19 @@ typedef struct {
 int32_t dgen_diffusion(dgen_ctx* ctx, const dgen_diffusion_in* in, const dgen_diffusion_out* out,
                        int64_t n, int32_t is_first_year, void* stream);
 
-/* Per-kernel timing of the most recent dgen_size_agents call on this context
- * (HIP events recorded on the launch stream; milliseconds).                   */
+/* Average per-call kernel time (ms) of the dgen_size_agents calls since the
+ * previous query: k_size, k_hourly_batt, k_batt_finance, each summed over the
+ * call's chunks (HIP events recorded on the stream each kernel runs on).
+ * Returns the number of calls averaged (>= 0) or an error code.              */
 int32_t dgen_kernel_times(dgen_ctx* ctx, double* ms_size, double* ms_hourly, double* ms_finance);
+
+/* Pipeline depth of dgen_size_agents: the batch is cut into `chunks` pieces;
+ * k_size of piece j+1 runs on the caller's stream while k_hourly_batt and
+ * k_batt_finance of piece j run on a context-owned second stream (forked from
+ * and joined back into the caller's stream, so stream order is unchanged for
+ * the caller).  1 = no overlap.  Range [1, 16]; default DGEN_DEFAULT_CHUNKS.
+ * Replaces nothing in the reference (its per-agent loop is serial, ff:1149). */
+int32_t dgen_set_pipeline(dgen_ctx* ctx, int32_t chunks);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Build kernel variants for A/B timing (diagnostic only; outputs are wrong
-by construction).  Each variant is a text edit of a temporary copy of the
-source; nothing here is part of the product build."""
+"""Build kernel variants for A/B timing into dgen_amd/lib/ablate/ (diagnostic
+only: occupancy variants compute the same results, the no_* variants are
+wrong by construction).  Each variant is a text edit of a temporary copy of
+the source; nothing here is part of the product build.  Run a variant with
+DGEN_LIB=dgen_amd/lib/ablate/libdgen_<name>.so python bench.py ..."""
 import os
 import subprocess
 import sys
@@ -12,15 +14,27 @@ OUT = os.path.join(REPO, "dgen_amd", "lib", "ablate")
 sys.path.insert(0, REPO)
 from dgen_amd.build import FLAGS, hipcc  # noqa: E402
 
+HB = "__global__ void __launch_bounds__(BLOCK, 2)\nk_hourly_batt("
+KS = "__global__ void __launch_bounds__(WAVE)\nk_size_w("
+
+
+def occ(decl, w):
+    head = decl.split("\n")[0].split("__launch_bounds__")[0]
+    lb = "__launch_bounds__(BLOCK)" if "BLOCK" in decl else "__launch_bounds__(WAVE)"
+    return head + lb + f" __attribute__((amdgpu_waves_per_eu({w}, {w})))\n" + decl.split("\n")[1]
+
+
 VARIANTS = {
     "base": [],
-    "no_target": [("target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0);",
-                   "target = 0.0; asm volatile(\"\" :: \"v\"(need0), \"v\"(dmax), \"v\"(a0), \"v\"(b0));")],
-    "no_hourly_stores": [("if (o_base) o_base[h * n + i] = (float)ld;", "asm volatile(\"\" :: \"v\"(ld));"),
-                         ("o_pvo[h * n + i] = (float)(dn > 0.0 ? dn : 0.0);", "asm volatile(\"\" :: \"v\"(dn));"),
-                         ("if (o_wb) o_wb[h * n + i] = (float)g2l;", "asm volatile(\"\" :: \"v\"(g2l));")],
-    "no_bins": [("acc.at(p) += ld;\n                    acc.hi(p) += sys;",
-                 "asm volatile(\"\" :: \"v\"(ld), \"v\"(sys), \"v\"(p));")],
+    "hb_w3": [(HB, occ(HB, 3))],
+    "hb_w4": [(HB, occ(HB, 4))],
+    "ks_w4": [(KS, occ(KS, 4))],
+    "ks_w5": [(KS, occ(KS, 5))],
+    "no_target": [("target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0, dmin_pos);",
+                   "target = 0.0; asm volatile(\"\" :: \"v\"(need0), \"v\"(dmax), \"v\"(a0), \"v\"(b0), \"v\"(avail), \"v\"(dmin_pos));")],
+    "no_hourly_stores": [("st_f32(ob + ho4, off4, (float)ld);", "asm volatile(\"\" :: \"v\"(ld));"),
+                         ("st_f32(op + ho4, off4, (float)fmax(dn, 0.0));", "asm volatile(\"\" :: \"v\"(dn));"),
+                         ("st_f32(ow + ho4, off4, (float)st.g2l);", "asm volatile(\"\" :: \"v\"(st.g2l));")],
 }
 
 
@@ -28,16 +42,17 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     src = open(SRC).read().replace('#include "../../include/dgen_hip.h"',
                                    f'#include "{REPO}/include/dgen_hip.h"')
-    for name, edits in VARIANTS.items():
+    names = sys.argv[1:] or list(VARIANTS)
+    for name in names:
         s = src
-        for a, b in edits:
-            assert a in s, (name, a[:40])
+        for a, b in VARIANTS[name]:
+            assert a in s, (name, a[:60])
             s = s.replace(a, b)
         tmp = f"/tmp/ablate_{name}.hip"
         open(tmp, "w").write(s)
         out = os.path.join(OUT, f"libdgen_{name}.so")
         subprocess.run([hipcc(), *FLAGS, "-o", out, tmp], check=True)
-        print("built", out)
+        print("built", out, flush=True)
 
 
 if __name__ == "__main__":

@@ -30,7 +30,9 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(L, name), name
     assert set(names) == set(_lib.EXPORTED)
-    assert L.dgen_abi_version() == 1
+    assert L.dgen_abi_version() == _lib.ABI_VERSION == 2
+    m = re.search(r"#define DGEN_DEFAULT_CHUNKS\s+(\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == _lib.DEFAULT_CHUNKS
 
 
 def test_workspace_bytes_formula():

@@ -61,3 +61,58 @@ def test_synthetic_population_matches_oracle(engine, cfg, n):
             assert np.allclose(o[k_o][i], ref_h, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(ref_h).max())), (i, k_o)
     if cfg != "ca_res_storage":
         assert n_switch > 0          # the population exercises the DG switch
+
+
+@pytest.mark.parametrize("cfg,n", [("national_mixed", 3000), ("ca_res_storage", 2000)])
+def test_profile_order_is_invisible(engine, cfg, n):
+    """The device layout chosen by profile_order (agents grouped by cf/load row)
+    returns, after outputs_to_host(out, perm), exactly the caller-order result."""
+    from dgen_amd.engine import profile_order
+    pop = _small_pop(cfg, n)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    res = []
+    for order in (None, profile_order(pop.cols)):
+        batch = engine.upload_agents(pop.cols, pop.n_scratch, order=order)
+        if order is not None:
+            rows = pop.cols["cf_row"][batch.perm]
+            assert (np.diff(rows) >= 0).all()
+        out = engine.alloc_outputs(batch.n, hourly=True)
+        engine.size(batch, out)
+        torch.cuda.synchronize()
+        res.append(outputs_to_host(out, batch.perm))
+    a, b = res
+    for k in a:
+        if a[k] is None:
+            continue
+        assert np.array_equal(a[k], b[k], equal_nan=True), k
+
+
+def test_pipeline_depth_is_invisible(engine):
+    """Chunking the batch across the two-stream pipeline (k_size of chunk j+1
+    beside k_hourly_batt / k_batt_finance of chunk j) changes no output bit,
+    including a batch size that is not a multiple of the block size."""
+    pop = _small_pop("national_mixed", 3001)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    res = []
+    engine.kernel_times()            # drain calls made by earlier tests
+    try:
+        for chunks in (1, 7, 16):
+            engine.set_pipeline(chunks)
+            out = engine.alloc_outputs(batch.n, hourly=True)
+            engine.size(batch, out)
+            torch.cuda.synchronize()
+            res.append(outputs_to_host(out))
+            _, _, _, cnt = engine.kernel_times()
+            assert cnt == 1
+    finally:
+        from dgen_amd import _lib
+        engine.set_pipeline(_lib.DEFAULT_CHUNKS)
+    for r in res[1:]:
+        for k in r:
+            if r[k] is not None:
+                assert np.array_equal(res[0][k], r[k], equal_nan=True), k
