@@ -69,7 +69,7 @@ AGENT_COLUMNS = [
 
 
 class Agents(ctypes.Structure):
-    _fields_ = [(name, _vp) for name, _ in AGENT_COLUMNS]
+    _fields_ = [(name, _vp) for name, _ in AGENT_COLUMNS] + [("max_years", _i32)]
 
 
 OUTPUT_SCALARS = [

@@ -641,20 +641,48 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
 // ===========================================================================
 constexpr int WAVE = 64;
 
-__device__ __forceinline__ double wave_sum(double v) {
-    // fixed butterfly, then lane 0's value for every lane (wave-uniform result)
+// An agent's lanes: LPA = 64 (one agent per wave, analysis periods up to
+// DGEN_MAXY years) or 32 (two agents per wave, periods up to 32 years -- the
+// reference's 25-year life fills 25 of 32 lanes instead of 25 of 64).  Every
+// per-agent quantity is uniform over its segment; reductions stay inside it.
+template <int LPA>
+struct Seg {
+    int lane;   // 0..63
+    int sl;     // lane within the segment (year - 1)
+    int base;   // first lane of the segment
+    __device__ explicit Seg(int l)
+        : lane(l), sl(LPA == WAVE ? l : (l & (LPA - 1))), base(LPA == WAVE ? 0 : (l & ~(LPA - 1))) {}
+    // fixed butterfly, then the segment's first lane's value (segment-uniform);
+    // lanes past the analysis period hold 0, so the result does not depend on LPA
+    __device__ __forceinline__ double sum(double v) const {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-    return __shfl(v, 0, WAVE);
-}
-
-__device__ __forceinline__ double wave_incl_scan(double v, int lane) {
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        double t = __shfl_up(v, o, WAVE);
-        if (lane >= o) v += t;
+        for (int o = LPA / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+        return __shfl(v, base, WAVE);
     }
-    return v;
+    __device__ __forceinline__ double incl_scan(double v) const {
+#pragma unroll
+        for (int o = 1; o < LPA; o <<= 1) {
+            double t = __shfl_up(v, o, WAVE);
+            if (sl >= o) v += t;
+        }
+        return v;
+    }
+    // first segment lane where pred holds, or -1
+    __device__ __forceinline__ int first(bool pred) const {
+        unsigned long long m = __ballot(pred);
+        if (LPA < WAVE) m = (m >> base) & ((1ull << LPA) - 1ull);
+        return m ? __ffsll((long long)m) - 1 : -1;
+    }
+    __device__ __forceinline__ double bcast(double v, int k) const { return __shfl(v, base + k, WAVE); }
+};
+
+// LDS hand-off between the lanes of one wave (every year-lane block is one
+// wave): orders the LDS stores before the loads without s_barrier, so it is
+// also correct where the two agents of a wave have diverged.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ double pow_seq(double b, int e) {   // 1 * b * b ... (e times)
@@ -664,9 +692,11 @@ __device__ __forceinline__ double pow_seq(double b, int e) {   // 1 * b * b ... 
 }
 
 // Per-block LDS (one wave):
-//   bins  L[12 * half], G[12 * half]         (wave-uniform, broadcast reads)
-//   lane  [4 * half][WAVE]                    (per-lane per-period state)
+//   tariff [WAVE / LPA][dgen_tariff]                 (LPA < WAVE: staged copy, see stage_tariff)
+//   bins  [WAVE / LPA][L[12 * half], G[12 * half]]  (segment-uniform, broadcast reads)
+//   lane  [4 * half][WAVE]                          (per-lane per-period state)
 struct YLds {
+    dgen_tariff* trf;   // the segment's staged tariff (LPA < WAVE only)
     double* L;
     double* G;
     double* lane;   // lane column base (already offset by lane)
@@ -674,17 +704,47 @@ struct YLds {
     __device__ double& at(int k) const { return lane[k * WAVE]; }
 };
 
-__host__ __device__ inline size_t ylds_bytes(int half) {
-    return sizeof(double) * ((size_t)24 * half + (size_t)4 * half * WAVE);
+static_assert(sizeof(dgen_tariff) % sizeof(double) == 0, "tariff staging copies qwords");
+constexpr int TRF_QW = (int)(sizeof(dgen_tariff) / sizeof(double));
+
+__host__ __device__ inline size_t ylds_bytes(int half, int lpa) {
+    const size_t trf = lpa < WAVE ? (size_t)(WAVE / lpa) * sizeof(dgen_tariff) : 0;
+    return trf + sizeof(double) * ((size_t)24 * half * (WAVE / lpa) + (size_t)4 * half * WAVE);
 }
 
-__device__ __forceinline__ YLds ylds_make(double* base, int half, int lane) {
+template <int LPA>
+__device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>& g) {
     YLds y;
-    y.L = base;
-    y.G = base + 12 * half;
-    y.lane = base + 24 * half + lane;
+    y.trf = nullptr;
+    if (LPA < WAVE) {
+        y.trf = reinterpret_cast<dgen_tariff*>(base) + g.lane / LPA;
+        base += (WAVE / LPA) * TRF_QW;
+    }
+    y.L = base + (LPA == WAVE ? 0 : (g.lane / LPA) * 24 * half);
+    y.G = y.L + 12 * half;
+    y.lane = base + (WAVE / LPA) * 24 * half + g.lane;
     y.half = half;
     return y;
+}
+
+// The tariff a year-lane agent bills with.  With one agent per wave the
+// global record is wave-uniform and read through the scalar cache; with two
+// agents per wave its address is per-lane, so every field read would be a
+// vector load waited on in the middle of the month recursion -- the segment
+// copies the record (1808 B) into its LDS slot once and reads it from there.
+template <int LPA>
+__device__ __forceinline__ const dgen_tariff* stage_tariff(const dgen_tariff* src, const YLds& S,
+                                                          const Seg<LPA>& g) {
+    if constexpr (LPA == WAVE) {
+        return src;
+    } else {
+        wave_lds_sync();
+        const double* s = reinterpret_cast<const double*>(src);
+        double* d = reinterpret_cast<double*>(S.trf);
+        for (int k = g.sl; k < TRF_QW; k += LPA) d[k] = s[k];
+        wave_lds_sync();
+        return S.trf;
+    }
 }
 
 // month energy charge from the lane's billed kWh u_p = at(uoff + p)
@@ -851,11 +911,12 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
 }
 
 // bins of a tariff from a row's slot sums, one (month, period) cell per lane
+template <int LPA>
 __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
                                               const double* __restrict__ gslots, double load_scale,
-                                              const YLds& S, int lane) {
+                                              const YLds& S, const Seg<LPA>& g) {
     const int P = t.P;
-    for (int cell = lane; cell < 12 * P; cell += WAVE) {
+    for (int cell = g.sl; cell < 12 * P; cell += LPA) {
         int m = cell / P, p = cell % P;
         double la = 0.0, ga = 0.0;
         for (int dt = 0; dt < 2; dt++) {
@@ -871,7 +932,7 @@ __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double
         S.L[m * S.half + p] = la * load_scale;
         S.G[m * S.half + p] = ga;
     }
-    __syncthreads();
+    wave_lds_sync();
 }
 
 // Per-agent loan constants (wave-uniform) + per-lane year factors.
@@ -914,8 +975,9 @@ struct YFlow {
 };
 
 // Cash flow of one lane's year + the wave reductions (Cashloan subset).
-__device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev, int y, int lane,
-                                             bool active) {
+template <int LPA>
+__device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev, int y,
+                                             const Seg<LPA>& g, bool active) {
     double debt = L.debt_frac * C;
     double pmt = 0.0;
     if (L.term > 0 && debt != 0.0) {
@@ -948,13 +1010,12 @@ __device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev
     double pb = ev - oe + taxsav;
     if (!active) { atcf = 0.0; pb = 0.0; }
     YFlow f;
-    f.npv = -(C - debt) + wave_sum(atcf * L.df);
-    double cum = -C + wave_incl_scan(pb, lane);
-    unsigned long long hit = __ballot(active && cum > 0.0);
+    f.npv = -(C - debt) + g.sum(atcf * L.df);
+    double cum = -C + g.incl_scan(pb);
+    const int k = g.first(active && cum > 0.0);          // first paying year - 1
     f.payback = 1e99;
-    if (hit) {
-        int k = __ffsll((long long)hit) - 1;              // first paying lane
-        double cum_k = __shfl(cum, k, WAVE), pb_k = __shfl(pb, k, WAVE);
+    if (k >= 0) {
+        double cum_k = g.bcast(cum, k), pb_k = g.bcast(pb, k);
         f.payback = (pb_k != 0.0) ? (double)(k + 1) - cum_k / pb_k : (double)(k + 1) - 0.5;
     }
     f.pb = pb;
@@ -966,8 +1027,10 @@ struct YLast {   // per-lane results of the most recent evaluation
     YFlow flow;
 };
 
+template <int LPA>
 struct YCtx {
     const dgen_tariff* tariffs;
+    const dgen_tariff* tp;      // current tariff (global record or LDS copy)
     const dgen_switch* sw_rows;
     int sw_cnt;
     int tariff, switched, status;
@@ -980,17 +1043,21 @@ struct YCtx {
     YLds S;
     YLoan loan;
     YLast last;
-    int lane, y, N;
+    Seg<LPA> g;
+    int y, N;
     bool active;
+    __device__ explicit YCtx(int lane) : g(lane) {}
 };
 
-__device__ __forceinline__ void yl_set_tariff(YCtx& c, int tix) {
-    const dgen_tariff& t = c.tariffs[tix];
+template <int LPA>
+__device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
+    c.tp = stage_tariff(c.tariffs + tix, c.S, c.g);
+    const dgen_tariff& t = *c.tp;
     c.tariff = tix;
     c.status |= t.flags;
     if (t.mo == 0) {
-        __syncthreads();
-        yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.lane);
+        wave_lds_sync();
+        yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);
     } else {
         c.wo1 = yl_bill_mo2(t, c.src, 1.0, false, c.S);
@@ -1000,7 +1067,8 @@ __device__ __forceinline__ void yl_set_tariff(YCtx& c, int tix) {
 // calc_system_performance(kw, en_batt=False) with lanes = years; returns -NPV
 // (wave-uniform).  Every evaluation leaves its per-lane results in `c.last`:
 // after the search they are the outputs of the last evaluation (ff:449-474).
-__device__ __forceinline__ double yl_objective(YCtx& c, double kw) {
+template <int LPA>
+__device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double otc = 0.0;
     if (kw > 0.0) {
         int nt;
@@ -1010,7 +1078,7 @@ __device__ __forceinline__ double yl_objective(YCtx& c, double kw) {
             if (nt != c.tariff) yl_set_tariff(c, nt);
         }
     }
-    const dgen_tariff& t = c.tariffs[c.tariff];
+    const dgen_tariff& t = *c.tp;
     double kws = ((kw * 1000.0) * 0.96) / 1000.0;                  // ff:118-120
     double total = ((c.capex * kw + 0.0) * c.ccm) + 0.0 + otc;     // ff:263,280-282
     double wb;
@@ -1023,7 +1091,7 @@ __device__ __forceinline__ double yl_objective(YCtx& c, double kw) {
     double w = wb * c.r_y;
     double wo = c.wo1 * c.r_y;
     double ev = wo - w;
-    YFlow f = yl_cashflow(c.loan, total, ev, c.y, c.lane, c.active);
+    YFlow f = yl_cashflow(c.loan, total, ev, c.y, c.g, c.active);
     c.last.total = total;
     c.last.ev = ev;
     c.last.w = w;
@@ -1032,16 +1100,19 @@ __device__ __forceinline__ double yl_objective(YCtx& c, double kw) {
     return -f.npv;
 }
 
-__global__ void __launch_bounds__(WAVE)
-k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0) {
-    const int64_t i = i0 + (int64_t)blockIdx.x;
-    if (i >= n) return;
+// occupancy floor of 3 waves per SIMD (<= 168 VGPRs): the 32-lane variant
+// otherwise takes 181 and runs 2 (measured 23.3 -> 18.6 ms at 1M agents)
+template <int LPA>
+__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3)))
+k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1) {
     const int lane = threadIdx.x;
+    const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
+    if (i >= i1) return;
     const int half = lds_half(T.max_periods);
-    YCtx c;
-    c.lane = lane;
-    c.y = lane + 1;
-    c.S = ylds_make(dyn_lds, half, lane);
+    YCtx<LPA> c(lane);
+    const int sl = c.g.sl;
+    c.y = sl + 1;
+    c.S = ylds_make(dyn_lds, half, c.g);
     c.tariffs = T.tariffs;
     c.sw_rows = T.switches + A.sw_solar_off[i];
     c.sw_cnt = A.sw_solar_cnt[i];
@@ -1077,7 +1148,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.src.ts_mult = A.price_mult[i];
 
     bool bad = false;
-    if (c.N < 1 || c.N > MAXY) { c.status |= DGEN_ST_YEARS; bad = true; }
+    if (c.N < 1 || c.N > MAXY || c.N > LPA) { c.status |= DGEN_ST_YEARS; bad = true; }
     if (t0 < 0 || t0 >= T.n_tariffs) { c.status |= DGEN_ST_TARIFF; bad = true; }
     const double max_load = c.kwh / naep0;                         // ff:440-444
     const double low = max_load * 0.8, high = max_load * 1.25;
@@ -1088,7 +1159,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     if (!isfinite(low) || !isfinite(high)) { c.status |= DGEN_ST_BOUNDS; bad = true; }
     if (c.kwh == 0.0) c.status |= DGEN_ST_ZERO_LOAD;
     if (bad) {
-        if (lane == 0) {
+        if (sl == 0) {
             O.status[i] = c.status;
             O.nfev[i] = 0;
             O.system_kw[i] = NAN; O.x_last[i] = NAN; O.npv[i] = NAN;
@@ -1106,9 +1177,9 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         low, high, xatol, &nfev, &x_last);
     const YLast& l = c.last;
     const YFlow& f = l.flow;
-    const double w1 = __shfl(l.w, 0, WAVE);
+    const double w1 = c.g.bcast(l.w, 0);
     const int64_t row = i * (MAXY + 1);
-    if (lane == 0) {
+    if (sl == 0) {
         O.cash_flow[row] = -l.total;
         O.cfev_pv[row] = 0.0;
         O.bill_w_pv[row] = 0.0;
@@ -1120,7 +1191,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         O.bill_w_pv[row + c.y] = l.w;
         O.bill_wo_pv[row + c.y] = l.wo;
     }
-    if (lane == 0) {
+    if (sl == 0) {
         O.npv[i] = f.npv;
         O.payback_raw[i] = f.payback;
         double pb = isfinite(f.payback) ? f.payback : 30.1;
@@ -1138,23 +1209,25 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
 }
 
 // Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
+template <int LPA>
 __global__ void __launch_bounds__(WAVE)
 k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-                 int64_t n_scratch, int64_t i0) {
-    const int64_t i = i0 + (int64_t)blockIdx.x;
-    if (i >= n) return;
+                 int64_t n_scratch, int64_t i0, int64_t i1) {
+    const int lane = threadIdx.x;
+    const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
+    if (i >= i1) return;
     const int st = O.status[i];
     if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH)) return;
-    const int lane = threadIdx.x;
-    const int y = lane + 1;
+    const Seg<LPA> g(lane);
+    const int y = g.sl + 1;
     const int half = lds_half(T.max_periods);
-    YLds S = ylds_make(dyn_lds, half, lane);
+    YLds S = ylds_make(dyn_lds, half, g);
     WsLayout W = ws_layout(ws, n);
     const bool is_res = (A.flags[i] & 1) != 0;
     const bool is_ca = (A.flags[i] & 2) != 0;
     const int N = A.econ_life[i];
     const bool active = y <= N;
-    const dgen_tariff& t = T.tariffs[O.tariff_final[i]];
+    const dgen_tariff& t = *stage_tariff(T.tariffs + O.tariff_final[i], S, g);
     const double kw = O.system_kw[i];
     const double bank = O.batt_kwh[i];
     const double otc = W.otc_b[i];
@@ -1169,13 +1242,13 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     const bool mo2 = t.mo == 2;
     double wo1, wb;
     if (!mo2) {
-        for (int cell = lane; cell < 12 * t.P; cell += WAVE) {
+        for (int cell = g.sl; cell < 12 * t.P; cell += LPA) {
             int m = cell / t.P, p = cell % t.P;
             int64_t b = (int64_t)(m * MAXP + p) * n + i;
             S.L[m * half + p] = W.Lb[b];
             S.G[m * half + p] = W.Gb[b];
         }
-        __syncthreads();
+        wave_lds_sync();
         wo1 = yl_bill_nem(t, S, 0.0, cfg.nm_yearend_sell_rate);
         wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
     } else {
@@ -1197,9 +1270,9 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     double w = wb * r_y;
     double wo = wo1 * r_y;
     double ev = (wo - w) + vor;                                    // ff:275
-    YFlow f = yl_cashflow(L, total, ev, y, lane, active);
+    YFlow f = yl_cashflow(L, total, ev, y, g, active);
     const int64_t row = i * (MAXY + 1);
-    if (lane == 0) {
+    if (g.sl == 0) {
         O.cfev_batt[row] = 0.0;
         O.bill_w_batt[row] = 0.0;
         O.bill_wo_batt[row] = 0.0;
@@ -1543,7 +1616,10 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->pending++;
     c->nch[slot] = nch;
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK;
-    const size_t ylds = ylds_bytes(lds_half(T->max_periods));
+    // two agents per wave when every analysis period fits 32 lanes
+    const int lpa = (A->max_years >= 1 && A->max_years <= 32) ? 32 : WAVE;
+    const size_t ylds = ylds_bytes(lds_half(T->max_periods), lpa);
+    const int apb = WAVE / lpa;   // agents per year-lane block
     hipStream_t s2 = c->s2;
     HIP_TRY(hipEventRecord(c->fork, s));
     HIP_TRY(hipStreamWaitEvent(s2, c->fork, 0));
@@ -1551,7 +1627,11 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         const int64_t i0 = (int64_t)j * csz, i1 = (i0 + csz < n) ? i0 + csz : n, m = i1 - i0;
         hipEvent_t* e = c->ev[slot][j];
         HIP_TRY(hipEventRecord(e[0], s));
-        hipLaunchKernelGGL(k_size_w, dim3((unsigned)m), dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0);
+        const dim3 ygrid((unsigned)((m + apb - 1) / apb));
+        if (lpa == 32)
+            hipLaunchKernelGGL(k_size_w<32>, ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+        else
+            hipLaunchKernelGGL(k_size_w<WAVE>, ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
         HIP_TRY(hipEventRecord(e[2], s2));
@@ -1563,8 +1643,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             hipLaunchKernelGGL(k_hourly_batt<false>, grid, block, lds, s2, *T, *A, *O, c->cfg, n, ws,
                                n_scratch, i0, i1);
         HIP_TRY(hipEventRecord(e[3], s2));
-        hipLaunchKernelGGL(k_batt_finance_w, dim3((unsigned)m), dim3(WAVE), ylds, s2, *T, *A, *O,
-                           c->cfg, n, ws, n_scratch, i0);
+        if (lpa == 32)
+            hipLaunchKernelGGL(k_batt_finance_w<32>, ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg, n,
+                               ws, n_scratch, i0, i1);
+        else
+            hipLaunchKernelGGL(k_batt_finance_w<WAVE>, ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
+                               n, ws, n_scratch, i0, i1);
         HIP_TRY(hipEventRecord(e[4], s2));
     }
     HIP_TRY(hipEventRecord(c->join, s2));

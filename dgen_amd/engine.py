@@ -182,6 +182,7 @@ class Engine:
         wsb = int(self.lib.dgen_workspace_bytes(n, n_scratch))
         ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
         ca = _lib.Agents(**{name: _ptr(dev[name]) for name, _ in _lib.AGENT_COLUMNS})
+        ca.max_years = int(dev["econ_life"].max().item()) if n else 0
         return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order)
 
     def validate_agents(self, dev, n):

@@ -151,6 +151,10 @@ typedef struct {
     const double* batt_capex_kwh;  /* batt_capex_per_kwh_combined                     */
     const double* ccm;             /* cap_cost_multiplier                             */
     const double* vor;             /* value_of_resiliency_usd                         */
+    int32_t max_years;             /* max econ_life over the batch: <= 32 runs two    */
+                                   /* agents per wave in the year-lane kernels; 0 or  */
+                                   /* > 32 runs one (agents above 32 lanes then fail  */
+                                   /* with DGEN_ST_YEARS instead of being truncated)  */
 } dgen_agents;
 
 /* Outputs (device pointers).  Hourly planes may be NULL (on-device reduction

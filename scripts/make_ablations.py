@@ -15,10 +15,12 @@ sys.path.insert(0, REPO)
 from dgen_amd.build import FLAGS, hipcc  # noqa: E402
 
 HB = "__global__ void __launch_bounds__(BLOCK, 2)\nk_hourly_batt("
-KS = "__global__ void __launch_bounds__(WAVE)\nk_size_w("
+KS = "__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3)))\nk_size_w("
+KF = "__global__ void __launch_bounds__(WAVE)\nk_batt_finance_w("
 
 
 def occ(decl, w):
+    decl = decl.replace(" __attribute__((amdgpu_waves_per_eu(3)))", "")
     head = decl.split("\n")[0].split("__launch_bounds__")[0]
     lb = "__launch_bounds__(BLOCK)" if "BLOCK" in decl else "__launch_bounds__(WAVE)"
     return head + lb + f" __attribute__((amdgpu_waves_per_eu({w}, {w})))\n" + decl.split("\n")[1]
@@ -28,8 +30,9 @@ VARIANTS = {
     "base": [],
     "hb_w3": [(HB, occ(HB, 3))],
     "hb_w4": [(HB, occ(HB, 4))],
+    "ks_w3": [(KS, occ(KS, 3))],
     "ks_w4": [(KS, occ(KS, 4))],
-    "ks_w5": [(KS, occ(KS, 5))],
+    "kf_w6": [(KF, occ(KF, 6))],
     "no_target": [("target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0, dmin_pos);",
                    "target = 0.0; asm volatile(\"\" :: \"v\"(need0), \"v\"(dmax), \"v\"(a0), \"v\"(b0), \"v\"(avail), \"v\"(dmin_pos));")],
     "no_hourly_stores": [("st_f32(ob + ho4, off4, (float)ld);", "asm volatile(\"\" :: \"v\"(ld));"),

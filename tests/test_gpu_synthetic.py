@@ -24,9 +24,16 @@ def _small_pop(cfg, n):
                            n_tariffs=48)
 
 
-@pytest.mark.parametrize("cfg,n", CASES)
-def test_synthetic_population_matches_oracle(engine, cfg, n):
+@pytest.mark.parametrize("cfg,n,long_life", [c + (False,) for c in CASES] + [("national_mixed", 300, True)])
+def test_synthetic_population_matches_oracle(engine, cfg, n, long_life):
+    """long_life: a third of the agents get 33..50-year analysis periods, so the
+    batch runs the one-agent-per-wave year-lane kernels (otherwise two agents
+    share a wave, 32 lanes each)."""
     pop = _small_pop(cfg, n)
+    if long_life:
+        life = pop.cols["econ_life"].copy()
+        life[::3] = 33 + (np.arange(life[::3].size) % 18)
+        pop.cols["econ_life"] = life
     engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     engine.set_tariffs(pop.tariffs)
     engine.set_switches(pop.switches)
@@ -50,7 +57,7 @@ def test_synthetic_population_matches_oracle(engine, cfg, n):
                   "npv_pv_batt"):
             assert np.isclose(o[k][i], r[k], rtol=1e-6, atol=1e-6), (i, k, o[k][i], r[k])
         assert o["payback_period"][i] == r["payback_period"], (i, o["payback_raw"][i], r["payback_raw"])
-        N1 = 26
+        N1 = int(pop.cols["econ_life"][i]) + 1
         for k_o, k_r in (("cash_flow", "cash_flow"), ("cfev_pv", "cf_energy_value_pv_only"),
                          ("bill_w_pv", "bill_w_pv_only"), ("cfev_batt", "cf_energy_value_pv_batt"),
                          ("bill_w_batt", "bill_w_pv_batt")):
