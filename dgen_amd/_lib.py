@@ -104,7 +104,7 @@ EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
     "dgen_kernel_times", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
-    "dgen_set_pipeline",
+    "dgen_set_pipeline", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
 ]
 
 

@@ -1413,6 +1413,206 @@ __global__ void k_diffusion(dgen_diffusion_in in, dgen_diffusion_out out, int64_
     out.market_value[i] = in.market_value_last_year[i] + nmv;
     out.system_kw_cum[i] = in.system_kw_cum_last_year[i] + nskw;
 }
+
+// ---------------------------------------------------------------------------
+// Battery attachment: attachment_rate_functions.py:58-138
+// largest-remainder integer battery adopters per (state, sector) group, and
+// the per-state hourly export weights / sums (:141-206).
+// ---------------------------------------------------------------------------
+constexpr int ATT_BLOCK = 256;
+
+struct NewVal {
+    const double* p;
+    __device__ double operator()(int i) const { return p[i]; }
+};
+
+// Block-wide int64 sum (every thread gets the total).
+__device__ __forceinline__ int64_t block_sum_i64(int64_t v, int64_t* red) {
+    const int t = threadIdx.x;
+    red[t] = v;
+    __syncthreads();
+    for (int w = ATT_BLOCK / 2; w > 0; w >>= 1) {
+        if (t < w) red[t] += red[t + w];
+        __syncthreads();
+    }
+    const int64_t r = red[0];
+    __syncthreads();
+    return r;
+}
+
+// One radix-select pass: histogram of digit (key >> shift) & 0xff over the
+// group's candidates (key & mask) == prefix, then the digit holding the k-th
+// key in the requested direction.  Updates prefix / mask / k (k-th among the
+// candidates left with that digit).  Keys come from key_of(i).
+template <class K>
+__device__ void radix_pass(const K& key_of, int64_t lo, int64_t hi, int shift, bool descending,
+                           uint64_t& prefix, uint64_t& mask, int64_t& k, uint32_t* hist,
+                           int64_t* sel) {
+    const int t = threadIdx.x;
+    hist[t] = 0;
+    __syncthreads();
+    for (int64_t i = lo + t; i < hi; i += ATT_BLOCK) {
+        const uint64_t key = key_of(i);
+        if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 0xffu], 1u);
+    }
+    __syncthreads();
+    if (t == 0) {
+        int64_t cum = 0;
+        int d = descending ? 255 : 0;
+        for (int s = 0; s < 256; s++, d += descending ? -1 : 1) {
+            const int64_t c = hist[d];
+            if (cum + c >= k) break;
+            cum += c;
+        }
+        sel[0] = d;
+        sel[1] = cum;
+    }
+    __syncthreads();
+    const uint64_t d = (uint64_t)sel[0];
+    k -= sel[1];
+    prefix |= d << shift;
+    mask |= (uint64_t)0xff << shift;
+    __syncthreads();
+}
+
+// One block per group (agents [seg_off[g], seg_off[g+1]) in the reference's
+// row order).  rate: per group.  aid_rank: rank of str(agent_id) (the
+// reference's tie-break sorts agent ids as strings, :125-128).
+__global__ void __launch_bounds__(ATT_BLOCK)
+k_batt_attach(dgen_attach_in in, dgen_attach_out out, const int64_t* __restrict__ seg_off,
+              const double* __restrict__ rate, int64_t n_seg) {
+    __shared__ uint32_t hist[256];
+    __shared__ int64_t red[ATT_BLOCK];
+    __shared__ int64_t sel[2];
+    __shared__ double tot;
+    const int64_t g = blockIdx.x;
+    if (g >= n_seg) return;
+    const int64_t lo = seg_off[g], hi = seg_off[g + 1];
+    const int t = threadIdx.x;
+    double r = rate[g];
+    r = fmax(0.0, fmin(1.0, r));                                   // :109
+    if (t == 0) tot = np_sum(NewVal{in.new_adopters + lo}, (int)(hi - lo));   // n.sum()
+    __syncthreads();
+    const double S = tot;
+    const bool active = (hi > lo) && !(S <= 0.0 || r <= 0.0);      // :112
+    int64_t rem = 0;
+    if (active) {
+        const int64_t target = (int64_t)rint(r * S);               // :116 round half even
+        int64_t bsum = 0;
+        for (int64_t i = lo + t; i < hi; i += ATT_BLOCK) bsum += (int64_t)floor(r * in.new_adopters[i]);
+        rem = target - block_sum_i64(bsum, red);                   // :121
+    }
+    // winners: frac desc, agent id (string) asc; threshold (T1, T2) by radix select
+    uint64_t p1 = 0, m1 = 0, p2 = 0, m2 = 0;
+    int64_t k1 = 0;
+    const bool pick = active && rem > 0;
+    const bool all = pick && rem >= hi - lo;
+    if (pick && !all) {
+        auto fkey = [&](int64_t i) -> uint64_t {
+            const double f = r * in.new_adopters[i];
+            const double fr = f - (double)(int64_t)floor(f);
+            return (uint64_t)__double_as_longlong(fr);             // fr >= 0: bits are monotone
+        };
+        k1 = rem;
+        for (int sh = 56; sh >= 0; sh -= 8) radix_pass(fkey, lo, hi, sh, true, p1, m1, k1, hist, sel);
+        // k1 = winners still needed among frac == T1: smallest string ranks
+        auto rkey = [&](int64_t i) -> uint64_t {
+            return fkey(i) == p1 ? (uint64_t)in.aid_rank[i] : ~(uint64_t)0;
+        };
+        int64_t k2 = k1;
+        for (int sh = 56; sh >= 0; sh -= 8) radix_pass(rkey, lo, hi, sh, false, p2, m2, k2, hist, sel);
+    }
+    for (int64_t i = lo + t; i < hi; i += ATT_BLOCK) {
+        int64_t a = 0;
+        if (active) {
+            const double f = r * in.new_adopters[i];
+            a = (int64_t)floor(f);
+            if (all) {
+                a += 1;
+            } else if (pick) {
+                const uint64_t key = (uint64_t)__double_as_longlong(f - (double)a);
+                if (key > p1 || (key == p1 && (uint64_t)in.aid_rank[i] <= p2)) a += 1;
+            }
+        }
+        const double nkw = (double)a * in.batt_kw[i];               // :133-136
+        const double nkwh = (double)a * in.batt_kwh[i];
+        out.added[i] = a;
+        out.new_batt_kw[i] = nkw;
+        out.new_batt_kwh[i] = nkwh;
+        out.batt_kw_cum[i] = in.batt_kw_cum_last_year[i] + nkw;
+        out.batt_kwh_cum[i] = in.batt_kwh_cum_last_year[i] + nkwh;
+    }
+}
+
+// Per-agent multipliers of the per-state export (:181-190):
+// w_pvo = pvo_cum, w_batt = batt_cum, w_non = max(n_cust - n_adopt, 0).
+__global__ void k_export_weights(const double* __restrict__ customers, const double* __restrict__ adopters,
+                                 const double* __restrict__ bkw_cum_ly, const double* __restrict__ bkw,
+                                 const int64_t* __restrict__ added, int64_t n, double* __restrict__ w_pvo,
+                                 double* __restrict__ w_batt, double* __restrict__ w_non) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double eps = 1e-9;
+    const double n_cust = customers[i], n_adopt = adopters[i];
+    const double b = bkw[i];
+    const double den = fmax(b != 0.0 ? b : eps, eps);              // max(float(x) or eps, eps)
+    const double prev = rint(fmax(bkw_cum_ly[i] / den, 0.0));      // int(round(max(., 0)))
+    double bc = prev + (double)added[i];
+    bc = bc > 0.0 ? bc : 0.0;
+    double pc = rint(n_adopt) - bc;
+    pc = pc > 0.0 ? pc : 0.0;
+    w_pvo[i] = pc;
+    w_batt[i] = bc;
+    const double nn = n_cust - n_adopt;
+    w_non[i] = 0.0 > nn ? 0.0 : nn;                                // Python max(nn, 0.0): NaN stays
+}
+
+// Per-state hourly net sums from the three f32 hourly planes ([h][n]):
+//   out[s * nh + h] = (sum_i pvo*w_pvo + wbt*w_batt + base*w_non) / 1000  (MW)
+// Members of state s are idx[seg_off[s] .. seg_off[s+1]) (idx null: the plane
+// columns themselves, states contiguous).  Block per (state, tile of SH_TILE
+// hours): the three weights of an agent are read once per tile instead of once
+// per hour, each plane row is a coalesced stream.  Fixed reduction order.
+constexpr int SH_TILE = 16;
+template <typename V>
+__global__ void __launch_bounds__(256)
+k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
+               const V* __restrict__ wbt, const double* __restrict__ w_pvo,
+               const double* __restrict__ w_batt, const double* __restrict__ w_non,
+               const int64_t* __restrict__ idx, int64_t n, int nh,
+               const int64_t* __restrict__ seg_off, int64_t n_seg, double* __restrict__ out) {
+    __shared__ double red[256];
+    const int64_t s = blockIdx.x;
+    const int h0 = blockIdx.y * SH_TILE;
+    if (s >= n_seg || h0 >= nh) return;
+    const int nt = nh - h0 < SH_TILE ? nh - h0 : SH_TILE;
+    const int64_t lo = seg_off[s], hi = seg_off[s + 1];
+    double acc[SH_TILE];
+#pragma unroll
+    for (int t = 0; t < SH_TILE; t++) acc[t] = 0.0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const int64_t c = idx ? idx[i] : i;
+        const double a = w_pvo[c], b = w_batt[c], d = w_non[c];
+        const int64_t o = (int64_t)h0 * n + c;
+#pragma unroll
+        for (int t = 0; t < SH_TILE; t++) {
+            if (t < nt) {
+                const int64_t r = o + (int64_t)t * n;
+                acc[t] += ((double)pvo[r] * a + (double)wbt[r] * b) + (double)base[r] * d;
+            }
+        }
+    }
+    for (int t = 0; t < nt; t++) {
+        red[threadIdx.x] = acc[t];
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) out[s * nh + h0 + t] = red[0] / 1000.0;
+        __syncthreads();
+    }
+}
 }  // namespace
 
 // ===========================================================================
@@ -1755,6 +1955,68 @@ int32_t dgen_brent_selftest(dgen_ctx* c, const double* lo, const double* hi, con
     HIP_TRY(hipSetDevice(c->device));
     hipLaunchKernelGGL(k_brent_selftest, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
                        (hipStream_t)stream, lo, hi, xatol, c2, x0, c1, n, xs, maxn, xopt, nfev);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_batt_attach(dgen_ctx* c, const dgen_attach_in* in, const dgen_attach_out* out,
+                         const int64_t* seg_off, const double* rate, int64_t n_seg, void* stream) {
+    if (!c || !in || !out || !seg_off || !rate || n_seg < 0) {
+        set_err("dgen_batt_attach: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n_seg == 0) return DGEN_OK;                                 // nothing to allocate
+    const void* req[] = {in->new_adopters, in->aid_rank, in->batt_kw, in->batt_kwh,
+                         in->batt_kw_cum_last_year, in->batt_kwh_cum_last_year, out->added,
+                         out->new_batt_kw, out->new_batt_kwh, out->batt_kw_cum, out->batt_kwh_cum};
+    for (const void* p : req)
+        if (!p) { set_err("dgen_batt_attach: missing column"); return DGEN_E_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_batt_attach, dim3((unsigned)n_seg), dim3(ATT_BLOCK), 0, (hipStream_t)stream,
+                       *in, *out, seg_off, rate, n_seg);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_export_weights(dgen_ctx* c, const double* customers_in_bin,
+                            const double* number_of_adopters, const double* batt_kw_cum_last_year,
+                            const double* batt_kw, const int64_t* added, int64_t n, double* w_pvo,
+                            double* w_batt, double* w_non, void* stream) {
+    if (!c || !customers_in_bin || !number_of_adopters || !batt_kw_cum_last_year || !batt_kw ||
+        !added || !w_pvo || !w_batt || !w_non || n < 0) {
+        set_err("dgen_export_weights: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n == 0) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_export_weights, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, customers_in_bin, number_of_adopters,
+                       batt_kw_cum_last_year, batt_kw, added, n, w_pvo, w_batt, w_non);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
+                          const void* with_batt, int32_t planes_f32, const double* w_pvo,
+                          const double* w_batt, const double* w_non, const int64_t* idx, int64_t n,
+                          int32_t n_hours, const int64_t* seg_off, int64_t n_seg, double* out,
+                          void* stream) {
+    if (!c || !baseline || !pvonly || !with_batt || !w_pvo || !w_batt || !w_non || !seg_off ||
+        !out || n < 0 || n_hours <= 0 || n_seg < 0 || n_seg > 0x7fffffff) {
+        set_err("dgen_state_hourly: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n_seg == 0) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const dim3 grid((unsigned)n_seg, (unsigned)((n_hours + SH_TILE - 1) / SH_TILE));
+    if (planes_f32)
+        hipLaunchKernelGGL(k_state_hourly<float>, grid, dim3(256), 0, (hipStream_t)stream,
+                           (const float*)baseline, (const float*)pvonly, (const float*)with_batt,
+                           w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);
+    else
+        hipLaunchKernelGGL(k_state_hourly<double>, grid, dim3(256), 0, (hipStream_t)stream,
+                           (const double*)baseline, (const double*)pvonly, (const double*)with_batt,
+                           w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
 }

@@ -290,6 +290,53 @@ typedef struct {
 int32_t dgen_diffusion(dgen_ctx* ctx, const dgen_diffusion_in* in, const dgen_diffusion_out* out,
                        int64_t n, int32_t is_first_year, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Battery attachment and the per-state hourly export:
+ *   attachment_rate_functions._allocate_battery_adopters_integer  :58-138
+ *   attachment_rate_functions.export_state_hourly_with_storage_mix :141-206
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    const double* new_adopters;           /* diffusion's new_adopters (float)     */
+    const int64_t* aid_rank;              /* rank of str(agent_id), unique        */
+    const double* batt_kw;
+    const double* batt_kwh;
+    const double* batt_kw_cum_last_year;
+    const double* batt_kwh_cum_last_year;
+} dgen_attach_in;
+
+typedef struct {
+    int64_t* added;                       /* batt_adopters_added_this_year        */
+    double *new_batt_kw, *new_batt_kwh, *batt_kw_cum, *batt_kwh_cum;
+} dgen_attach_out;
+
+/* Largest-remainder allocation per group: agents of group g are
+ * [seg_off[g], seg_off[g+1]) in the reference's row order (its n.sum() is
+ * numpy-pairwise in that order); rate[g] = the group's storage_attachment_rate.
+ * Tie-break among equal fractional parts: ascending str(agent_id) (aid_rank).
+ * Replaces the per-group pandas sort (:105-129).  Integer results bit-exact. */
+int32_t dgen_batt_attach(dgen_ctx* ctx, const dgen_attach_in* in, const dgen_attach_out* out,
+                         const int64_t* seg_off, const double* rate, int64_t n_seg, void* stream);
+
+/* Per-agent multipliers of the state export (:181-190): w_pvo = pvo_cum,
+ * w_batt = batt_cum (integers as doubles), w_non = max(n_cust - n_adopt, 0). */
+int32_t dgen_export_weights(dgen_ctx* ctx, const double* customers_in_bin,
+                            const double* number_of_adopters, const double* batt_kw_cum_last_year,
+                            const double* batt_kw, const int64_t* added, int64_t n, double* w_pvo,
+                            double* w_batt, double* w_non, void* stream);
+
+/* Per-state hourly net sums in MW (:179-198) from the three hourly planes
+ * ([n_hours][n]; float32 when planes_f32 != 0 -- dgen_size_agents' hourly
+ * outputs in place -- else float64) and the per-column weights:
+ * out[s * n_hours + h].  Members of state s are the plane columns
+ * idx[seg_off[s] .. seg_off[s+1]) (idx NULL: columns seg_off[s] ..
+ * seg_off[s+1]).  Fixed summation order (deterministic); the reference's
+ * sequential iterrows sum is matched to fp64 rounding, not bit for bit.    */
+int32_t dgen_state_hourly(dgen_ctx* ctx, const void* baseline, const void* pvonly,
+                          const void* with_batt, int32_t planes_f32, const double* w_pvo,
+                          const double* w_batt, const double* w_non, const int64_t* idx, int64_t n,
+                          int32_t n_hours, const int64_t* seg_off, int64_t n_seg, double* out,
+                          void* stream);
+
 /* Average per-call kernel time (ms) of the dgen_size_agents calls since the
  * previous query: k_size, k_hourly_batt, k_batt_finance, each summed over the
  * call's chunks (HIP events recorded on the stream each kernel runs on).

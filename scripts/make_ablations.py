@@ -38,6 +38,10 @@ VARIANTS = {
     "no_hourly_stores": [("st_f32(ob + ho4, off4, (float)ld);", "asm volatile(\"\" :: \"v\"(ld));"),
                          ("st_f32(op + ho4, off4, (float)fmax(dn, 0.0));", "asm volatile(\"\" :: \"v\"(dn));"),
                          ("st_f32(ow + ho4, off4, (float)st.g2l);", "asm volatile(\"\" :: \"v\"(st.g2l));")],
+    "no_batt_day": [("            if (has_batt) {\n                // day statistics",
+                     "            if (false) {\n                // day statistics")],
+    "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
+                 "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
 }
 
 

@@ -135,3 +135,17 @@ def golden_rows():
         store.add_solar((s["solar_re_9809_gid"], s["tilt"], s["azimuth"]), arr["cfs"][cr])
         rows.append(pd.Series(s, name=i))
     return rows, store, pd.DataFrame(meta["switch_table"])
+
+
+@lru_cache(maxsize=None)
+def golden_attach():
+    """(meta, hourly): attach.json cases + the f32 planes from attach.npz,
+    hourly[name] = (baseline, pvonly, with_batt) as float64 [n, n_hours]."""
+    with open(os.path.join(GOLDEN, "attach.json")) as f:
+        meta = json.load(f)
+    z = np.load(os.path.join(GOLDEN, "attach.npz"), allow_pickle=False)
+    hourly = {}
+    for c in meta["cases"]:
+        k = c["name"]
+        hourly[k] = tuple(z[f"{k}__{p}"].astype(np.float64) for p in ("baseline", "pvonly", "with_batt"))
+    return meta, hourly

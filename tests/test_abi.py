@@ -55,6 +55,7 @@ PROBE = r"""
 #define O(t, f) printf(#t "." #f " %zu\n", offsetof(t, f));
 int main(void) {
   S(dgen_cfg) S(dgen_tariff) S(dgen_switch) S(dgen_tables) S(dgen_agents) S(dgen_outputs)
+  S(dgen_attach_in) S(dgen_attach_out) S(dgen_diffusion_in) S(dgen_diffusion_out)
   O(dgen_cfg, batt_v_nom) O(dgen_cfg, batt_eta_out) O(dgen_tariff, fixed) O(dgen_tariff, buy)
   O(dgen_tariff, sell) O(dgen_tariff, wkday) O(dgen_tariff, flags) O(dgen_tables, n_shapes)
   O(dgen_tables, n_tariffs) O(dgen_agents, vor) O(dgen_outputs, baseline) O(dgen_outputs, net_with_batt)
@@ -81,6 +82,11 @@ def test_struct_sizes(layout):
     assert layout["dgen_tables"] == ctypes.sizeof(_lib.Tables)
     assert layout["dgen_agents"] == ctypes.sizeof(_lib.Agents)
     assert layout["dgen_outputs"] == ctypes.sizeof(_lib.Outputs)
+    from dgen_amd import attachment, diffusion
+    assert layout["dgen_attach_in"] == ctypes.sizeof(attachment.AttachIn)
+    assert layout["dgen_attach_out"] == ctypes.sizeof(attachment.AttachOut)
+    assert layout["dgen_diffusion_in"] == ctypes.sizeof(diffusion.DiffIn)
+    assert layout["dgen_diffusion_out"] == ctypes.sizeof(diffusion.DiffOut)
 
 
 def test_struct_offsets(layout):
