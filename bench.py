@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--chunks", type=int, default=None,
                     help="size() pipeline depth (default: the library's DGEN_DEFAULT_CHUNKS)")
+    ap.add_argument("--hb-months", type=int, default=None,
+                    help="months per k_hourly_batt launch (default: the library's)")
+    ap.add_argument("--order-major", default="load", choices=["cf", "load"],
+                    help="profile_order grouping: by (cf_row, load_row) or (load_row, cf_row)")
     ap.add_argument("--caller-order", action="store_true",
                     help="keep the generator's agent order on device (no profile_order grouping)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_bytes_per_agent.json"))
@@ -111,10 +115,12 @@ def main():
     eng = Engine(local if ws > 1 else 0)
     if args.chunks is not None:
         eng.set_pipeline(args.chunks)
+    if args.hb_months is not None:
+        eng.set_hourly_segment(args.hb_months)
     eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     eng.set_tariffs(pop.tariffs)
     eng.set_switches(pop.switches)
-    order = None if args.caller_order else profile_order(pop.cols)
+    order = None if args.caller_order else profile_order(pop.cols, args.order_major)
     batch = eng.upload_agents(pop.cols, pop.n_scratch, order=order)
     out = eng.alloc_outputs(batch.n, hourly=not args.no_hourly)
     c_out = eng.c_outputs(out)
@@ -164,7 +170,10 @@ def main():
             "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch,
             "kernel_ms": {"k_size": ms_size, "k_hourly_batt": ms_hourly, "k_batt_finance": ms_fin},
-            "dominant_kernel": dom, "event_samples": cnt}
+            "dominant_kernel": dom, "event_samples": cnt,
+            # k_hourly_batt sweeps the year in month segments: kernel_ms is the
+            # per-step sum over these launches (rocprof reports per launch)
+            "hourly_launches_per_step": -(-12 // eng.hb_months) * eng.chunks}
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
@@ -183,8 +192,9 @@ def main():
             "config": {"workload": args.config, "agents_per_gpu": args.agents,
                        "global_agents": args.agents * ws,
                        "hourly_outputs": not args.no_hourly,
-                       "pipeline_chunks": eng.chunks,
-                       "device_order": "caller" if args.caller_order else "profile (cf_row, load_row)",
+                       "pipeline_chunks": eng.chunks, "hourly_months_per_launch": eng.hb_months,
+                       "device_order": "caller" if args.caller_order else
+                       ("profile (cf_row, load_row)" if args.order_major == "cf" else "profile (load_row, cf_row)"),
                        "parallelism": f"dp{ws} (agent shards, no collective in the step)",
                        "agents_with_status_errors": n_bad},
             "roofline": roof, "cpu_baseline": cpu,

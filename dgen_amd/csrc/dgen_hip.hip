@@ -42,6 +42,7 @@ constexpr int MAXT = DGEN_MAXT;
 constexpr int MAXY = DGEN_MAXY;
 constexpr int NBIN = 12 * MAXP;
 constexpr int BLOCK = 128;   // threads per block for the per-agent kernels
+constexpr int HB_DAY_BYTES = 12 * 1024;   // k_hourly_batt day buffer per wave (LDS)
 
 __constant__ int c_month_start_day[13] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334, 365};
 __constant__ int c_days_in_month[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
@@ -319,8 +320,8 @@ __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, d
 
 struct WsLayout {
     // doubles, plane-major [k][n]
-    double* L;        // NBIN planes
-    double* G;        // NBIN planes
+    double* carry;    // NBIN planes: [0] SOC, [1] annual PV kWh between month-segment launches
+    double* G;        // NBIN planes (unused)
     double* Lb;       // NBIN planes (battery case, final tariff)
     double* Gb;       // NBIN planes
     double* otc_b;    // 1 plane: storage one-time charge
@@ -330,7 +331,7 @@ struct WsLayout {
 __host__ __device__ inline WsLayout ws_layout(void* base, int64_t n) {
     WsLayout w;
     double* p = (double*)base;
-    w.L = p; p += (int64_t)NBIN * n;
+    w.carry = p; p += (int64_t)NBIN * n;
     w.G = p; p += (int64_t)NBIN * n;
     w.Lb = p; p += (int64_t)NBIN * n;
     w.Gb = p; p += (int64_t)NBIN * n;
@@ -480,11 +481,58 @@ __device__ __forceinline__ HourStep batt_hour(double nn, double pv, double targe
     return r;
 }
 
+typedef __attribute__((address_space(3))) char* lds_ptr_t;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// 16 B per lane global -> LDS at lds + lane * 16 (m0 = wave-uniform base)
+__device__ __forceinline__ void lds_dma16(const void* g, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(g), "s"(lds) : "memory", "m0");
+}
+
+// Read back a day buffer (lane's 12 chunks) after vmcnt(VM): chunk q of the
+// shape row at +q KB, of the cf row at +(6 + q) KB.
+template <int VM>
+__device__ __forceinline__ void day_read(uint32_t a, DayRaw& r) {
+    f32x4 s0, s1, s2, s3, s4, s5;
+    i32x4 c0, c1, c2, c3, c4, c5;
+    asm volatile("s_waitcnt vmcnt(%12)\n\t"
+                 "ds_read_b128 %0, %13\n\t"
+                 "ds_read_b128 %1, %13 offset:1024\n\t"
+                 "ds_read_b128 %2, %13 offset:2048\n\t"
+                 "ds_read_b128 %3, %13 offset:3072\n\t"
+                 "ds_read_b128 %4, %13 offset:4096\n\t"
+                 "ds_read_b128 %5, %13 offset:5120\n\t"
+                 "ds_read_b128 %6, %13 offset:6144\n\t"
+                 "ds_read_b128 %7, %13 offset:7168\n\t"
+                 "ds_read_b128 %8, %13 offset:8192\n\t"
+                 "ds_read_b128 %9, %13 offset:9216\n\t"
+                 "ds_read_b128 %10, %13 offset:10240\n\t"
+                 "ds_read_b128 %11, %13 offset:11264\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(s5),
+                   "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3), "=&v"(c4), "=&v"(c5)
+                 : "n"(VM), "v"(a)
+                 : "memory");
+    const f32x4 sv[6] = {s0, s1, s2, s3, s4, s5};
+    const i32x4 cv[6] = {c0, c1, c2, c3, c4, c5};
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        r.s[4 * q + 0] = sv[q].x; r.s[4 * q + 1] = sv[q].y; r.s[4 * q + 2] = sv[q].z; r.s[4 * q + 3] = sv[q].w;
+        r.c[4 * q + 0] = cv[q].x; r.c[4 * q + 1] = cv[q].y; r.c[4 * q + 2] = cv[q].z; r.c[4 * q + 3] = cv[q].w;
+    }
+}
+
 template <bool HOURLY>
 __global__ void __launch_bounds__(BLOCK, 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-              int64_t n_scratch, int64_t i0, int64_t i1) {
-    // agents [i0, i1) of a batch of n (row stride of every plane stays n)
+              int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi) {
+    // agents [i0, i1) of a batch of n (row stride of every plane stays n),
+    // months [m_lo, m_hi) of the year: the year is swept in month segments,
+    // one launch each, so that every resident wave works on the same weeks
+    // and the profile-row slices they read stay in L2 / MALL (SOC and the
+    // running annual PV sum carry between launches in W.carry)
     int64_t i = i0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= i1) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
@@ -530,8 +578,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const double out_per_bank = bank > 0.0 ? 1.0 / (cfg.batt_eta_out * bank) : 0.0;
     const bool has_batt = bank > 0.0;
     if (!has_batt) power = 0.0;
-    double soc = cfg.batt_init_soc;
-    double annual = 0.0;
+    double soc = m_lo == 0 ? cfg.batt_init_soc : W.carry[i];
+    double annual = m_lo == 0 ? 0.0 : W.carry[n + i];
+    const int d_lo = c_month_start_day[m_lo];
     // hour rows: wave-uniform bases advanced by one row per hour; per-lane
     // 32-bit byte offsets (host guarantees n < 2^29, n_scratch < 2^28)
     const uint32_t off4 = (uint32_t)i * 4u;
@@ -541,27 +590,56 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     char* const op = reinterpret_cast<char*>(O.net_pvonly);
     char* const ow = reinterpret_cast<char*>(O.net_with_batt);
     char* const osc = reinterpret_cast<char*>(W.scratch);
-    size_t ho4 = 0, ho8 = 0;
+    size_t ho4 = (size_t)d_lo * 24 * row4, ho8 = (size_t)d_lo * 24 * row8;
 
-    for (int m = 0; m < 12; m++) {
+    // Software pipeline over days through LDS: the next day's raw profile
+    // values (96 B of the shape row + 96 B of the cf row per lane) are DMA'd
+    // global -> LDS (global_load_lds_dwordx4: no VGPRs held in flight) at the
+    // start of the current day, BEFORE the day's 72 hourly stores.  vmcnt is
+    // shared by loads and stores and retires in issue order, so at the next
+    // day start vmcnt(48) already implies the DMA landed while the last 48
+    // stores may still be in flight (a wait on a load issued after the stores
+    // would drain them all).  DMA and read-back are inline asm: the compiler
+    // would otherwise order every LDS access of the kernel (the bins) behind
+    // a vmcnt(0).  Per wave: 12 chunks x 64 lanes x 16 B = HB_DAY_BYTES.
+    const uint32_t dbase = (uint32_t)(size_t)(lds_ptr_t)(reinterpret_cast<char*>(dyn_lds) +
+                           (size_t)16 * lds_half(T.max_periods) * BLOCK +
+                           (size_t)(threadIdx.x / 64) * HB_DAY_BYTES);
+    const uint32_t dbase_s = __builtin_amdgcn_readfirstlane(dbase);
+    const uint32_t dlane = dbase_s + (threadIdx.x & 63u) * 16u;
+    auto day_dma = [&](int dd) {
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            lds_dma16(shp + dd * 24 + 4 * q, dbase_s + q * 1024u);
+            lds_dma16(cfp + dd * 24 + 4 * q, dbase_s + (6 + q) * 1024u);
+        }
+    };
+    // the day's period schedule (24 bytes, 8-aligned rows) in 3 registers,
+    // loaded one day ahead as well (issued before the day's stores)
+    uint64_t sched[3];
+    {
+        const uint64_t* sr = reinterpret_cast<const uint64_t*>(((d_lo % 7) >= 5) ? t.wkend[m_lo]
+                                                                             : t.wkday[m_lo]);
+        sched[0] = sr[0]; sched[1] = sr[1]; sched[2] = sr[2];
+    }
+    // settle every load before the day loop: the waitcnt pass merges the
+    // loop entry with the back edge, and a pending entry load would put a
+    // vmcnt wait (which also drains the in-flight day DMA) into hour 0
+    __builtin_amdgcn_s_waitcnt(0x0f70);                  // vmcnt(0)
+    day_dma(d_lo);
+    const int d_last = c_month_start_day[m_hi] - 1;
+    DayRaw r;
+    for (int m = m_lo; m < m_hi; m++) {
         for (int p = 0; p < P; p++) bins[p * BLOCK] = make_double2(0.0, 0.0);
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
-            const int h0 = d * 24;
-            // the day's period schedule: 24 bytes (8-aligned rows) in 3 registers
-            const uint64_t* sr =
-                reinterpret_cast<const uint64_t*>(((d % 7) >= 5) ? t.wkend[m] : t.wkday[m]);
-            const uint64_t sched[3] = {sr[0], sr[1], sr[2]};
-            DayRaw r;
-            // 96 B of the shape row and 96 B of the cf row: 6 x 16 B loads each
-            const float4* s4 = reinterpret_cast<const float4*>(shp + h0);
-            const int4* c4 = reinterpret_cast<const int4*>(cfp + h0);
-#pragma unroll
-            for (int q = 0; q < 6; q++) {
-                float4 sv = s4[q];
-                int4 cv = c4[q];
-                r.s[4 * q + 0] = sv.x; r.s[4 * q + 1] = sv.y; r.s[4 * q + 2] = sv.z; r.s[4 * q + 3] = sv.w;
-                r.c[4 * q + 0] = cv.x; r.c[4 * q + 1] = cv.y; r.c[4 * q + 2] = cv.z; r.c[4 * q + 3] = cv.w;
-            }
+            if (HOURLY && d > d_lo) day_read<48>(dlane, r);
+            else day_read<0>(dlane, r);
+            const int dx = d < d_last ? d + 1 : d;
+            const int mx = dx < c_month_start_day[m + 1] ? m : (m < 11 ? m + 1 : 11);
+            const uint64_t* nsr =
+                reinterpret_cast<const uint64_t*>(((dx % 7) >= 5) ? t.wkend[mx] : t.wkday[mx]);
+            const uint64_t nsched[3] = {nsr[0], nsr[1], nsr[2]};
+            if (d < d_last) day_dma(d + 1);
             double target = 0.0;
             if (has_batt) {
                 // day statistics of d_h = max(load_h - pv_h, 0) for the target
@@ -609,6 +687,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 }
                 ho8 += row8;
             }
+            sched[0] = nsched[0]; sched[1] = nsched[1]; sched[2] = nsched[2];
         }
         if (!mo2) {
             for (int p = 0; p < P; p++) {
@@ -618,6 +697,11 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 W.Gb[k] = b.y;
             }
         }
+    }
+    if (m_hi < 12) {
+        W.carry[i] = soc;
+        W.carry[n + i] = annual;
+        return;
     }
     O.annual_kwh[i] = annual;
     double den = kw_star > 1e-9 ? kw_star : 1e-9;
@@ -1631,6 +1715,7 @@ struct dgen_ctx {
     hipEvent_t fork, join;
     hipStream_t s2;    // hourly + finance stream of the chunk pipeline
     int chunks;        // pipeline depth (dgen_set_pipeline)
+    int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
     int head;          // next ring slot to record
     int pending;       // recorded, not yet folded
     double sum_ms[3];
@@ -1683,6 +1768,7 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     c->cfg = *cfg;
     c->head = 0; c->pending = 0; c->count = 0;
     c->chunks = DGEN_DEFAULT_CHUNKS;
+    c->hb_months = DGEN_DEFAULT_HOURLY_MONTHS;
     c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
@@ -1815,7 +1901,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->head = (c->head + 1) % dgen_ctx::RING;
     c->pending++;
     c->nch[slot] = nch;
-    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK;
+    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK +
+                       (size_t)(BLOCK / 64) * HB_DAY_BYTES;
     // two agents per wave when every analysis period fits 32 lanes
     const int lpa = (A->max_years >= 1 && A->max_years <= 32) ? 32 : WAVE;
     const size_t ylds = ylds_bytes(lds_half(T->max_periods), lpa);
@@ -1836,12 +1923,15 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
         HIP_TRY(hipEventRecord(e[2], s2));
         dim3 grid((unsigned)((m + BLOCK - 1) / BLOCK)), block(BLOCK);
-        if (hourly)
-            hipLaunchKernelGGL(k_hourly_batt<true>, grid, block, lds, s2, *T, *A, *O, c->cfg, n, ws,
-                               n_scratch, i0, i1);
-        else
-            hipLaunchKernelGGL(k_hourly_batt<false>, grid, block, lds, s2, *T, *A, *O, c->cfg, n, ws,
-                               n_scratch, i0, i1);
+        for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
+            const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
+            if (hourly)
+                hipLaunchKernelGGL(k_hourly_batt<true>, grid, block, lds, s2, *T, *A, *O, c->cfg, n,
+                                   ws, n_scratch, i0, i1, m0, m1);
+            else
+                hipLaunchKernelGGL(k_hourly_batt<false>, grid, block, lds, s2, *T, *A, *O, c->cfg, n,
+                                   ws, n_scratch, i0, i1, m0, m1);
+        }
         HIP_TRY(hipEventRecord(e[3], s2));
         if (lpa == 32)
             hipLaunchKernelGGL(k_batt_finance_w<32>, ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg, n,
@@ -1854,6 +1944,15 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     HIP_TRY(hipEventRecord(c->join, s2));
     HIP_TRY(hipStreamWaitEvent(s, c->join, 0));
     HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_set_hourly_segment(dgen_ctx* c, int32_t months) {
+    if (!c || months < 1 || months > 12) {
+        set_err("dgen_set_hourly_segment: months must be in [1, 12]");
+        return DGEN_E_ARG;
+    }
+    c->hb_months = months;
     return DGEN_OK;
 }
 

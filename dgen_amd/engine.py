@@ -39,16 +39,22 @@ class AgentBatch:
     perm: Optional[np.ndarray] = None
 
 
-def profile_order(cols: Dict[str, np.ndarray]) -> np.ndarray:
-    """Device order for a batch: agents grouped by (cf_row, load_row).
+def profile_order(cols: Dict[str, np.ndarray], major: str = "load") -> np.ndarray:
+    """Device order for a batch: agents grouped by (load_row, cf_row)
+    (major="cf": by (cf_row, load_row)).
 
     k_hourly_batt runs one agent per lane and streams the agent's two profile
-    rows day by day; when the 64 lanes of a wave share a cf row its loads are
-    one broadcast line instead of 64, and the load-shape lines of a group stay
-    hot in L2.  The reference's agent order carries no
-    meaning (size_chunk returns rows keyed by agent_id, ff:1149-1218), so the
-    host columnarizer is free to choose it.  Stable, so ties keep caller order."""
-    return np.lexsort((np.asarray(cols["load_row"]), np.asarray(cols["cf_row"]))).astype(np.int64)
+    rows day by day; when the 64 lanes of a wave share a row, its loads are one
+    broadcast line instead of 64.  Load-major shares the larger table (the
+    load shapes) inside a wave and leaves the per-lane reads on the smaller cf
+    table, which stays cache-resident (measured at 1M agents: 35.2 ms vs
+    38.0 ms cf-major, 45.3 ms caller order).  The
+    reference's agent order carries no meaning (size_chunk returns rows keyed
+    by agent_id, ff:1149-1218), so the host columnarizer is free to choose it.
+    Stable, so ties keep caller order."""
+    lr, cr = np.asarray(cols["load_row"]), np.asarray(cols["cf_row"])
+    keys = (lr, cr) if major == "cf" else (cr, lr)
+    return np.lexsort(keys).astype(np.int64)
 
 
 class Engine:
@@ -67,6 +73,7 @@ class Engine:
         self.ctx = h
         self.tables = _lib.Tables()
         self.chunks = _lib.DEFAULT_CHUNKS
+        self.hb_months = _lib.DEFAULT_HOURLY_MONTHS
         self._keep: Dict[str, object] = {}
 
     # ------------------------------------------------------------------ utils
@@ -238,6 +245,11 @@ class Engine:
         """Chunk-pipeline depth of size() (dgen_set_pipeline; 1 = no overlap)."""
         _lib.check(self.lib.dgen_set_pipeline(self.ctx, int(chunks)), "dgen_set_pipeline")
         self.chunks = int(chunks)
+
+    def set_hourly_segment(self, months: int):
+        """Months per k_hourly_batt launch (dgen_set_hourly_segment)."""
+        _lib.check(self.lib.dgen_set_hourly_segment(self.ctx, int(months)), "dgen_set_hourly_segment")
+        self.hb_months = int(months)
 
     def kernel_times(self):
         """Average per-launch device time (ms) of the three sizing kernels over

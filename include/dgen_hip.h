@@ -39,6 +39,7 @@ extern "C" {
 
 #define DGEN_ABI_VERSION 2
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
+#define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_NH    8760   /* hours per year                                    */
 #define DGEN_NSLOT 576    /* 12 months x {weekday, weekend} x 24 hours         */
 #define DGEN_MAXP  12     /* TOU periods                                        */
@@ -350,6 +351,14 @@ int32_t dgen_kernel_times(dgen_ctx* ctx, double* ms_size, double* ms_hourly, dou
  * the caller).  1 = no overlap.  Range [1, 16]; default DGEN_DEFAULT_CHUNKS.
  * Replaces nothing in the reference (its per-agent loop is serial, ff:1149). */
 int32_t dgen_set_pipeline(dgen_ctx* ctx, int32_t chunks);
+
+/* Months of the year per k_hourly_batt launch (the sequential 8760-h scan of
+ * dgen_size_agents): the year is swept in ceil(12 / months) launches, SOC and
+ * the annual PV sum carried between them in the workspace, so that all
+ * resident waves read the same weeks of the shared profile rows and those
+ * slices stay cache-resident.  Results do not depend on it.  Range [1, 12];
+ * default DGEN_DEFAULT_HOURLY_MONTHS.  Replaces nothing in the reference.   */
+int32_t dgen_set_hourly_segment(dgen_ctx* ctx, int32_t months);
 
 #ifdef __cplusplus
 }

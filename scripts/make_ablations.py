@@ -40,6 +40,10 @@ VARIANTS = {
                          ("st_f32(ow + ho4, off4, (float)st.g2l);", "asm volatile(\"\" :: \"v\"(st.g2l));")],
     "no_batt_day": [("            if (has_batt) {\n                // day statistics",
                      "            if (false) {\n                // day statistics")],
+    # profile loads always from the agent's first two days (L1/L2-resident):
+    # measures how much of the scan waits on the day loads
+    "hot_loads": [("const float4* s4 = reinterpret_cast<const float4*>(shp + h0);\n            const int4* c4 = reinterpret_cast<const int4*>(cfp + h0);",
+                   "const float4* s4 = reinterpret_cast<const float4*>(shp + (d & 1) * 24);\n            const int4* c4 = reinterpret_cast<const int4*>(cfp + (d & 1) * 24);")],
     "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
                  "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
 }

@@ -14,9 +14,13 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 tag, agents = sys.argv[1], int(sys.argv[2])
+# k_hourly_batt runs as HB_LAUNCHES month-segment launches per sizing call
+# (dgen_set_hourly_segment): its per-agent bytes sum the per-launch means
+HB_LAUNCHES = int(os.environ.get("HB_LAUNCHES", "12"))
 out_json = sys.argv[3] if len(sys.argv) > 3 else f"gpurun_out/prof_{tag}_pmc_bytes.json"
 agg = collections.defaultdict(list)
 for f in glob.glob(f"gpurun_out/prof_{tag}_pmc_*/run_counter_collection.csv"):
@@ -35,10 +39,13 @@ for kn in kernels:
             means[c] = sum(v) / len(v)
             print(f"   {c:24s} n={len(v):2d} mean={means[c]:.4g}")
     if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
-        rd, wr = 2.0 * means["FETCH_SIZE"] * 1024.0, means["WRITE_SIZE"] * 1024.0
+        per_call = HB_LAUNCHES if kn == "k_hourly_batt" else 1
+        rd = 2.0 * means["FETCH_SIZE"] * 1024.0 * per_call
+        wr = means["WRITE_SIZE"] * 1024.0 * per_call
         res[kn] = {"fetch_size_kib": means["FETCH_SIZE"], "write_size_kib": means["WRITE_SIZE"],
                    "hbm_read_bytes": rd, "hbm_write_bytes": wr,
                    "hbm_bytes_per_agent": (rd + wr) / agents, "agents": agents,
+                   "launches_per_call": per_call,
                    "correction": "2 x FETCH_SIZE (gfx950 half-count) + WRITE_SIZE"}
         print(f"   -> HBM bytes/agent {(rd + wr) / agents:.1f} (read {rd / agents:.1f}, write {wr / agents:.1f})")
 json.dump(res, open(out_json, "w"), indent=1)

@@ -33,6 +33,8 @@ def test_library_exports_every_declared_symbol():
     assert L.dgen_abi_version() == _lib.ABI_VERSION == 2
     m = re.search(r"#define DGEN_DEFAULT_CHUNKS\s+(\d+)", open(HEADER).read())
     assert m and int(m.group(1)) == _lib.DEFAULT_CHUNKS
+    m = re.search(r"#define DGEN_DEFAULT_HOURLY_MONTHS\s+(\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == _lib.DEFAULT_HOURLY_MONTHS
 
 
 def test_workspace_bytes_formula():

@@ -83,7 +83,7 @@ def test_profile_order_is_invisible(engine, cfg, n):
     for order in (None, profile_order(pop.cols)):
         batch = engine.upload_agents(pop.cols, pop.n_scratch, order=order)
         if order is not None:
-            rows = pop.cols["cf_row"][batch.perm]
+            rows = pop.cols["load_row"][batch.perm]
             assert (np.diff(rows) >= 0).all()
         out = engine.alloc_outputs(batch.n, hourly=True)
         engine.size(batch, out)
@@ -119,6 +119,32 @@ def test_pipeline_depth_is_invisible(engine):
     finally:
         from dgen_amd import _lib
         engine.set_pipeline(_lib.DEFAULT_CHUNKS)
+    for r in res[1:]:
+        for k in r:
+            if r[k] is not None:
+                assert np.array_equal(res[0][k], r[k], equal_nan=True), k
+
+
+def test_hourly_segment_is_invisible(engine):
+    """Sweeping the year in month-segment launches of k_hourly_batt (SOC and
+    the annual PV sum carried in the workspace) changes no output bit; mixed
+    population with net-billing (mo 2) agents and storage switches."""
+    from dgen_amd import _lib
+    pop = _small_pop("national_mixed", 3001)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    res = []
+    try:
+        for months in (1, 12, 5):
+            engine.set_hourly_segment(months)
+            out = engine.alloc_outputs(batch.n, hourly=True)
+            engine.size(batch, out)
+            torch.cuda.synchronize()
+            res.append(outputs_to_host(out))
+    finally:
+        engine.set_hourly_segment(_lib.DEFAULT_HOURLY_MONTHS)
     for r in res[1:]:
         for k in r:
             if r[k] is not None:
