@@ -825,7 +825,19 @@ __device__ __forceinline__ const dgen_tariff* stage_tariff(const dgen_tariff* sr
         wave_lds_sync();
         const double* s = reinterpret_cast<const double*>(src);
         double* d = reinterpret_cast<double*>(S.trf);
-        for (int k = g.sl; k < TRF_QW; k += LPA) d[k] = s[k];
+        // every load of the lane issued before the first store (one latency)
+        constexpr int PER = (TRF_QW + LPA - 1) / LPA;
+        double v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int k = g.sl + j * LPA;
+            v[j] = k < TRF_QW ? s[k] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const int k = g.sl + j * LPA;
+            if (k < TRF_QW) d[k] = v[j];
+        }
         wave_lds_sync();
         return S.trf;
     }
@@ -1003,13 +1015,27 @@ __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double
     for (int cell = g.sl; cell < 12 * P; cell += LPA) {
         int m = cell / P, p = cell % P;
         double la = 0.0, ga = 0.0;
+        // the month's 48 slot sums of both rows in batches of BB (2 BB loads
+        // in flight, branch-free), then the period's slots added in slot order
+        // (the oracle's order; a skipped slot is a select, not a + 0.0)
+        constexpr int BB = 4;
+        const double* lm = lslots + m * 48;
+        const double* gm = gslots + m * 48;
         for (int dt = 0; dt < 2; dt++) {
             const uint8_t* sched = dt ? t.wkend[m] : t.wkday[m];
-            for (int hod = 0; hod < 24; hod++) {
-                if (sched[hod] == p) {
-                    int sl = m * 48 + dt * 24 + hod;
-                    la += lslots[sl];
-                    ga += gslots[sl];
+#pragma unroll 1
+            for (int h0 = 0; h0 < 24; h0 += BB) {
+                double lv[BB], gv[BB];
+#pragma unroll
+                for (int k = 0; k < BB; k++) {
+                    lv[k] = lm[dt * 24 + h0 + k];
+                    gv[k] = gm[dt * 24 + h0 + k];
+                }
+#pragma unroll
+                for (int k = 0; k < BB; k++) {
+                    const bool on = sched[h0 + k] == p;
+                    la = on ? la + lv[k] : la;
+                    ga = on ? ga + gv[k] : ga;
                 }
             }
         }
