@@ -44,6 +44,12 @@ VARIANTS = {
     # measures how much of the scan waits on the day loads
     "hot_loads": [("const float4* s4 = reinterpret_cast<const float4*>(shp + h0);\n            const int4* c4 = reinterpret_cast<const int4*>(cfp + h0);",
                    "const float4* s4 = reinterpret_cast<const float4*>(shp + (d & 1) * 24);\n            const int4* c4 = reinterpret_cast<const int4*>(cfp + (d & 1) * 24);")],
+    # k_size: slot-sum bins without their global loads (constant slot sums)
+    "ks_no_slot_loads": [("                    lv[k] = lm[dt * 24 + h0 + k];\n                    gv[k] = gm[dt * 24 + h0 + k];",
+                          "                    lv[k] = 1.0 + k; gv[k] = 0.5 + k;")],
+    # hourly planes written with plain (temporal) stores instead of nt
+    "plain_stores": [("    __builtin_nontemporal_store(v, reinterpret_cast<float*>(row + off));",
+                      "    *reinterpret_cast<float*>(row + off) = v;")],
     "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
                  "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
 }
