@@ -354,80 +354,76 @@ __device__ __forceinline__ void batt_size(double desired_kw, double desired_kwh,
 }
 
 // Daily peak-shaving target (same algorithm as the oracle's day_target):
-// smallest T >= 0 with f(T) = sum_h min(max(d_h - T, 0), P) <= E,
-// d_h = max(load_h - pv_h, 0).  No saturated hour: Newton from 0 on the convex
-// water-filling function.  Otherwise bisection until no breakpoint (d_h,
-// d_h - P) is inside the bracket, then the exact linear solve.  d_h is
-// recomputed from the raw day registers.
-// An opaque copy: stops the compiler from keeping 24 hoisted products live
-// across the three per-day loops (recomputing them is cheaper than spilling).
-__device__ __forceinline__ double opaque(double x) {
-    asm volatile("" : "+v"(x));
-    return x;
+// smallest T >= 0 with f(T) = sum_h min(max(d_h - T, 0), P) <= E on the day's
+// deficits d_h = max(load_h - pv_h, 0), sorted descending (s[0] = max).
+// No saturated hour (s[0] <= P): f(T) = max_k (S_k - k T) with S_k the sum of
+// the k largest, so T = (S_K - E) / K for the largest K with
+// f(s[K-1]) = S_K - K s[K-1] <= E -- exact, one pass over the sorted day
+// instead of the 4-5 Newton passes a wave ran before.  Otherwise bisection
+// until no breakpoint (s_k, s_k - P) is inside the bracket, then the exact
+// linear piece.  Every sum runs over the sorted order.
+__device__ __forceinline__ void cswap_desc(double& a, double& b) {
+    const double hi = fmax(a, b), lo = fmin(a, b);
+    a = hi;
+    b = lo;
 }
 
-struct DayRaw {
-    float s[24];
-    int32_t c[24];
-};
-
-__device__ __forceinline__ float opaque_f(float x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-__device__ __forceinline__ int32_t opaque_i(int32_t x) {
-    asm volatile("" : "+v"(x));
-    return x;
-}
-
-// load_h - pv_h clamped at 0, re-derived from the raw registers (the opaque
-// copies keep the compiler from caching 48 converted doubles across passes).
-__device__ __forceinline__ double day_d(const DayRaw& r, int h, double ls, double cs6) {
-    return fmax((double)r.s[h] * ls - (double)r.c[h] * cs6, 0.0);
-}
-
-__device__ __forceinline__ double day_target(const DayRaw& r, double ls, double cs6, double power, double avail,
-                             double dmax, double need0, int a_lo, int b_lo, double dmin_pos) {
-    if (need0 <= avail) return 0.0;
-    if (dmax <= power) {
-        // no hour saturates: convex water-filling, Newton from T = 0, exact once
-        // the active count stops changing.  `mact` = min{d_h : d_h > t}: the
-        // count at tn equals the count at t iff mact > tn, so the confirming
-        // pass of the plain iteration is skipped (same iterates, same result).
-        double t = 0.0, f = need0, mact = dmin_pos;
-        int a = a_lo;
-        for (int it = 0; it < 48; it++) {
-            double tn = t + (f - avail) / (double)a;
-            t = tn;
-            if (mact > tn) break;
-            double fn = 0.0, mn = INFINITY;
-            int an = 0;
+// 132-comparator network (Batcher odd-even merge for 32 restricted to 24
+// inputs), verified on all 2^24 binary inputs by scripts/gen_sortnet.py
+__device__ __forceinline__ void sort24_desc(double (&v)[24]) {
+    constexpr uint8_t net[132][2] = {
+        {0, 1}, {2, 3}, {0, 2}, {1, 3}, {1, 2}, {4, 5}, {6, 7}, {4, 6}, {5, 7}, {5, 6}, {0, 4},
+        {2, 6}, {2, 4}, {1, 5}, {3, 7}, {3, 5}, {1, 2}, {3, 4}, {5, 6}, {8, 9}, {10, 11}, {8, 10},
+        {9, 11}, {9, 10}, {12, 13}, {14, 15}, {12, 14}, {13, 15}, {13, 14}, {8, 12}, {10, 14},
+        {10, 12}, {9, 13}, {11, 15}, {11, 13}, {9, 10}, {11, 12}, {13, 14}, {0, 8}, {4, 12},
+        {4, 8}, {2, 10}, {6, 14}, {6, 10}, {2, 4}, {6, 8}, {10, 12}, {1, 9}, {5, 13}, {5, 9},
+        {3, 11}, {7, 15}, {7, 11}, {3, 5}, {7, 9}, {11, 13}, {1, 2}, {3, 4}, {5, 6}, {7, 8},
+        {9, 10}, {11, 12}, {13, 14}, {16, 17}, {18, 19}, {16, 18}, {17, 19}, {17, 18}, {20, 21},
+        {22, 23}, {20, 22}, {21, 23}, {21, 22}, {16, 20}, {18, 22}, {18, 20}, {17, 21}, {19, 23},
+        {19, 21}, {17, 18}, {19, 20}, {21, 22}, {18, 20}, {19, 21}, {17, 18}, {19, 20}, {21, 22},
+        {0, 16}, {8, 16}, {4, 20}, {12, 20}, {4, 8}, {12, 16}, {2, 18}, {10, 18}, {6, 22},
+        {14, 22}, {6, 10}, {14, 18}, {2, 4}, {6, 8}, {10, 12}, {14, 16}, {18, 20}, {1, 17},
+        {9, 17}, {5, 21}, {13, 21}, {5, 9}, {13, 17}, {3, 19}, {11, 19}, {7, 23}, {15, 23},
+        {7, 11}, {15, 19}, {3, 5}, {7, 9}, {11, 13}, {15, 17}, {19, 21}, {1, 2}, {3, 4}, {5, 6},
+        {7, 8}, {9, 10}, {11, 12}, {13, 14}, {15, 16}, {17, 18}, {19, 20}, {21, 22}};
 #pragma unroll
-            for (int h = 0; h < 24; h++) {
-                const double dh = day_d(r, h, ls, cs6);
-                const double e = dh - tn;
-                const bool on = e > 0.0;
-                an += on;
-                fn += fmax(e, 0.0);
-                mn = fmin(mn, on ? dh : INFINITY);
-            }
-            if (an == a || fn <= avail || an == 0) break;
-            f = fn;
-            a = an;
-            mact = mn;
+    for (int c = 0; c < 132; c++) cswap_desc(v[net[c][0]], v[net[c][1]]);
+}
+
+__device__ __forceinline__ double day_target_sorted(const double (&s)[24], double power,
+                                                    double avail) {
+    double need0 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 24; k++) need0 += fmin(s[k], power);
+    if (need0 <= avail) return 0.0;
+    if (s[0] <= power) {
+        double S = 0.0, SK = s[0];
+        int K = 1;
+#pragma unroll
+        for (int k = 1; k <= 24; k++) {
+            S += s[k - 1];
+            const bool ok = S - (double)k * s[k - 1] <= avail;
+            K = ok ? k : K;
+            SK = ok ? S : SK;
         }
-        return t;
+        return (SK - avail) / (double)K;
     }
-    double lo = 0.0, hi = dmax, f_hi = 0.0;
+    int a_lo = 0, b_lo = 0;
+#pragma unroll
+    for (int k = 0; k < 24; k++) {
+        a_lo += s[k] > 0.0;
+        b_lo += (s[k] - power) >= 0.0;
+    }
+    double lo = 0.0, hi = s[0], f_hi = 0.0;
     int a_hi = 0, b_hi = 0;
     for (int it = 0; it < 48; it++) {
         if (a_lo == a_hi && b_lo == b_hi) break;
-        double mid = 0.5 * (lo + hi);
+        const double mid = 0.5 * (lo + hi);
         double f = 0.0;
         int am = 0, bm = 0;
 #pragma unroll
-        for (int h = 0; h < 24; h++) {
-            const double e = day_d(r, h, ls, cs6) - mid;
+        for (int k = 0; k < 24; k++) {
+            const double e = s[k] - mid;
             am += e > 0.0;
             bm += (e - power) >= 0.0;
             f += fmin(fmax(e, 0.0), power);
@@ -435,12 +431,30 @@ __device__ __forceinline__ double day_target(const DayRaw& r, double ls, double 
         if (f <= avail) { hi = mid; f_hi = f; a_hi = am; b_hi = bm; }
         else { lo = mid; a_lo = am; b_lo = bm; }
     }
-    int k = a_hi - b_hi;
+    const int k = a_hi - b_hi;
     if (k <= 0) return hi;
     double t = hi - (avail - f_hi) / (double)k;
     if (t < lo) t = lo;
     if (t > hi) t = hi;
     return t;
+}
+
+struct DayRaw {
+    float s[24];
+    int32_t c[24];
+};
+
+__device__ __forceinline__ double opaque(double x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ float opaque_f(float x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ int32_t opaque_i(int32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
 }
 
 // Byte-addressed store into one hour row: `row` is wave-uniform (SGPRs), the
@@ -515,6 +529,36 @@ __device__ __forceinline__ void day_read(uint32_t a, DayRaw& r) {
                  : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(s5),
                    "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3), "=&v"(c4), "=&v"(c5)
                  : "n"(VM), "v"(a)
+                 : "memory");
+    const f32x4 sv[6] = {s0, s1, s2, s3, s4, s5};
+    const i32x4 cv[6] = {c0, c1, c2, c3, c4, c5};
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        r.s[4 * q + 0] = sv[q].x; r.s[4 * q + 1] = sv[q].y; r.s[4 * q + 2] = sv[q].z; r.s[4 * q + 3] = sv[q].w;
+        r.c[4 * q + 0] = cv[q].x; r.c[4 * q + 1] = cv[q].y; r.c[4 * q + 2] = cv[q].z; r.c[4 * q + 3] = cv[q].w;
+    }
+}
+
+// Read the day buffer again (no vmcnt wait: it already landed).
+__device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
+    f32x4 s0, s1, s2, s3, s4, s5;
+    i32x4 c0, c1, c2, c3, c4, c5;
+    asm volatile("ds_read_b128 %0, %12\n\t"
+                 "ds_read_b128 %1, %12 offset:1024\n\t"
+                 "ds_read_b128 %2, %12 offset:2048\n\t"
+                 "ds_read_b128 %3, %12 offset:3072\n\t"
+                 "ds_read_b128 %4, %12 offset:4096\n\t"
+                 "ds_read_b128 %5, %12 offset:5120\n\t"
+                 "ds_read_b128 %6, %12 offset:6144\n\t"
+                 "ds_read_b128 %7, %12 offset:7168\n\t"
+                 "ds_read_b128 %8, %12 offset:8192\n\t"
+                 "ds_read_b128 %9, %12 offset:9216\n\t"
+                 "ds_read_b128 %10, %12 offset:10240\n\t"
+                 "ds_read_b128 %11, %12 offset:11264\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(s0), "=&v"(s1), "=&v"(s2), "=&v"(s3), "=&v"(s4), "=&v"(s5),
+                   "=&v"(c0), "=&v"(c1), "=&v"(c2), "=&v"(c3), "=&v"(c4), "=&v"(c5)
+                 : "v"(a)
                  : "memory");
     const f32x4 sv[6] = {s0, s1, s2, s3, s4, s5};
     const i32x4 cv[6] = {c0, c1, c2, c3, c4, c5};
@@ -640,25 +684,20 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             const uint64_t* nsr =
                 reinterpret_cast<const uint64_t*>(((dx % 7) >= 5) ? t.wkend[mx] : t.wkday[mx]);
             const uint64_t nsched[3] = {nsr[0], nsr[1], nsr[2]};
-            if (d < d_last) day_dma(d + 1);
             double target = 0.0;
             if (has_batt) {
-                // day statistics of d_h = max(load_h - pv_h, 0) for the target
-                double need0 = 0.0, dmax = 0.0, dmin_pos = INFINITY;
-                int a0 = 0, b0 = 0;
+                // the day's deficits d_h = max(load_h - pv_h, 0), sorted; the raw
+                // registers are dead meanwhile and re-read from the LDS buffer
+                double dv[24];
 #pragma unroll
-                for (int hh = 0; hh < 24; hh++) {
-                    const double dd = fmax((double)r.s[hh] * ls - (double)r.c[hh] * cs6, 0.0);
-                    dmax = fmax(dmax, dd);
-                    need0 += fmin(dd, power);
-                    const bool on = dd > 0.0;
-                    a0 += on;
-                    b0 += (dd - power) >= 0.0;
-                    dmin_pos = fmin(dmin_pos, on ? dd : INFINITY);
-                }
+                for (int hh = 0; hh < 24; hh++)
+                    dv[hh] = fmax((double)r.s[hh] * ls - (double)r.c[hh] * cs6, 0.0);
+                sort24_desc(dv);
                 const double avail = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
-                target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0, dmin_pos);
+                target = day_target_sorted(dv, power, avail);
+                day_reread(dlane, r);
             }
+            if (d < d_last) day_dma(d + 1);                     // after the last read of the buffer
             const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);
 #pragma unroll
             for (int hh = 0; hh < 24; hh++) {

@@ -364,43 +364,44 @@ void orc_batt_size(double desired_kw, double desired_kwh, double desired_v, cons
  * exact in a few steps.  Otherwise bisect [0, max d] until no breakpoint lies
  * inside the bracket (the counts a = #{d > T} and b = #{d - P >= T} agree at
  * both ends), then solve the linear piece exactly (slope -(a - b)). */
+/* Daily peak-shaving target: smallest T >= 0 with
+ * f(T) = sum_h min(max(d_h - T, 0), P) <= E over the day's deficits
+ * d_h = max(load_h - pv_h, 0), evaluated on the deficits sorted descending
+ * (s[0] = max; every sum below runs in that order, as on the device).
+ * No saturated hour (s[0] <= P): f(T) = max_k (S_k - k T), S_k the sum of the
+ * k largest, so T = (S_K - E) / K for the largest K with S_K - K s[K-1] <= E.
+ * Otherwise bisection until no breakpoint (s_k, s_k - P) lies inside the
+ * bracket, then the exact linear piece. */
 static double day_target(const double* load, const double* pv, int h0, double power, double avail) {
-    double d[24];
-    double need0 = 0.0, dmax = 0.0;
-    int a_lo = 0, b_lo = 0;
+    double s[24];
     for (int k = 0; k < 24; k++) {
         double v = load[h0 + k] - pv[h0 + k];
-        if (v < 0.0) v = 0.0;
-        d[k] = v;
-        if (v > dmax) dmax = v;
-        need0 += v < power ? v : power;
-        a_lo += v > 0.0;
-        b_lo += (v - power) >= 0.0;
+        s[k] = v > 0.0 ? v : 0.0;
     }
+    for (int i = 1; i < 24; i++) {          /* insertion sort, descending */
+        double x = s[i];
+        int j = i - 1;
+        while (j >= 0 && s[j] < x) { s[j + 1] = s[j]; j--; }
+        s[j + 1] = x;
+    }
+    double need0 = 0.0;
+    for (int k = 0; k < 24; k++) need0 += s[k] < power ? s[k] : power;
     if (need0 <= avail) return 0.0;
-    if (dmax <= power) {
-        /* no hour saturates: f(T) = sum max(d - T, 0) is convex and decreasing,
-         * so Newton from T = 0 stays left of the root and is exact once the
-         * active count stops changing. */
-        double t = 0.0, f = need0;
-        int a = a_lo;
-        for (int it = 0; it < 48; it++) {
-            double tn = t + (f - avail) / (double)a;
-            double fn = 0.0;
-            int an = 0;
-            for (int k = 0; k < 24; k++) {
-                double e = d[k] - tn;
-                an += e > 0.0;
-                fn += e > 0.0 ? e : 0.0;
-            }
-            t = tn;
-            if (an == a || fn <= avail || an == 0) break;
-            f = fn;
-            a = an;
+    if (s[0] <= power) {
+        double S = 0.0, SK = s[0];
+        int K = 1;
+        for (int k = 1; k <= 24; k++) {
+            S += s[k - 1];
+            if (S - (double)k * s[k - 1] <= avail) { K = k; SK = S; }
         }
-        return t;
+        return (SK - avail) / (double)K;
     }
-    double lo = 0.0, hi = dmax, f_hi = 0.0;
+    int a_lo = 0, b_lo = 0;
+    for (int k = 0; k < 24; k++) {
+        a_lo += s[k] > 0.0;
+        b_lo += (s[k] - power) >= 0.0;
+    }
+    double lo = 0.0, hi = s[0], f_hi = 0.0;
     int a_hi = 0, b_hi = 0;
     for (int it = 0; it < 48; it++) {
         if (a_lo == a_hi && b_lo == b_hi) break;
@@ -408,7 +409,7 @@ static double day_target(const double* load, const double* pv, int h0, double po
         double f = 0.0;
         int am = 0, bm = 0;
         for (int k = 0; k < 24; k++) {
-            double e = d[k] - mid;
+            double e = s[k] - mid;
             am += e > 0.0;
             bm += (e - power) >= 0.0;
             if (e < 0.0) e = 0.0;
