@@ -941,6 +941,12 @@ constexpr int PREG = 4;
 __device__ __forceinline__ double yl_bill_mo0_reg(const dgen_tariff& t, const YLds& S, double gscale,
                                                   double yearend) {
     const int P = t.P, T = t.T, half = S.half;
+    const double fixed = t.fixed;
+    const bool daily = t.unit == 2;
+    // first-tier prices in registers (every month reads them)
+    double b0[PREG];
+#pragma unroll
+    for (int p = 0; p < PREG; p++) b0[p] = p < P ? t.buy[p][0] : 0.0;
     double credit[PREG], u[PREG];
 #pragma unroll
     for (int p = 0; p < PREG; p++) { credit[p] = 0.0; u[p] = 0.0; }
@@ -964,20 +970,32 @@ __device__ __forceinline__ double yl_bill_mo0_reg(const dgen_tariff& t, const YL
             if (p < P) U += u[p];
         double charge = 0.0;
         if (U > 0.0) {
-            double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
-            double prev = 0.0;
-            for (int k = 0; k < T; k++) {
-                double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
-                double top = U < hi ? U : hi;
-                double amt = top - prev;
-                if (amt < 0.0) amt = 0.0;
-                if (hi > prev) prev = hi;
+            // each period's share of the month, once per month (the same
+            // quotient the tier loop used to recompute per tier)
+            double fr[PREG];
+#pragma unroll
+            for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
+            if (T == 1) {
+                // one tier: hi = inf, amt = U
 #pragma unroll
                 for (int p = 0; p < PREG; p++)
-                    if (p < P) charge += (u[p] / U) * amt * t.buy[p][k];
+                    if (p < P) charge += fr[p] * U * b0[p];
+            } else {
+                const double scale = daily ? (double)c_days_in_month[m] : 1.0;
+                double prev = 0.0;
+                for (int k = 0; k < T; k++) {
+                    double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
+                    double top = U < hi ? U : hi;
+                    double amt = top - prev;
+                    if (amt < 0.0) amt = 0.0;
+                    if (hi > prev) prev = hi;
+#pragma unroll
+                    for (int p = 0; p < PREG; p++)
+                        if (p < P) charge += fr[p] * amt * (k == 0 ? b0[p] : t.buy[p][k]);
+                }
             }
         }
-        double bill = t.fixed + charge;
+        double bill = fixed + charge;
         if (m == 11) {
             double cc = 0.0;
 #pragma unroll

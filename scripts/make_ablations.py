@@ -50,6 +50,11 @@ VARIANTS = {
     # hourly planes written with plain (temporal) stores instead of nt
     "plain_stores": [("    __builtin_nontemporal_store(v, reinterpret_cast<float*>(row + off));",
                       "    *reinterpret_cast<float*>(row + off) = v;")],
+    # k_size: Brent stops after its first evaluation (per-evaluation cost)
+    "ks_one_eval": [("    while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {", "    while (false) {")],
+    # k_size: no NEM bill (per-lane year bill replaced by a constant)
+    "ks_no_bill": [("    return (t.P <= PREG) ? yl_bill_mo0_reg(t, S, gscale, yearend) : yl_bill_mo0(t, S, gscale, yearend);",
+                    "    return 100.0 + gscale;")],
     "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
                  "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
 }
