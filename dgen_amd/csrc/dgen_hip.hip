@@ -887,6 +887,11 @@ __device__ __forceinline__ double yl_month_charge(const dgen_tariff& t, int m, c
     double U = 0.0;
     for (int p = 0; p < P; p++) U += S.at(uoff + p);
     if (!(U > 0.0)) return 0.0;
+    if (T == 1) {                       // one tier: sum_p u_p * buy_p (oracle order)
+        double charge = 0.0;
+        for (int p = 0; p < P; p++) charge += S.at(uoff + p) * t.buy[p][0];
+        return charge;
+    }
     double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
     double charge = 0.0, prev = 0.0;
     for (int k = 0; k < T; k++) {
@@ -970,17 +975,18 @@ __device__ __forceinline__ double yl_bill_mo0_reg(const dgen_tariff& t, const YL
             if (p < P) U += u[p];
         double charge = 0.0;
         if (U > 0.0) {
-            // each period's share of the month, once per month (the same
-            // quotient the tier loop used to recompute per tier)
-            double fr[PREG];
-#pragma unroll
-            for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
             if (T == 1) {
-                // one tier: hi = inf, amt = U
+                // one tier: every period's kWh at its own price (the oracle's
+                // month_energy_charge; no share / re-multiplication)
 #pragma unroll
                 for (int p = 0; p < PREG; p++)
-                    if (p < P) charge += fr[p] * U * b0[p];
+                    if (p < P) charge += u[p] * b0[p];
             } else {
+                // each period's share of the month, once per month (the same
+                // quotient the tier loop used to recompute per tier)
+                double fr[PREG];
+#pragma unroll
+                for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
                 const double scale = daily ? (double)c_days_in_month[m] : 1.0;
                 double prev = 0.0;
                 for (int k = 0; k < T; k++) {

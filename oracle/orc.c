@@ -133,11 +133,18 @@ static void hour_calendar(const orc_tariff* t, int* month_of, int* period_of) {
 }
 
 /* Energy charge for one month: tier amounts from total monthly usage U, each
- * period billed its share u_p/U of every tier at its own price. */
+ * period billed its share u_p/U of every tier at its own price.  One tier:
+ * every period's kWh at its own price, sum_p u_p * buy_p (the same quantity
+ * without the share / re-multiplication round trip). */
 static double month_energy_charge(const orc_tariff* t, int m, const double* u) {
     double U = 0.0;
     for (int p = 0; p < t->P; p++) U += u[p];
     if (!(U > 0.0)) return 0.0;
+    if (t->T == 1) {
+        double charge = 0.0;
+        for (int p = 0; p < t->P; p++) charge += u[p] * t->buy[p][0];
+        return charge;
+    }
     double scale = (t->unit == 2) ? (double)kDaysInMonth[m] : 1.0;
     double charge = 0.0, prev = 0.0;
     for (int k = 0; k < t->T; k++) {
