@@ -462,8 +462,13 @@ __device__ __forceinline__ int32_t opaque_i(int32_t x) {
 // The hourly output planes (105 KB per agent, read by nobody in the step) go
 // out non-temporal so they do not evict the profile-row slices the resident
 // waves share from L2 / MALL (1M agents: 33.2 -> 31.8 ms).
+// Written as the scalar-base form (global_store v_off, v_data, s[base]): the
+// wave-uniform row base stays in SGPRs and the per-hour 64-bit vector address
+// adds the compiler otherwise emits (3 per hour) disappear.  The store is
+// invisible to the compiler's vmcnt bookkeeping, which only makes its waits
+// stricter (vmcnt retires in issue order).
 __device__ __forceinline__ void st_f32(char* row, uint32_t off, float v) {
-    __builtin_nontemporal_store(v, reinterpret_cast<float*>(row + off));
+    asm volatile("global_store_dword %0, %1, %2 nt" :: "v"(off), "v"(v), "s"(row) : "memory");
 }
 __device__ __forceinline__ void st_f64(char* row, uint32_t off, double v) {
     *reinterpret_cast<double*>(row + off) = v;

@@ -48,7 +48,7 @@ VARIANTS = {
     "ks_no_slot_loads": [("                    lv[k] = lm[dt * 24 + h0 + k];\n                    gv[k] = gm[dt * 24 + h0 + k];",
                           "                    lv[k] = 1.0 + k; gv[k] = 0.5 + k;")],
     # hourly planes written with plain (temporal) stores instead of nt
-    "plain_stores": [("    __builtin_nontemporal_store(v, reinterpret_cast<float*>(row + off));",
+    "plain_stores": [("    asm volatile(\"global_store_dword %0, %1, %2 nt\" :: \"v\"(off), \"v\"(v), \"s\"(row) : \"memory\");",
                       "    *reinterpret_cast<float*>(row + off) = v;")],
     # k_size: Brent stops after its first evaluation (per-evaluation cost)
     "ks_one_eval": [("    while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {", "    while (false) {")],
