@@ -106,6 +106,7 @@ EXPORTED = [
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
     "dgen_kernel_times", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
     "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
+    "dgen_finance_series",
 ]
 
 
@@ -149,6 +150,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
                                     ctypes.POINTER(_f64)]
     L.dgen_set_pipeline.restype = _i32
     L.dgen_set_pipeline.argtypes = [_vp, _i32]
+    L.dgen_finance_series.restype = _i32
+    L.dgen_finance_series.argtypes = [_vp, ctypes.POINTER(Outputs), _vp, _i64, _vp, _vp]
     L.dgen_set_hourly_segment.restype = _i32
     L.dgen_set_hourly_segment.argtypes = [_vp, _i32]
     L.dgen_segment_sums.restype = _i32

@@ -43,6 +43,12 @@ constexpr int MAXY = DGEN_MAXY;
 constexpr int NBIN = 12 * MAXP;
 constexpr int BLOCK = 128;   // threads per block for the per-agent kernels
 constexpr int HB_DAY_BYTES = 12 * 1024;   // k_hourly_batt day buffer per wave (LDS)
+typedef __attribute__((address_space(3))) char* lds_ptr_t;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+#ifndef DGEN_HOURLY_TILE
+#define DGEN_HOURLY_TILE 1
+#endif
 
 __constant__ int c_month_start_day[13] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334, 365};
 __constant__ int c_days_in_month[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
@@ -462,6 +468,10 @@ __device__ __forceinline__ int32_t opaque_i(int32_t x) {
 // The hourly output planes (105 KB per agent, read by nobody in the step) go
 // out non-temporal so they do not evict the profile-row slices the resident
 // waves share from L2 / MALL (1M agents: 33.2 -> 31.8 ms).
+__device__ __forceinline__ void st_f32x4(char* row, uint32_t off, const float (&q)[4]) {
+    const f32x4 v = {q[0], q[1], q[2], q[3]};
+    asm volatile("global_store_dwordx4 %0, %1, %2 nt" :: "v"(off), "v"(v), "s"(row) : "memory");
+}
 // Written as the scalar-base form (global_store v_off, v_data, s[base]): the
 // wave-uniform row base stays in SGPRs and the per-hour 64-bit vector address
 // adds the compiler otherwise emits (3 per hour) disappear.  The store is
@@ -501,9 +511,6 @@ __device__ __forceinline__ HourStep batt_hour(double nn, double pv, double targe
     return r;
 }
 
-typedef __attribute__((address_space(3))) char* lds_ptr_t;
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // 16 B per lane global -> LDS at lds + lane * 16 (m0 = wave-uniform base)
 __device__ __forceinline__ void lds_dma16(const void* g, uint32_t lds) {
@@ -641,6 +648,14 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     char* const ow = reinterpret_cast<char*>(O.net_with_batt);
     char* const osc = reinterpret_cast<char*>(W.scratch);
     size_t ho4 = (size_t)d_lo * 24 * row4, ho8 = (size_t)d_lo * 24 * row8;
+#if DGEN_HOURLY_TILE == 4
+    // hour-quad tiles: (hour h, agent i) at ((h / 4) * n + i) * 4 + h % 4, so a
+    // lane writes 16 B and a wave 1 KB contiguous per plane every 4 hours
+    const uint32_t off16 = (uint32_t)i * 16u;
+    const size_t row16 = (size_t)n * 16u;
+    size_t q16 = (size_t)d_lo * 6 * row16;
+    float qb[4], qp[4], qw[4];
+#endif
 
     // Software pipeline over days through LDS: the next day's raw profile
     // values (96 B of the shape row + 96 B of the cf row per lane) are DMA'd
@@ -716,9 +731,21 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                                         in_per_bank, out_per_bank);
                 if constexpr (HOURLY) {
                     const double dn = ld - pl;
+#if DGEN_HOURLY_TILE == 4
+                    qb[hh & 3] = (float)ld;
+                    qp[hh & 3] = (float)fmax(dn, 0.0);
+                    qw[hh & 3] = (float)st.g2l;
+                    if ((hh & 3) == 3) {
+                        st_f32x4(ob + q16, off16, qb);
+                        st_f32x4(op + q16, off16, qp);
+                        st_f32x4(ow + q16, off16, qw);
+                        q16 += row16;
+                    }
+#else
                     st_f32(ob + ho4, off4, (float)ld);
                     st_f32(op + ho4, off4, (float)fmax(dn, 0.0));
                     st_f32(ow + ho4, off4, (float)st.g2l);
+#endif
                 }
                 ho4 += row4;
                 if (put_sys) {
@@ -1791,6 +1818,29 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
         __syncthreads();
     }
 }
+
+// ---------------------------------------------------------------------------
+// Finance-series export: finance_series_export._norm25 over the
+// six 26-long yearly arrays of every agent, finance_series_export.py:9-20 --
+// first 25 entries, zero past the agent's list length (N + 1), non-finite -> 0.
+// Thread per (agent, series, entry); out [6][n][25].
+// ---------------------------------------------------------------------------
+constexpr int NORM25 = 25;
+struct Series6 {
+    const double* p[6];
+};
+__global__ void k_finance_series(Series6 src, const int32_t* __restrict__ len, int64_t n,
+                                 int32_t stride, double* __restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 6 * n * NORM25) return;
+    const int c = (int)(t / (n * NORM25));
+    const int64_t r = t - (int64_t)c * n * NORM25;
+    const int64_t i = r / NORM25;
+    const int k = (int)(r - i * NORM25);
+    double v = 0.0;
+    if (k < len[i]) v = src.p[c][i * stride + k];
+    out[t] = isfinite(v) ? v : 0.0;
+}
 }  // namespace
 
 // ===========================================================================
@@ -2210,6 +2260,25 @@ int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
         hipLaunchKernelGGL(k_state_hourly<double>, grid, dim3(256), 0, (hipStream_t)stream,
                            (const double*)baseline, (const double*)pvonly, (const double*)with_batt,
                            w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_finance_series(dgen_ctx* c, const dgen_outputs* O, const int32_t* list_len, int64_t n,
+                            double* out, void* stream) {
+    if (!c || !O || !list_len || !out || n < 0) {
+        set_err("dgen_finance_series: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n == 0) return DGEN_OK;
+    Series6 src = {{O->cfev_pv, O->bill_w_pv, O->bill_wo_pv, O->cfev_batt, O->bill_w_batt,
+                    O->bill_wo_batt}};
+    for (const double* p : src.p)
+        if (!p) { set_err("dgen_finance_series: missing yearly output"); return DGEN_E_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t total = 6 * n * NORM25;
+    hipLaunchKernelGGL(k_finance_series, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, src, list_len, n, (int32_t)(MAXY + 1), out);
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
 }

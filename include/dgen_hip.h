@@ -338,6 +338,19 @@ int32_t dgen_state_hourly(dgen_ctx* ctx, const void* baseline, const void* pvonl
                           int32_t n_hours, const int64_t* seg_off, int64_t n_seg, double* out,
                           void* stream);
 
+/* ------------------------------------------------------------------------
+ * Finance-series export, finance_series_export.py:9-81:
+ * _norm25 of the six yearly arrays the export writes per agent, in the
+ * reference's column order -- cf_energy_value / utility_bill_w_sys /
+ * utility_bill_wo_sys of the pv_only case, then of the pv_batt case (O's
+ * cfev_pv, bill_w_pv, bill_wo_pv, cfev_batt, bill_w_batt, bill_wo_batt).
+ * Entry k of agent i = O.<series>[i * (DGEN_MAXY + 1) + k] for k < list_len[i]
+ * (the agent's list length, economic life + 1), 0 otherwise; first 25 entries
+ * (the 26-long lists are truncated); non-finite -> 0.  out: [6][n][25] f64.
+ * ---------------------------------------------------------------------- */
+int32_t dgen_finance_series(dgen_ctx* ctx, const dgen_outputs* O, const int32_t* list_len, int64_t n,
+                            double* out, void* stream);
+
 /* Average per-call kernel time (ms) of the dgen_size_agents calls since the
  * previous query: k_size, k_hourly_batt, k_batt_finance, each summed over the
  * call's chunks (HIP events recorded on the stream each kernel runs on).

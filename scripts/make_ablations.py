@@ -33,8 +33,9 @@ VARIANTS = {
     "ks_w3": [(KS, occ(KS, 3))],
     "ks_w4": [(KS, occ(KS, 4))],
     "kf_w6": [(KF, occ(KF, 6))],
-    "no_target": [("target = day_target(r, ls, cs6, power, avail, dmax, need0, a0, b0, dmin_pos);",
-                   "target = 0.0; asm volatile(\"\" :: \"v\"(need0), \"v\"(dmax), \"v\"(a0), \"v\"(b0), \"v\"(avail), \"v\"(dmin_pos));")],
+    "no_target": [("                target = day_target_sorted(dv, power, avail);",
+                   "                target = 0.0; asm volatile(\"\" :: \"v\"(dv[0]), \"v\"(dv[23]), \"v\"(avail));")],
+    "no_sort": [("                sort24_desc(dv);", "")],
     "no_hourly_stores": [("st_f32(ob + ho4, off4, (float)ld);", "asm volatile(\"\" :: \"v\"(ld));"),
                          ("st_f32(op + ho4, off4, (float)fmax(dn, 0.0));", "asm volatile(\"\" :: \"v\"(dn));"),
                          ("st_f32(ow + ho4, off4, (float)st.g2l);", "asm volatile(\"\" :: \"v\"(st.g2l));")],
@@ -42,8 +43,10 @@ VARIANTS = {
                      "            if (false) {\n                // day statistics")],
     # profile loads always from the agent's first two days (L1/L2-resident):
     # measures how much of the scan waits on the day loads
-    "hot_loads": [("const float4* s4 = reinterpret_cast<const float4*>(shp + h0);\n            const int4* c4 = reinterpret_cast<const int4*>(cfp + h0);",
-                   "const float4* s4 = reinterpret_cast<const float4*>(shp + (d & 1) * 24);\n            const int4* c4 = reinterpret_cast<const int4*>(cfp + (d & 1) * 24);")],
+    "hot_loads": [("lds_dma16(shp + dd * 24 + 4 * q, dbase_s + q * 1024u);",
+                   "lds_dma16(shp + (dd & 1) * 24 + 4 * q, dbase_s + q * 1024u);"),
+                  ("lds_dma16(cfp + dd * 24 + 4 * q, dbase_s + (6 + q) * 1024u);",
+                   "lds_dma16(cfp + (dd & 1) * 24 + 4 * q, dbase_s + (6 + q) * 1024u);")],
     # k_size: slot-sum bins without their global loads (constant slot sums)
     "ks_no_slot_loads": [("                    lv[k] = lm[dt * 24 + h0 + k];\n                    gv[k] = gm[dt * 24 + h0 + k];",
                           "                    lv[k] = 1.0 + k; gv[k] = 0.5 + k;")],
@@ -55,6 +58,8 @@ VARIANTS = {
     # k_size: no NEM bill (per-lane year bill replaced by a constant)
     "ks_no_bill": [("    return (t.P <= PREG) ? yl_bill_mo0_reg(t, S, gscale, yearend) : yl_bill_mo0(t, S, gscale, yearend);",
                     "    return 100.0 + gscale;")],
+    # hourly planes in hour-quad tiles (16 B per lane, 1 KB per wave per store)
+    "tile4": [("#define DGEN_HOURLY_TILE 1\n", "#define DGEN_HOURLY_TILE 4\n")],
     "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
                  "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
 }

@@ -149,3 +149,24 @@ def golden_attach():
         k = c["name"]
         hourly[k] = tuple(z[f"{k}__{p}"].astype(np.float64) for p in ("baseline", "pvonly", "with_batt"))
     return meta, hourly
+
+
+def _dec(cell):
+    """finance_series.json cell -> the Python value the reference saw."""
+    f = lambda x: float(x) if isinstance(x, str) and x in ("nan", "inf", "-inf") else x
+    if "list" in cell:
+        return [f(x) for x in cell["list"]]
+    if "array" in cell:
+        return np.asarray([f(x) for x in cell["array"]], dtype=float)
+    return f(cell["scalar"])
+
+
+@lru_cache(maxsize=None)
+def golden_finance():
+    """finance_series.json with the input rows decoded (lists, numpy arrays,
+    scalars, non-finite floats) -- cases[k]['rows'] are dicts per agent."""
+    with open(os.path.join(GOLDEN, "finance_series.json")) as f:
+        meta = json.load(f)
+    for c in meta["cases"]:
+        c["rows"] = [{k: _dec(v) for k, v in r.items()} for r in c["rows"]]
+    return meta
