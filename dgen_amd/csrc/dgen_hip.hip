@@ -327,7 +327,7 @@ __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, d
 struct WsLayout {
     // doubles, plane-major [k][n]
     double* carry;    // NBIN planes: [0] SOC, [1] annual PV kWh between month-segment launches
-    double* G;        // NBIN planes (unused)
+    double* aux;      // NBIN planes: [0] 1.0 where the storage switch changed the tariff
     double2* LGb;     // [n][NBIN] (load, system) bins, battery case, final tariff (2 NBIN planes)
     double* otc_b;    // 1 plane: storage one-time charge
     double* scratch;  // [8760][n_scratch] battery system output (mo 2)
@@ -337,7 +337,7 @@ __host__ __device__ inline WsLayout ws_layout(void* base, int64_t n) {
     WsLayout w;
     double* p = (double*)base;
     w.carry = p; p += (int64_t)NBIN * n;
-    w.G = p; p += (int64_t)NBIN * n;
+    w.aux = p; p += (int64_t)NBIN * n;
     w.LGb = reinterpret_cast<double2*>(p); p += (int64_t)2 * NBIN * n;
     w.otc_b = p; p += n;
     w.scratch = p;
@@ -780,6 +780,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     O.capacity_factor[i] = naep / 8760.0;
     O.batt_kw[i] = has_batt ? power : 0.0;
     O.batt_kwh[i] = bank;
+    // battery run on the PV run's tariff: k_batt_finance reuses its no-system
+    // bill (same load, same tariff -> the same bill, as in the oracle)
+    W.aux[i] = (tariff != O.tariff_final[i]) ? 1.0 : 0.0;
     O.tariff_final[i] = tariff;
     O.switched[i] = switched;
     O.status[i] = status;
@@ -1435,6 +1438,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     const double kw = O.system_kw[i];
     const double bank = O.batt_kwh[i];
     const double otc = W.otc_b[i];
+    const bool same_tariff = W.aux[i] == 0.0;    // no storage switch: k_size's wo1 applies
     const double rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
     const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
     const double r_y = pow_seq(rate_base, y - 1), s_y = pow_seq(sys_base, y - 1);
@@ -1454,7 +1458,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             S.G[m * half + p] = b.y;
         }
         wave_lds_sync();
-        wo1 = yl_bill_nem(t, S, 0.0, cfg.nm_yearend_sell_rate);
+        wo1 = same_tariff ? O.first_without[i] : yl_bill_nem(t, S, 0.0, cfg.nm_yearend_sell_rate);
         wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
     } else {
         YSrc src;
@@ -1469,7 +1473,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         const int wr = A.wholesale_row[i];
         src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
         src.ts_mult = A.price_mult[i];
-        wo1 = yl_bill_mo2(t, src, 1.0, false, S);
+        wo1 = same_tariff ? O.first_without[i] : yl_bill_mo2(t, src, 1.0, false, S);
         wb = yl_bill_mo2(t, src, s_y, true, S);
     }
     double w = wb * r_y;
