@@ -1065,6 +1065,114 @@ struct YSrc {
     double ts_mult;
 };
 
+// Month energy charge from register-held billed kWh (P <= PREG), the same
+// arithmetic and order as yl_month_charge.
+__device__ __forceinline__ double reg_month_charge(const dgen_tariff& t, int m, const double (&u)[PREG]) {
+    const int P = t.P, T = t.T;
+    double U = 0.0;
+#pragma unroll
+    for (int p = 0; p < PREG; p++)
+        if (p < P) U += u[p];
+    if (!(U > 0.0)) return 0.0;
+    double charge = 0.0;
+    if (T == 1) {
+#pragma unroll
+        for (int p = 0; p < PREG; p++)
+            if (p < P) charge += u[p] * t.buy[p][0];
+        return charge;
+    }
+    double fr[PREG];
+#pragma unroll
+    for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
+    const double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
+    double prev = 0.0;
+    for (int k = 0; k < T; k++) {
+        double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
+        double top = U < hi ? U : hi;
+        double amt = top - prev;
+        if (amt < 0.0) amt = 0.0;
+        if (hi > prev) prev = hi;
+#pragma unroll
+        for (int p = 0; p < PREG; p++)
+            if (p < P) charge += fr[p] * amt * t.buy[p][k];
+    }
+    return charge;
+}
+
+// Net-billing (mo 2) bill with the per-period import / export sums in
+// registers (P <= PREG).  The hour loop of yl_bill_mo2 waited on two loads
+// and an LDS read-modify-write per hour; here each 8-hour chunk's profile
+// (and system output / sell-rate) values are loaded together before use, and
+// each hour adds dd (or the export credit) into its period's register, the
+// others adding an exact +0.0 -- the same sums in the same hour order.
+constexpr int MO2_CH = 4;
+__device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YSrc& src, double s,
+                                                  bool with_gen) {
+    const int P = t.P;
+    double total = 0.0;
+    int h = 0;
+    for (int m = 0; m < 12; m++) {
+        double imp[PREG], exv[PREG];
+#pragma unroll
+        for (int p = 0; p < PREG; p++) { imp[p] = 0.0; exv[p] = 0.0; }
+        for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++, h += 24) {
+            const uint64_t* sr = reinterpret_cast<const uint64_t*>(((d % 7) >= 5) ? t.wkend[m] : t.wkday[m]);
+#pragma unroll 1
+            for (int c0 = 0; c0 < 24; c0 += MO2_CH) {
+                const uint64_t sch = sr[c0 / 8] >> (8 * (c0 % 8));
+                float sh[MO2_CH];
+                double g[MO2_CH], tsv[MO2_CH];
+#pragma unroll
+                for (int k = 0; k < MO2_CH; k += 4) {
+                    const float4 a = *reinterpret_cast<const float4*>(src.shape + h + c0 + k);
+                    sh[k] = a.x; sh[k + 1] = a.y; sh[k + 2] = a.z; sh[k + 3] = a.w;
+                }
+#pragma unroll
+                for (int k = 0; k < MO2_CH; k++) g[k] = 0.0;
+                if (with_gen) {
+                    if (src.sysgen) {
+#pragma unroll
+                        for (int k = 0; k < MO2_CH; k++) g[k] = src.sysgen[(int64_t)(h + c0 + k) * src.sys_stride];
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < MO2_CH; k += 4) {
+                            const int4 a = *reinterpret_cast<const int4*>(src.cf + h + c0 + k);
+                            g[k] = ((double)a.x / 1e6) * src.gen_scale;
+                            g[k + 1] = ((double)a.y / 1e6) * src.gen_scale;
+                            g[k + 2] = ((double)a.z / 1e6) * src.gen_scale;
+                            g[k + 3] = ((double)a.w / 1e6) * src.gen_scale;
+                        }
+                    }
+                }
+                if (src.ts) {
+#pragma unroll
+                    for (int k = 0; k < MO2_CH; k++) tsv[k] = src.ts[h + c0 + k];
+                }
+#pragma unroll
+                for (int k = 0; k < MO2_CH; k++) {
+                    const double load = (double)sh[k] * src.load_scale;
+                    const double dd = load - g[k] * s;
+                    const int p = (int)((sch >> (8 * k)) & 0xffu);
+                    const bool pos = dd > 0.0;
+                    double e = -dd;
+                    if (src.ts) e *= (double)(float)(tsv[k] * src.ts_mult);
+#pragma unroll
+                    for (int q = 0; q < PREG; q++) {
+                        imp[q] += (pos && p == q) ? dd : 0.0;
+                        exv[q] += (!pos && p == q) ? e : 0.0;
+                    }
+                }
+            }
+        }
+        double cr = 0.0;
+#pragma unroll
+        for (int p = 0; p < PREG; p++)
+            if (p < P) cr += src.ts ? exv[p] : exv[p] * t.sell[p][0];
+        total += t.fixed + reg_month_charge(t, m, imp) - cr;
+    }
+    return total;
+}
+
 // Net-billing (mo 2) bill of the lane's year (system output x s).
 __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& src, double s,
                                               bool with_gen, const YLds& S) {
@@ -1101,6 +1209,13 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
         total += t.fixed + yl_month_charge(t, m, S, 0) - cr;
     }
     return total;
+}
+
+// k_batt_finance's net-billing bills (k_size keeps the LDS version: the register
+// version's chunk buffers push its 168-VGPR budget into spills, measured slower)
+__device__ __forceinline__ double yl_bill_net(const dgen_tariff& t, const YSrc& src, double s,
+                                              bool with_gen, const YLds& S) {
+    return (t.P <= PREG) ? yl_bill_mo2_reg(t, src, s, with_gen) : yl_bill_mo2(t, src, s, with_gen, S);
 }
 
 // bins of a tariff from a row's slot sums, one (month, period) cell per lane
@@ -1473,8 +1588,8 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         const int wr = A.wholesale_row[i];
         src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
         src.ts_mult = A.price_mult[i];
-        wo1 = same_tariff ? O.first_without[i] : yl_bill_mo2(t, src, 1.0, false, S);
-        wb = yl_bill_mo2(t, src, s_y, true, S);
+        wo1 = same_tariff ? O.first_without[i] : yl_bill_net(t, src, 1.0, false, S);
+        wb = yl_bill_net(t, src, s_y, true, S);
     }
     double w = wb * r_y;
     double wo = wo1 * r_y;

@@ -35,6 +35,7 @@ VARIANTS = {
     "kf_w6": [(KF, occ(KF, 6))],
     "no_target": [("                target = day_target_sorted(dv, power, avail);",
                    "                target = 0.0; asm volatile(\"\" :: \"v\"(dv[0]), \"v\"(dv[23]), \"v\"(avail));")],
+    "no_bisect": [("    if (s[0] <= power) {\n        double S = 0.0, SK = s[0];", "    if (true) {\n        double S = 0.0, SK = s[0];")],
     "no_sort": [("                sort24_desc(dv);", "")],
     "no_hourly_stores": [("st_f32(ob + ho4, off4, (float)ld);", "asm volatile(\"\" :: \"v\"(ld));"),
                          ("st_f32(op + ho4, off4, (float)fmax(dn, 0.0));", "asm volatile(\"\" :: \"v\"(dn));"),
@@ -60,6 +61,11 @@ VARIANTS = {
                     "    return 100.0 + gscale;")],
     # hourly planes in hour-quad tiles (16 B per lane, 1 KB per wave per store)
     "tile4": [("#define DGEN_HOURLY_TILE 1\n", "#define DGEN_HOURLY_TILE 4\n")],
+    # k_size / k_batt_finance without the net-billing (mo 2) code (register pressure of the NEM path)
+    "no_mo2": [("    return (t.P <= PREG) ? yl_bill_mo2_reg(t, src, s, with_gen) : yl_bill_mo2(t, src, s, with_gen, S);",
+                "    return 0.0;"),
+               ("        c.wo1 = yl_bill_mo2(t, c.src, 1.0, false, c.S);", "        c.wo1 = 0.0;"),
+               ("        wb = yl_bill_mo2(t, c.src, c.s_y, true, c.S);", "        wb = 0.0;")],
     "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
                  "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
 }
