@@ -1183,21 +1183,41 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
         for (int p = 0; p < P; p++) { S.at(p) = 0.0; S.at(half + p) = 0.0; }
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
-            for (int hod = 0; hod < 24; hod++, h++) {
-                double load = (double)src.shape[h] * src.load_scale;
-                double g = 0.0;
+#pragma unroll 1
+            for (int c0 = 0; c0 < 24; c0 += 4, h += 4) {
+                // the 4 hours' inputs loaded together (one latency, not four)
+                const float4 sv = *reinterpret_cast<const float4*>(src.shape + h);
+                const uint32_t pq = *reinterpret_cast<const uint32_t*>(sched + c0);
+                const float shv[4] = {sv.x, sv.y, sv.z, sv.w};
+                double g[4] = {0.0, 0.0, 0.0, 0.0}, tsv[4] = {0.0, 0.0, 0.0, 0.0};
                 if (with_gen) {
-                    if (src.sysgen) g = src.sysgen[(int64_t)h * src.sys_stride];
-                    else g = ((double)src.cf[h] / 1e6) * src.gen_scale;
+                    if (src.sysgen) {
+#pragma unroll
+                        for (int k = 0; k < 4; k++) g[k] = src.sysgen[(int64_t)(h + k) * src.sys_stride];
+                    } else {
+                        const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
+                        g[0] = ((double)cv.x / 1e6) * src.gen_scale;
+                        g[1] = ((double)cv.y / 1e6) * src.gen_scale;
+                        g[2] = ((double)cv.z / 1e6) * src.gen_scale;
+                        g[3] = ((double)cv.w / 1e6) * src.gen_scale;
+                    }
                 }
-                double dd = load - g * s;
-                int p = sched[hod];
-                if (dd > 0.0) {
-                    S.at(p) += dd;
-                } else {
-                    double e = -dd;
-                    if (src.ts) e *= (double)(float)(src.ts[h] * src.ts_mult);
-                    S.at(half + p) += e;
+                if (src.ts) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) tsv[k] = src.ts[h + k];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    double load = (double)shv[k] * src.load_scale;
+                    double dd = load - g[k] * s;
+                    int p = (int)((pq >> (8 * k)) & 0xffu);
+                    if (dd > 0.0) {
+                        S.at(p) += dd;
+                    } else {
+                        double e = -dd;
+                        if (src.ts) e *= (double)(float)(tsv[k] * src.ts_mult);
+                        S.at(half + p) += e;
+                    }
                 }
             }
         }
