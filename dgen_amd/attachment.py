@@ -175,18 +175,27 @@ def export_weights(engine, customers_in_bin, number_of_adopters, batt_kw_cum_las
 
 
 def state_hourly(engine, planes, weights, idx, seg_off):
-    """k_state_hourly: planes = (baseline, pvonly, with_batt) device tensors
-    [n_hours, n] (float32 or float64), weights from export_weights(), idx: plane
-    column of each group member (None: identity), seg_off [S+1].  Returns a
-    [S, n_hours] float64 device tensor in MW."""
+    """k_state_hourly: planes = (baseline, pvonly, with_batt) device tensors,
+    float32 in dgen_size_agents' hour-quad tiles [n_hours / 4, n, 4] (the sizing
+    outputs in place; engine.tile_hourly makes them from [n_hours, n]) or
+    float64 [n_hours, n]; weights from export_weights(), idx: plane column of
+    each group member (None: identity), seg_off [S+1].  Returns a [S, n_hours]
+    float64 device tensor in MW."""
     import torch
     eng = _engine(engine)
     L = _bind(eng.lib)
     base, pvo, wbt = planes
-    nh, n = base.shape
     if any(p.shape != base.shape or p.dtype != base.dtype for p in (pvo, wbt)):
         raise ValueError("state_hourly: the three planes must share shape and dtype")
-    if base.dtype not in (torch.float32, torch.float64):
+    if base.dtype == torch.float32:
+        if base.dim() != 3 or base.shape[2] != 4:
+            raise ValueError("state_hourly: float32 planes must be hour-quad tiles [n_hours/4, n, 4]")
+        nh, n = base.shape[0] * 4, base.shape[1]
+    elif base.dtype == torch.float64:
+        if base.dim() != 2:
+            raise ValueError("state_hourly: float64 planes must be [n_hours, n]")
+        nh, n = base.shape
+    else:
         raise TypeError("state_hourly: planes must be float32 or float64")
     if any(w.numel() != n for w in weights):
         raise ValueError("state_hourly: one weight per plane column")
@@ -296,7 +305,7 @@ def export_state_hourly_with_storage_mix(engine, schema, owner, year: int,
 def state_hourly_from_outputs(engine, out, perm, state_abbr, customers_in_bin, number_of_adopters,
                               batt_kw_cum_last_year, batt_kw, added):
     """Per-state hourly sums straight from dgen_size_agents' device hourly
-    planes (out["baseline"/"net_pvonly"/"net_with_batt"], [8760, n], device
+    planes (out["baseline"/"net_pvonly"/"net_with_batt"], tiled [2190, n, 4], device
     order `perm` = AgentBatch.perm or None).  Host columns are in caller order.
     Returns ([S, 8760] float64 device tensor in MW, state keys)."""
     import torch

@@ -46,9 +46,6 @@ constexpr int HB_DAY_BYTES = 12 * 1024;   // k_hourly_batt day buffer per wave (
 typedef __attribute__((address_space(3))) char* lds_ptr_t;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
-#ifndef DGEN_HOURLY_TILE
-#define DGEN_HOURLY_TILE 1
-#endif
 
 __constant__ int c_month_start_day[13] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334, 365};
 __constant__ int c_days_in_month[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
@@ -463,22 +460,17 @@ __device__ __forceinline__ int32_t opaque_i(int32_t x) {
     return x;
 }
 
-// Byte-addressed store into one hour row: `row` is wave-uniform (SGPRs), the
-// lane's 32-bit offset zero-extends (global_store ... v_off, s[base]).
-// The hourly output planes (105 KB per agent, read by nobody in the step) go
-// out non-temporal so they do not evict the profile-row slices the resident
-// waves share from L2 / MALL (1M agents: 33.2 -> 31.8 ms).
+// Store of one lane's hour quad into a tile row, in the scalar-base form
+// (global_store v_off, v_data, s[base]): the wave-uniform row base stays in
+// SGPRs, the lane's 32-bit offset zero-extends, no per-store 64-bit vector
+// address arithmetic.  The hourly output planes (105 KB per agent, read by
+// nobody in the step) go out non-temporal so they do not evict the
+// profile-row slices the resident waves share from L2 / MALL (1M agents:
+// 33.2 -> 31.8 ms).  The store is invisible to the compiler's vmcnt
+// bookkeeping, which only makes its waits stricter (vmcnt retires in order).
 __device__ __forceinline__ void st_f32x4(char* row, uint32_t off, const float (&q)[4]) {
     const f32x4 v = {q[0], q[1], q[2], q[3]};
     asm volatile("global_store_dwordx4 %0, %1, %2 nt" :: "v"(off), "v"(v), "s"(row) : "memory");
-}
-// Written as the scalar-base form (global_store v_off, v_data, s[base]): the
-// wave-uniform row base stays in SGPRs and the per-hour 64-bit vector address
-// adds the compiler otherwise emits (3 per hour) disappear.  The store is
-// invisible to the compiler's vmcnt bookkeeping, which only makes its waits
-// stricter (vmcnt retires in issue order).
-__device__ __forceinline__ void st_f32(char* row, uint32_t off, float v) {
-    asm volatile("global_store_dword %0, %1, %2 nt" :: "v"(off), "v"(v), "s"(row) : "memory");
 }
 __device__ __forceinline__ void st_f64(char* row, uint32_t off, double v) {
     *reinterpret_cast<double*>(row + off) = v;
@@ -638,24 +630,23 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     double soc = m_lo == 0 ? cfg.batt_init_soc : W.carry[i];
     double annual = m_lo == 0 ? 0.0 : W.carry[n + i];
     const int d_lo = c_month_start_day[m_lo];
-    // hour rows: wave-uniform bases advanced by one row per hour; per-lane
-    // 32-bit byte offsets (host guarantees n < 2^29, n_scratch < 2^28)
-    const uint32_t off4 = (uint32_t)i * 4u;
+    // hour rows: wave-uniform bases advanced per row; per-lane 32-bit byte
+    // offsets (host guarantees n < 2^28, n_scratch < 2^28)
     const uint32_t off8 = (uint32_t)(put_sys ? slot : 0) * 8u;
-    const size_t row4 = (size_t)n * 4u, row8 = (size_t)n_scratch * 8u;
+    const size_t row8 = (size_t)n_scratch * 8u;
     char* const ob = reinterpret_cast<char*>(O.baseline);
     char* const op = reinterpret_cast<char*>(O.net_pvonly);
     char* const ow = reinterpret_cast<char*>(O.net_with_batt);
     char* const osc = reinterpret_cast<char*>(W.scratch);
-    size_t ho4 = (size_t)d_lo * 24 * row4, ho8 = (size_t)d_lo * 24 * row8;
-#if DGEN_HOURLY_TILE == 4
-    // hour-quad tiles: (hour h, agent i) at ((h / 4) * n + i) * 4 + h % 4, so a
-    // lane writes 16 B and a wave 1 KB contiguous per plane every 4 hours
+    size_t ho8 = (size_t)d_lo * 24 * row8;
+    // hourly planes in hour-quad tiles (include/dgen_hip.h): (hour h, agent i)
+    // at ((h / 4) * n + i) * 4 + h % 4, so a lane stores 16 B and a wave 1 KB
+    // contiguous per plane every 4 hours (measured 29.3 -> 27.9 ms vs one
+    // 4-B store per lane-hour)
     const uint32_t off16 = (uint32_t)i * 16u;
     const size_t row16 = (size_t)n * 16u;
     size_t q16 = (size_t)d_lo * 6 * row16;
     float qb[4], qp[4], qw[4];
-#endif
 
     // Software pipeline over days through LDS: the next day's raw profile
     // values (96 B of the shape row + 96 B of the cf row per lane) are DMA'd
@@ -731,7 +722,6 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                                         in_per_bank, out_per_bank);
                 if constexpr (HOURLY) {
                     const double dn = ld - pl;
-#if DGEN_HOURLY_TILE == 4
                     qb[hh & 3] = (float)ld;
                     qp[hh & 3] = (float)fmax(dn, 0.0);
                     qw[hh & 3] = (float)st.g2l;
@@ -741,13 +731,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                         st_f32x4(ow + q16, off16, qw);
                         q16 += row16;
                     }
-#else
-                    st_f32(ob + ho4, off4, (float)ld);
-                    st_f32(op + ho4, off4, (float)fmax(dn, 0.0));
-                    st_f32(ow + ho4, off4, (float)st.g2l);
-#endif
                 }
-                ho4 += row4;
                 if (put_sys) {
                     st_f64(osc + ho8, off8, st.sys);         // plane [h][slot]
                 } else if (!mo2) {
@@ -1911,12 +1895,15 @@ __global__ void k_export_weights(const double* __restrict__ customers, const dou
     w_non[i] = 0.0 > nn ? 0.0 : nn;                                // Python max(nn, 0.0): NaN stays
 }
 
-// Per-state hourly net sums from the three f32 hourly planes ([h][n]):
+// Per-state hourly net sums from the three hourly planes:
 //   out[s * nh + h] = (sum_i pvo*w_pvo + wbt*w_batt + base*w_non) / 1000  (MW)
-// Members of state s are idx[seg_off[s] .. seg_off[s+1]) (idx null: the plane
-// columns themselves, states contiguous).  Block per (state, tile of SH_TILE
-// hours): the three weights of an agent are read once per tile instead of once
-// per hour, each plane row is a coalesced stream.  Fixed reduction order.
+// f32 planes are dgen_size_agents' outputs in place, in its hour-quad tiles
+// ((h, i) at ((h / 4) * n + i) * 4 + h % 4: one 16-B load per agent and 4
+// hours); f64 planes are plain [h][n].  Members of state s are
+// idx[seg_off[s] .. seg_off[s+1]) (idx null: the plane columns themselves,
+// states contiguous).  Block per (state, tile of SH_TILE hours): the three
+// weights of an agent are read once per tile instead of once per hour.  Fixed
+// reduction order.
 constexpr int SH_TILE = 16;
 template <typename V>
 __global__ void __launch_bounds__(256)
@@ -1937,12 +1924,28 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
     for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
         const int64_t c = idx ? idx[i] : i;
         const double a = w_pvo[c], b = w_batt[c], d = w_non[c];
-        const int64_t o = (int64_t)h0 * n + c;
+        if constexpr (sizeof(V) == 4) {
+            // nh % 4 == 0 (host), h0 % 4 == 0: whole quads
 #pragma unroll
-        for (int t = 0; t < SH_TILE; t++) {
-            if (t < nt) {
-                const int64_t r = o + (int64_t)t * n;
-                acc[t] += ((double)pvo[r] * a + (double)wbt[r] * b) + (double)base[r] * d;
+            for (int q = 0; q < SH_TILE / 4; q++) {
+                if (4 * q < nt) {
+                    const int64_t r = (((int64_t)(h0 >> 2) + q) * n + c) * 4;
+                    const f32x4 vp = *reinterpret_cast<const f32x4*>(pvo + r);
+                    const f32x4 vw = *reinterpret_cast<const f32x4*>(wbt + r);
+                    const f32x4 vb = *reinterpret_cast<const f32x4*>(base + r);
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        acc[4 * q + u] += ((double)vp[u] * a + (double)vw[u] * b) + (double)vb[u] * d;
+                }
+            }
+        } else {
+            const int64_t o = (int64_t)h0 * n + c;
+#pragma unroll
+            for (int t = 0; t < SH_TILE; t++) {
+                if (t < nt) {
+                    const int64_t r = o + (int64_t)t * n;
+                    acc[t] += ((double)pvo[r] * a + (double)wbt[r] * b) + (double)base[r] * d;
+                }
             }
         }
     }
@@ -2386,6 +2389,10 @@ int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
     if (!c || !baseline || !pvonly || !with_batt || !w_pvo || !w_batt || !w_non || !seg_off ||
         !out || n < 0 || n_hours <= 0 || n_seg < 0 || n_seg > 0x7fffffff) {
         set_err("dgen_state_hourly: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (planes_f32 && n_hours % 4 != 0) {
+        set_err("dgen_state_hourly: f32 (hour-quad tiled) planes need n_hours %% 4 == 0");
         return DGEN_E_ARG;
     }
     if (n_seg == 0) return DGEN_OK;

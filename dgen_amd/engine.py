@@ -220,7 +220,8 @@ class Engine:
         for name in _lib.OUTPUT_YEARLY:
             out[name] = torch.zeros((n, _lib.MAXY + 1), dtype=torch.float64, device=self.dev)
         for name in _lib.OUTPUT_HOURLY:
-            out[name] = (torch.empty((_lib.NH, n), dtype=torch.float32, device=self.dev)
+            # hour-quad tiles (include/dgen_hip.h): [NH / 4][n][4]
+            out[name] = (torch.empty((_lib.NH // 4, n, 4), dtype=torch.float32, device=self.dev)
                          if hourly else None)
         return out
 
@@ -304,6 +305,27 @@ class Engine:
         return xs.cpu().numpy(), xo.cpu().numpy(), nf.cpu().numpy()
 
 
+def hourly_plane(t):
+    """A hourly output plane in its device tiles [NH/4][n][4] -> the logical
+    time-major [NH][n] (a copy, on the same device)."""
+    q, n, four = t.shape
+    return t.permute(0, 2, 1).reshape(q * four, n)
+
+
+def hourly_agent_major(t):
+    """Tiled plane [NH/4][n][4] -> [n][NH] (a copy): each agent's 8760-h list."""
+    q, n, four = t.shape
+    return t.permute(1, 0, 2).reshape(n, q * four)
+
+
+def tile_hourly(p):
+    """Logical time-major [NH][n] plane -> the device tile layout [NH/4][n][4]."""
+    nh, n = p.shape
+    if nh % 4:
+        raise ValueError("hourly planes need a multiple of 4 hours")
+    return p.reshape(nh // 4, 4, n).permute(0, 2, 1).contiguous()
+
+
 def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
     """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly),
     in caller order when `perm` (AgentBatch.perm) is given."""
@@ -314,7 +336,7 @@ def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None) -
         res[name] = out[name].cpu().numpy()
     for name in _lib.OUTPUT_HOURLY:
         t = out.get(name)
-        res[name] = None if t is None else t.cpu().numpy().T.copy()
+        res[name] = None if t is None else hourly_agent_major(t).cpu().numpy()
     if perm is not None:
         for k, v in res.items():
             if v is not None:

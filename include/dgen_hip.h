@@ -24,8 +24,10 @@
  *   - Calls are stream-ordered on the given hipStream_t (NULL = default stream)
  *     and asynchronous unless stated otherwise.
  *   - Yearly array outputs are agent-major: value (agent, y) at
- *     [agent * (DGEN_MAXY + 1) + y]; hourly outputs are time-major:
- *     (hour, agent) at [hour * n + agent].
+ *     [agent * (DGEN_MAXY + 1) + y]; hourly outputs are time-major in
+ *     hour-quad tiles: (hour, agent) at [((hour / 4) * n + agent) * 4 + hour % 4]
+ *     (a [2190][n][4] array: each agent's 4 consecutive hours are 16 B, so a
+ *     wave writes 1 KB contiguous per plane every 4 hours).
  */
 #ifndef DGEN_HIP_H
 #define DGEN_HIP_H
@@ -186,9 +188,9 @@ typedef struct {
     double* cfev_batt;             /* [n][MAXY+1] cf_energy_value_pv_batt             */
     double* bill_w_batt;           /* [n][MAXY+1] utility_bill_w_sys_pv_batt          */
     double* bill_wo_batt;          /* [n][MAXY+1] utility_bill_wo_sys_pv_batt         */
-    float*  baseline;              /* [8760][n] baseline_net_hourly (may be NULL)     */
-    float*  net_pvonly;            /* [8760][n] adopter_net_hourly_pvonly             */
-    float*  net_with_batt;         /* [8760][n] adopter_net_hourly_with_batt          */
+    float*  baseline;              /* [2190][n][4] baseline_net_hourly (may be NULL)  */
+    float*  net_pvonly;            /* [2190][n][4] adopter_net_hourly_pvonly          */
+    float*  net_with_batt;         /* [2190][n][4] adopter_net_hourly_with_batt       */
 } dgen_outputs;
 
 typedef struct dgen_ctx dgen_ctx;
@@ -326,8 +328,9 @@ int32_t dgen_export_weights(dgen_ctx* ctx, const double* customers_in_bin,
                             double* w_batt, double* w_non, void* stream);
 
 /* Per-state hourly net sums in MW (:179-198) from the three hourly planes
- * ([n_hours][n]; float32 when planes_f32 != 0 -- dgen_size_agents' hourly
- * outputs in place -- else float64) and the per-column weights:
+ * (float32 when planes_f32 != 0: dgen_size_agents' hourly outputs in place,
+ * in their hour-quad tiles [n_hours / 4][n][4], n_hours % 4 == 0; else
+ * float64 [n_hours][n]) and the per-column weights:
  * out[s * n_hours + h].  Members of state s are the plane columns
  * idx[seg_off[s] .. seg_off[s+1]) (idx NULL: columns seg_off[s] ..
  * seg_off[s+1]).  Fixed summation order (deterministic); the reference's

@@ -66,6 +66,11 @@ VARIANTS = {
                 "    return 0.0;"),
                ("        c.wo1 = yl_bill_mo2(t, c.src, 1.0, false, c.S);", "        c.wo1 = 0.0;"),
                ("        wb = yl_bill_mo2(t, c.src, c.s_y, true, c.S);", "        wb = 0.0;")],
+    # NEM register bill with the month loop unrolled by 2 / fully
+    "bill_unroll2": [("    double total = 0.0;\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn",
+                      "    double total = 0.0;\n#pragma unroll 2\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn")],
+    "bill_unroll12": [("    double total = 0.0;\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn",
+                       "    double total = 0.0;\n#pragma unroll\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn")],
     "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
                  "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
 }

@@ -5,6 +5,7 @@ import pytest
 import torch
 
 from dgen_amd.dist import global_totals, group_order
+from dgen_amd.engine import hourly_plane
 
 pytestmark = pytest.mark.gpu
 
@@ -47,8 +48,8 @@ def test_state_hourly_net_sums_from_sizing(engine):
     n_adopt = np.linspace(0.0, 3.0, batch.n)
     n_non = 10.0 - n_adopt
     p = torch.as_tensor(perm, device=engine.dev)
-    adop = out["net_pvonly"].index_select(1, p)
-    base = out["baseline"].index_select(1, p)
+    adop = hourly_plane(out["net_pvonly"]).index_select(1, p)
+    base = hourly_plane(out["baseline"]).index_select(1, p)
     got = engine.segment_sums(adop, off, w1=n_adopt[perm], v2=base, w2=n_non[perm]).cpu().numpy()
     h = outputs_to_host(out)
     for s, st in enumerate(uniq):

@@ -12,6 +12,7 @@ import pytest
 import torch
 
 from dgen_amd import attachment as ga
+from dgen_amd.engine import tile_hourly
 from oracle import attach as oa
 from tests.helpers import golden_attach
 
@@ -148,7 +149,8 @@ def test_state_hourly_full_size(engine):
     planes = [torch.rand((nh, n), dtype=torch.float32, device=engine.dev) for _ in range(3)]
     wts = [torch.as_tensor(rng.integers(0, 20, n).astype(np.float64), device=engine.dev)
            for _ in range(2)] + [torch.as_tensor(rng.uniform(0, 100, n), device=engine.dev)]
-    got = ga.state_hourly(engine, planes, wts, None, so)
+    # f32 planes are read in the sizing outputs' hour-quad tiles
+    got = ga.state_hourly(engine, [tile_hourly(p) for p in planes], wts, None, so)
     P = [p.double() for p in planes]
     contrib = P[1] * wts[0] + P[2] * wts[1] + P[0] * wts[2]              # [nh, n]
     ref = torch.stack([contrib[:, so[s]:so[s + 1]].sum(dim=1) for s in range(S)]) / 1000.0

@@ -43,13 +43,13 @@ def test_status_and_bracket(full, engine):
 
 def test_hourly_energy_balance(full):
     pop, batch, out = full
-    base = out["baseline"].double().sum(0).cpu().numpy()
+    base = out["baseline"].double().sum((0, 2)).cpu().numpy()
     assert np.allclose(base, pop.cols["load_kwh"], rtol=2e-5)
     assert float(out["net_pvonly"].min()) >= 0.0
     assert float(out["net_with_batt"].min()) >= 0.0
     # the battery never raises imports above the PV-only imports
-    pv_imp = out["net_pvonly"].double().sum(0)
-    wb_imp = out["net_with_batt"].double().sum(0)
+    pv_imp = out["net_pvonly"].double().sum((0, 2))
+    wb_imp = out["net_with_batt"].double().sum((0, 2))
     assert bool((wb_imp <= pv_imp * (1 + 1e-6) + 1e-3).all())
 
 
