@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Benchmark of the device model-year loop (BASELINE config C5: national
+synthetic population, 2026-2050 diffusion loop with RCCL state totals).
+
+Per model year, on every rank's resident shard of WHOLE states: per-year
+inputs, dgen_size_agents (Brent PV sizing + PV+battery run), max market share,
+Bass diffusion, largest-remainder battery attachment, per-state 8760-h export
+(in place from the sizing planes, or by re-sizing chunks with --hourly-chunk
+for shards whose planes do not fit), per-state totals, and one all-reduce of
+the [51 x 5] totals + [51 x 8760] hourly rows (RCCL over xGMI for N > 1).
+
+Launch like bench.py (python bench_loop.py, or torch.distributed.run with one
+rank per GPU).  Weak scaling: --agents per GPU.  Prints ONE JSON line on rank 0:
+value = agents x model years / slowest rank's time for the timed years.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--agents", type=int, default=1_000_000, help="agents per GPU")
+    ap.add_argument("--first-year", type=int, default=2026)
+    ap.add_argument("--years", type=int, default=25, help="timed model years (2026-2050)")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed model years, then reset")
+    ap.add_argument("--hourly-chunk", type=int, default=None,
+                    help="re-size chunks of this many agents for the state export")
+    ap.add_argument("--no-export", action="store_true", help="skip the per-state hourly export")
+    args = ap.parse_args()
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if ws > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from dgen_amd.engine import Engine
+    from dgen_amd.synth import make_population
+    from dgen_amd.year_loop import LoopTables, YearLoop, loop_agents, rank_states
+
+    t_setup = time.perf_counter()
+    pop = make_population("national_mixed", args.agents, seed=20260000 + 5 + 7919 * rank,
+                          state_pool=rank_states(rank, ws))
+    eng = Engine(local if ws > 1 else 0)
+    eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    eng.set_tariffs(pop.tariffs)
+    eng.set_switches(pop.switches)
+    loop = YearLoop(eng, pop, loop_agents(pop, agent_id0=rank * args.agents), LoopTables.synthetic(),
+                    first_year=args.first_year, hourly_export=not args.no_export,
+                    hourly_chunk=args.hourly_chunk)
+    del pop
+    setup_s = time.perf_counter() - t_setup
+    for k in range(args.warmup):
+        loop.run_year(args.first_year + k)
+    loop.reset()
+    eng.kernel_times()
+    years = list(range(args.first_year, args.first_year + args.years))
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = [loop.run_year(y) for y in years]
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=eng.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms_size, ms_hourly, ms_fin, cnt = eng.kernel_times()
+    last = res[-1].totals.cpu().numpy()
+    if rank == 0:
+        line = {
+            "metric": "agent-years/sec (national diffusion loop: sizing + diffusion + attachment "
+                      "+ state export + RCCL totals)",
+            "value": args.agents * ws * len(years) / el, "unit": "agent-years/s", "n_gpus": ws,
+            "steps": len(years), "warmup": args.warmup, "ms_per_step": el / len(years) * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic national population (numpy PCG64; synthetic Bass / max-market-share "
+                    "/ attachment tables; no DB offline)",
+            "config": {"workload": "national_loop", "agents_per_gpu": args.agents,
+                       "global_agents": args.agents * ws, "years": [years[0], years[-1]],
+                       "state_export": not args.no_export, "hourly_chunk": args.hourly_chunk,
+                       "parallelism": f"dp{ws} (whole states per rank; one all-reduce per year)"},
+            "sizing_kernel_ms_per_call": {"k_size": ms_size, "k_hourly_batt": ms_hourly,
+                                          "k_batt_finance": ms_fin, "launch_samples": cnt},
+            "final_year": {"adopters": float(last[:, 3].sum()), "system_mw": float(last[:, 0].sum() / 1e3),
+                           "batt_mw": float(last[:, 1].sum() / 1e3), "agents": float(last[:, 4].sum())},
+            "setup_s": setup_s,
+        }
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -42,6 +42,7 @@ class Population:
     cols: Dict[str, np.ndarray]  # agent SoA columns
     n_scratch: int
     config: str
+    state_ix: Optional[np.ndarray] = None   # int16 index into STATES per agent
 
 
 def load_shapes(rng, n_rows: int, commercial: bool) -> np.ndarray:
@@ -141,7 +142,11 @@ STATES = ["AL", "AZ", "AR", "CA", "CO", "CT", "DE", "FL", "GA", "ID", "IL", "IN"
 
 def make_population(config: str, n_agents: int, seed: Optional[int] = None,
                     n_res_shapes: int = 4096, n_com_shapes: int = 2048, n_cf: int = 2048,
-                    n_counties: int = 3100, n_tariffs: int = 256) -> Population:
+                    n_counties: int = 3100, n_tariffs: int = 256,
+                    state_pool: Optional[np.ndarray] = None) -> Population:
+    """Synthetic population of `config`.  `state_pool` (indices into
+    STATES) restricts the agents' states, e.g. to the states one rank of the
+    model-year loop owns (year_loop.rank_states); CA agents take the NEM3 path."""
     if config not in CONFIGS:
         raise KeyError(f"unknown config {config!r}; one of {sorted(CONFIGS)}")
     cnum, sector, metering, _ = CONFIGS[config]
@@ -168,7 +173,11 @@ def make_population(config: str, n_agents: int, seed: Optional[int] = None,
     if metering == "ca":
         is_ca = np.ones(n, dtype=bool)
     elif sector == "mixed" or metering == "mixed":
-        is_ca = rng.integers(0, len(STATES), n) == STATES.index("CA")
+        pool = np.arange(len(STATES)) if state_pool is None else np.asarray(state_pool, np.int64)
+        if len(pool) == 0:
+            raise ValueError("empty state pool")
+        state_ix = pool[rng.integers(0, len(pool), n)]
+        is_ca = state_ix == STATES.index("CA")
     else:
         is_ca = np.zeros(n, dtype=bool)
 
@@ -227,5 +236,15 @@ def make_population(config: str, n_agents: int, seed: Optional[int] = None,
     cols["sw_storage_cnt"] = np.zeros(n, dtype=np.int32)
     tariffs = tt.array()
     n_scratch = assign_scratch(cols, tariffs, switches)
+    if not (sector == "mixed" or metering == "mixed"):
+        # states of the single-market configs from their own stream, so the
+        # population above is unchanged: CA for the CA stand-in, else non-CA
+        srng = np.random.default_rng((20260000 + cnum if seed is None else seed) + 1)
+        pool = np.asarray([i for i in range(len(STATES)) if STATES[i] != "CA"]
+                          if state_pool is None else state_pool, np.int64)
+        if metering == "ca":
+            pool = np.asarray([STATES.index("CA")])
+        state_ix = pool[srng.integers(0, len(pool), n)]
     return Population(shapes=shapes, cfs=cfs, wholesale=wholesale, tariffs=tariffs,
-                      switches=switches, cols=cols, n_scratch=n_scratch, config=config)
+                      switches=switches, cols=cols, n_scratch=n_scratch, config=config,
+                      state_ix=state_ix.astype(np.int16))

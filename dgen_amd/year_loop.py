@@ -1,0 +1,385 @@
+"""Device model-year loop (BASELINE config C5).
+
+The reference's year loop (`dgen_model.py:245-462`) restricted to the hot path
+and the steps that consume it, kept resident on the GPU from one model year to
+the next:
+
+    per-year inputs      elec.apply_* merges (elec.py:29-409) -> synthetic
+                         trajectories applied to the resident SoA columns
+                         (capex / battery capex learning, load growth, price
+                         multiplier); the agent frame is reset to its base
+                         columns every year, dgen_model.py:245-247
+    sizing               size_chunk -> dgen_size_agents (dgen_model.py:309-384)
+    max market share     calc_max_market_share (ff:1264-1310) -> k_max_market_share
+    diffusion            calc_diffusion_solar (diffusion_functions_elec.py:24-156)
+                         -> k_diffusion
+    battery attachment   _allocate_battery_adopters_integer
+                         (attachment_rate_functions.py:58-138) -> k_batt_attach
+                         over (state, sector) groups
+    state hourly export  export_state_hourly_with_storage_mix (:141-206)
+                         -> k_export_weights + k_state_hourly
+    state totals         last_year_installed_capacity groupby state
+                         (dgen_model.py:437-440) -> k_segment_sums, then ONE
+                         all-reduce per year (RCCL over xGMI on GPU tensors)
+    carry                market_last_year (diffusion_functions_elec.py:131-150,
+                         dgen_model.py:417-427): last year's market share,
+                         adopters, market value and cumulative PV / battery
+                         capacity stay on device as the next year's inputs
+
+Sharding: a rank owns WHOLE states (`rank_states`), so the (state, sector)
+groups of the largest-remainder attachment and the per-state hourly sums are
+rank-local, exactly as in the single-process reference; the only exchange is
+the per-state totals (and per-state hourly rows) all-reduce at the end of each
+year.  Nothing here runs on the CPU except index bookkeeping done once.
+
+Synthetic stand-ins (the DB tables are not available offline): Bass
+parameters per (state, sector), the max-market-share curves, storage
+attachment rates per state, customers per agent and the developable fraction
+(`LoopTables.synthetic`).  First model year: the reference seeds the market
+from observed state capacities (elec.py:701-765, DB); here the market starts
+empty (market share, adopters, value and capacities 0).
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import pandas as pd
+
+from . import _lib
+from .attachment import ATTACH_IN, ATTACH_OUT, AttachIn, AttachOut
+from .attachment import _bind as _bind_attach
+from .attachment import export_weights, state_hourly, string_ranks
+from .diffusion import DIFF_IN, DIFF_OUT, DiffIn, DiffOut, MmsTable, mms_table
+from .diffusion import _bind as _bind_diff
+from .dist import allreduce_sum
+from .synth import STATES
+
+SECTORS = ("res", "com")
+TOTAL_COLS = ["system_kw_cum", "batt_kw_cum", "batt_kwh_cum", "number_of_adopters", "n_agents"]
+# per-year synthetic trajectories relative to the first model year
+TRAJ = {"capex": -0.020, "capex_combined": -0.020, "batt_capex_kwh": -0.030,
+        "load_kwh": 0.010, "price_mult": 0.005}
+
+
+def rank_states(rank: int, world: int, n_states: int = len(STATES)) -> np.ndarray:
+    """States owned by `rank`: s % world == rank (every state on exactly one
+    rank; whole states keep the attachment groups and state sums local)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank / world")
+    return np.arange(rank, n_states, world, dtype=np.int64)
+
+
+def merge_state_rows(local_rows, local_states: Sequence[int], n_states: int):
+    """Scatter this rank's per-state rows [S_local, k] into the full [n_states, k]
+    table and all-reduce (SUM) it over the process group: states are disjoint
+    across ranks, so the sum is the gather (RCCL on GPU tensors, gloo on CPU)."""
+    import torch
+    full = torch.zeros((n_states,) + tuple(local_rows.shape[1:]), dtype=local_rows.dtype,
+                       device=local_rows.device)
+    if len(local_states):
+        idx = torch.as_tensor(np.asarray(local_states, np.int64), device=local_rows.device)
+        full.index_copy_(0, idx, local_rows)
+    return allreduce_sum(full)
+
+
+@dataclass
+class LoopTables:
+    """Per-(state, sector) Bass parameters, max-market-share curves (the
+    reference's max_market_share_df format), per-state storage attachment
+    rates; identical on every rank (fixed seed)."""
+    bass: pd.DataFrame
+    mms_df: pd.DataFrame
+    attach_rate: np.ndarray                  # [n_states]
+
+    @staticmethod
+    def synthetic(seed: int = 20260105) -> "LoopTables":
+        rng = np.random.default_rng(seed)
+        rows = []
+        for s in STATES:
+            for sec in SECTORS:
+                rows.append({"state_abbr": s, "sector_abbr": sec, "tech": "solar",
+                             "bass_param_p": float(rng.uniform(0.001, 0.01)),
+                             "bass_param_q": float(rng.uniform(0.2, 0.5)),
+                             "teq_yr1": float(rng.uniform(1.0, 11.0))})
+        bass = pd.DataFrame(rows)
+        pb = np.round(np.arange(0, 302) * 0.1, 1)
+        pb[-1] = 30.1
+        recs = []
+        for sec, (a, k) in (("res", (0.93, 0.16)), ("com", (0.85, 0.28))):
+            mms = a / (1.0 + np.exp(k * (pb - 8.0))) / (1.0 / (1.0 + np.exp(-k * 8.0)))
+            mms = np.minimum(mms, 1.0)
+            for p, v in zip(pb, mms):
+                recs.append({"payback_period": float(p), "sector_abbr": sec,
+                             "max_market_share": float(v), "metric": "payback_period",
+                             "source": "synthetic", "business_model": "host_owned"})
+        return LoopTables(bass=bass, mms_df=pd.DataFrame(recs),
+                          attach_rate=rng.uniform(0.05, 0.35, len(STATES)))
+
+
+def loop_agents(pop, agent_id0: int = 0, seed: int = 20260205) -> Dict[str, np.ndarray]:
+    """Per-agent columns of the diffusion / attachment steps for a synthetic
+    population (caller order): agent_id, state, sector, customers_in_bin,
+    developable_agent_weight (= customers x developable fraction,
+    elec.calculate_developable_customers_and_load)."""
+    n = len(pop.cols["load_kwh"])
+    rng = np.random.default_rng(seed + int(agent_id0))
+    is_res = (np.asarray(pop.cols["flags"]) & 1).astype(bool)
+    cust = np.where(is_res, rng.lognormal(np.log(400.0), 0.5, n), rng.lognormal(np.log(40.0), 0.5, n))
+    frac = rng.uniform(0.5, 0.9, n)
+    return {"agent_id": np.arange(agent_id0, agent_id0 + n, dtype=np.int64),
+            "state": np.asarray(pop.state_ix, dtype=np.int64),
+            "sector": np.where(is_res, 0, 1).astype(np.int64),
+            "customers_in_bin": cust, "developable_agent_weight": cust * frac}
+
+
+@dataclass
+class YearResult:
+    year: int
+    totals: object                              # [n_states, 5] float64, all-reduced
+    hourly: Optional[object]                    # [n_states, 8760] float64 MW, all-reduced
+    seconds: float
+    per_agent: Dict[str, object] = field(default_factory=dict)   # device order
+
+
+class YearLoop:
+    """Resident multi-year loop over one rank's shard (see module docstring).
+
+    engine: a loaded Engine (tables set); pop: synth.Population of this rank's
+    agents; agents: loop_agents(pop, ...); hourly_export: per-state 8760-h sums
+    each year; hourly_chunk: None sizes the shard once with hourly planes and
+    exports from them in place (105 KB / agent of HBM), an int re-sizes the
+    shard in chunks of that many agents with a reusable plane buffer for the
+    export (the 2.5M-agents-per-GPU national case)."""
+
+    def __init__(self, engine, pop, agents: Dict[str, np.ndarray], tables: LoopTables,
+                 first_year: int = 2026, hourly_export: bool = True,
+                 hourly_chunk: Optional[int] = None, order: Optional[np.ndarray] = None):
+        import torch
+        from .engine import profile_order
+        self.eng, self.tables = engine, tables
+        self.first_year = int(first_year)
+        self.hourly_export, self.hourly_chunk = bool(hourly_export), hourly_chunk
+        n = len(pop.cols["load_kwh"])
+        self.n = n
+        perm = profile_order(pop.cols) if order is None else np.asarray(order, np.int64)
+        self.perm = perm
+        inv = np.empty(n, np.int64)
+        inv[perm] = np.arange(n, dtype=np.int64)
+        self.batch = engine.upload_agents(pop.cols, n_scratch=pop.n_scratch, order=perm)
+        dev = engine.dev
+        f64 = lambda a: torch.as_tensor(np.asarray(a, np.float64)[perm], device=dev)
+        self.base = {k: self.batch.cols[k].clone() for k in TRAJ}
+        st, sec = agents["state"], agents["sector"]
+        self.state_caller = st
+        # per-agent Bass parameters (the reference's merge on (state, sector), :41-44)
+        b = tables.bass[tables.bass["tech"] == "solar"].set_index(["state_abbr", "sector_abbr"])
+        keys = [(STATES[s], SECTORS[c]) for s, c in zip(st, sec)]
+        uk = {k: i for i, k in enumerate(dict.fromkeys(keys))}
+        kix = np.array([uk[k] for k in keys], np.int64)
+        tab = b.reindex(list(uk.keys()))
+        self.bass = {c: f64(tab[src].to_numpy(np.float64)[kix]) for c, src in
+                     (("bass_p", "bass_param_p"), ("bass_q", "bass_param_q"), ("teq_yr1", "teq_yr1"))}
+        self.cust = f64(agents["customers_in_bin"])
+        self.dev_w = f64(agents["developable_agent_weight"])
+        # max market share table, curve row per agent (sector)
+        mt, rows, fmin, min_pb, max_pb = mms_table(tables.mms_df)
+        self.mms_tab = torch.as_tensor(mt, device=dev)
+        self.mms_tb = MmsTable(mms=self.mms_tab.data_ptr(), n_rows=mt.shape[0], n_factors=mt.shape[1],
+                               factor_min=fmin, pad=0, min_pb=min_pb, max_pb=max_pb)
+        self.mms_row = torch.as_tensor(np.array([rows.get(SECTORS[c], -1) for c in sec],
+                                                np.int32)[perm], device=dev)
+        # (state, sector) attachment groups in caller (reference row) order
+        g_keys = list(zip(st.tolist(), sec.tolist()))
+        g_first: Dict = {}
+        for i, k in enumerate(g_keys):
+            g_first.setdefault(k, []).append(i)
+        g_idx = np.concatenate([np.asarray(v, np.int64) for v in g_first.values()]) if n else \
+            np.zeros(0, np.int64)
+        g_off = np.concatenate([[0], np.cumsum([len(v) for v in g_first.values()])]).astype(np.int64)
+        self.g_dev = torch.as_tensor(inv[g_idx], device=dev)
+        self.g_off = torch.as_tensor(g_off, device=dev)
+        self.g_n = len(g_first)
+        self.g_rate = torch.as_tensor(np.array([tables.attach_rate[k[0]] for k in g_first],
+                                               np.float64), device=dev)
+        self.aid_rank = torch.as_tensor(string_ranks(agents["agent_id"])[g_idx], device=dev)
+        # state segments (first-appearance order, like the export's groupby)
+        s_first: Dict = {}
+        for i, s in enumerate(st.tolist()):
+            s_first.setdefault(s, []).append(i)
+        self.local_states = list(s_first.keys())
+        s_idx = np.concatenate([np.asarray(v, np.int64) for v in s_first.values()]) if n else \
+            np.zeros(0, np.int64)
+        self.s_off = np.concatenate([[0], np.cumsum([len(v) for v in s_first.values()])]).astype(np.int64)
+        self.s_dev_idx = inv[s_idx]                   # device column of each state member
+        self.s_dev = torch.as_tensor(self.s_dev_idx, device=dev)
+        self.state_dev_order = np.asarray(st, np.int64)[perm]   # state of each device row
+        # carry (market_last_year), device order
+        z = lambda: torch.zeros(n, dtype=torch.float64, device=dev)
+        self.carry = {k: z() for k in ("market_share_last_year", "adopters_cum_last_year",
+                                       "market_value_last_year", "system_kw_cum_last_year",
+                                       "batt_kw_cum_last_year", "batt_kwh_cum_last_year")}
+        whole = hourly_export and hourly_chunk is None
+        self.out = engine.alloc_outputs(n, hourly=whole)
+        self.c_out = engine.c_outputs(self.out)
+        self._chunk_out = None
+        if hourly_export and hourly_chunk is not None:
+            ch = min(int(hourly_chunk), max(n, 1))
+            self._chunk_out = engine.alloc_outputs(ch, hourly=False)
+            self._chunk_out = {k: v for k, v in self._chunk_out.items() if v is not None}
+            self._chunk_planes = {k: torch.empty(_lib.NH * ch, dtype=torch.float32, device=dev)
+                                  for k in _lib.OUTPUT_HOURLY}
+        self.Ld, self.La = _bind_diff(engine.lib), _bind_attach(engine.lib)
+
+    # --------------------------------------------------------------- steps
+    def apply_year_inputs(self, year: int):
+        """Base columns x synthetic trajectory (reset each year, dm:245-247)."""
+        k = year - self.first_year
+        for c, r in TRAJ.items():
+            self.batch.cols[c].copy_(self.base[c] * float((1.0 + r) ** k))
+
+    def _max_market_share(self):
+        import torch
+        eng, n = self.eng, self.n
+        b = torch.empty(n, dtype=torch.float64, device=eng.dev)
+        fct = torch.empty(n, dtype=torch.int64, device=eng.dev)
+        mms = torch.empty(n, dtype=torch.float64, device=eng.dev)
+        _lib.check(self.Ld.dgen_max_market_share(eng.ctx, ctypes.byref(self.mms_tb),
+                                                 self.out["payback_period"].data_ptr(),
+                                                 self.mms_row.data_ptr(), n, b.data_ptr(),
+                                                 fct.data_ptr(), mms.data_ptr(), eng.stream_handle()),
+                   "dgen_max_market_share")
+        return mms
+
+    def _diffusion(self, mms, first: bool):
+        import torch
+        eng, n, c = self.eng, self.n, self.carry
+        src = {"max_market_share": mms, "market_share_last_year": c["market_share_last_year"],
+               "bass_p": self.bass["bass_p"], "bass_q": self.bass["bass_q"],
+               "teq_yr1": self.bass["teq_yr1"], "developable_agent_weight": self.dev_w,
+               "system_kw": self.out["system_kw"], "system_capex_per_kw": self.batch.cols["capex"],
+               "adopters_cum_last_year": c["adopters_cum_last_year"],
+               "market_value_last_year": c["market_value_last_year"],
+               "system_kw_cum_last_year": c["system_kw_cum_last_year"]}
+        outs = {k: torch.empty(n, dtype=torch.float64, device=eng.dev) for k in DIFF_OUT}
+        din = DiffIn(**{k: src[k].data_ptr() for k in DIFF_IN})
+        dout = DiffOut(**{k: outs[k].data_ptr() for k in DIFF_OUT})
+        _lib.check(self.Ld.dgen_diffusion(eng.ctx, ctypes.byref(din), ctypes.byref(dout), n,
+                                          int(first), eng.stream_handle()), "dgen_diffusion")
+        return outs
+
+    def _attach(self, new_adopters):
+        import torch
+        eng, n, g = self.eng, self.n, self.g_dev
+        src = {"new_adopters": new_adopters.index_select(0, g), "aid_rank": self.aid_rank,
+               "batt_kw": self.out["batt_kw"].index_select(0, g),
+               "batt_kwh": self.out["batt_kwh"].index_select(0, g),
+               "batt_kw_cum_last_year": self.carry["batt_kw_cum_last_year"].index_select(0, g),
+               "batt_kwh_cum_last_year": self.carry["batt_kwh_cum_last_year"].index_select(0, g)}
+        grp = {k: torch.empty(n, dtype=torch.int64 if k == "added" else torch.float64,
+                              device=eng.dev) for k in ATTACH_OUT}
+        ci = AttachIn(**{k: src[k].data_ptr() for k in ATTACH_IN})
+        co = AttachOut(**{k: grp[k].data_ptr() for k in ATTACH_OUT})
+        if self.g_n:
+            _lib.check(self.La.dgen_batt_attach(eng.ctx, ctypes.byref(ci), ctypes.byref(co),
+                                                self.g_off.data_ptr(), self.g_rate.data_ptr(),
+                                                self.g_n, eng.stream_handle()), "dgen_batt_attach")
+        res = {}
+        for k, v in grp.items():                    # group order -> device order
+            d = torch.empty_like(v)
+            d.index_copy_(0, g, v)
+            res[k] = d
+        return res
+
+    def _state_hourly(self, w):
+        """[S_local, 8760] MW in local_states order."""
+        import torch
+        eng = self.eng
+        if self.hourly_chunk is None:
+            planes = (self.out["baseline"], self.out["net_pvonly"], self.out["net_with_batt"])
+            return state_hourly(eng, planes, w, self.s_dev_idx, self.s_off)
+        # chunked: re-size each chunk of device rows with hourly planes, sum
+        # its members per state (the planes depend only on the agent)
+        from .engine import AgentBatch
+        S = len(self.local_states)
+        pos = {s: j for j, s in enumerate(self.local_states)}
+        acc = torch.zeros((S, _lib.NH), dtype=torch.float64, device=eng.dev)
+        ch = int(self.hourly_chunk)
+        B = self.batch
+        for a in range(0, self.n, ch):
+            b = min(a + ch, self.n)
+            m = b - a
+            cols = {k: v[a:b] for k, v in B.cols.items()}
+            ca = _lib.Agents(**{name: cols[name].data_ptr() for name, _ in _lib.AGENT_COLUMNS})
+            ca.max_years = B.c_agents.max_years
+            sub = AgentBatch(n=m, n_scratch=B.n_scratch, cols=cols, workspace=B.workspace,
+                             c_agents=ca)
+            # prefixes of the chunk buffers: [m] scalars, [m][26] yearly, and the
+            # first 8760*m floats of each plane viewed as [2190][m][4] tiles
+            out = {k: v[:m] for k, v in self._chunk_out.items()}
+            out.update({k: v[:_lib.NH * m].view(_lib.NH // 4, m, 4)
+                        for k, v in self._chunk_planes.items()})
+            co = eng.c_outputs(out)
+            planes = (out["baseline"], out["net_pvonly"], out["net_with_batt"])
+            eng.size(sub, None, co)
+            st = self.state_dev_order[a:b]
+            order = np.argsort(np.array([pos[s] for s in st], np.int64), kind="stable")
+            cnt = np.bincount(np.array([pos[s] for s in st], np.int64), minlength=S)
+            off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+            wc = tuple(x[a:b] for x in w)
+            acc += state_hourly(eng, planes, wc, order, off)
+        return acc
+
+    def run_year(self, year: int, keep_per_agent: bool = False) -> YearResult:
+        import torch
+        eng = self.eng
+        first = year == self.first_year
+        torch.cuda.synchronize(eng.dev)
+        t0 = time.perf_counter()
+        self.apply_year_inputs(year)
+        eng.size(self.batch, self.out, self.c_out)
+        mms = self._max_market_share()
+        d = self._diffusion(mms, first)
+        att = self._attach(d["new_adopters"])
+        hourly_local = None
+        if self.hourly_export:
+            # the export reads the frame's last-year battery cumulative (:185)
+            w = export_weights(eng, self.cust, d["number_of_adopters"],
+                               self.carry["batt_kw_cum_last_year"], self.out["batt_kw"], att["added"])
+            hourly_local = self._state_hourly(w)
+        # per-state totals (dgen_model.py:437-440) on device, one all-reduce
+        sd = self.s_dev
+        cols = torch.stack([d["system_kw_cum"].index_select(0, sd), att["batt_kw_cum"].index_select(0, sd),
+                            att["batt_kwh_cum"].index_select(0, sd),
+                            d["number_of_adopters"].index_select(0, sd),
+                            torch.ones(self.n, dtype=torch.float64, device=eng.dev)])
+        loc = eng.segment_sums(cols, self.s_off)                     # [S_local, 5]
+        totals = merge_state_rows(loc, self.local_states, len(STATES))
+        hourly = (merge_state_rows(hourly_local, self.local_states, len(STATES))
+                  if hourly_local is not None else None)
+        per_agent = {}
+        if keep_per_agent:
+            per_agent = {"max_market_share": mms, **d, **att,
+                         **{k + "_in": v.clone() for k, v in self.carry.items()}}
+        # market_last_year carry (diffusion :131-150; batt cumulatives dm:417-427)
+        c = self.carry
+        c["market_share_last_year"].copy_(d["market_share"])
+        c["adopters_cum_last_year"].copy_(d["number_of_adopters"])
+        c["market_value_last_year"].copy_(d["market_value"])
+        c["system_kw_cum_last_year"].copy_(d["system_kw_cum"])
+        c["batt_kw_cum_last_year"].copy_(att["batt_kw_cum"])
+        c["batt_kwh_cum_last_year"].copy_(att["batt_kwh_cum"])
+        torch.cuda.synchronize(eng.dev)
+        return YearResult(year=year, totals=totals, hourly=hourly,
+                          seconds=time.perf_counter() - t0, per_agent=per_agent)
+
+    def reset(self):
+        """Back to an empty market (before the first model year)."""
+        for v in self.carry.values():
+            v.zero_()
+
+    def run(self, years: Sequence[int]) -> List[YearResult]:
+        return [self.run_year(int(y)) for y in years]

@@ -90,3 +90,74 @@ def test_totals_allreduce_gloo_world2():
 def test_allreduce_identity_without_pg():
     t = torch.ones(3)
     assert allreduce_sum(t) is t
+
+
+# ---------------------------------------------------------------------------
+# model-year loop sharding (dgen_amd.year_loop): whole states per rank, one
+# all-reduce of the per-state rows per year
+# ---------------------------------------------------------------------------
+def test_rank_states_partition():
+    from dgen_amd.synth import STATES
+    from dgen_amd.year_loop import rank_states
+    for world in (1, 2, 3, 8):
+        got = np.concatenate([rank_states(r, world) for r in range(world)])
+        assert sorted(got.tolist()) == list(range(len(STATES)))
+    with pytest.raises(ValueError):
+        rank_states(2, 2)
+
+
+def test_state_pool_population():
+    from dgen_amd.synth import STATES, make_population
+    from dgen_amd.year_loop import loop_agents, rank_states
+    pool = rank_states(1, 8)
+    pop = make_population("national_mixed", 500, seed=7, n_res_shapes=8, n_com_shapes=4, n_cf=4,
+                          n_counties=4, n_tariffs=8, state_pool=pool)
+    assert set(np.unique(pop.state_ix)) <= set(pool.tolist())
+    is_ca = (pop.cols["flags"] >> 1) & 1
+    assert np.array_equal(is_ca.astype(bool), pop.state_ix == STATES.index("CA"))
+    ag = loop_agents(pop, agent_id0=500)
+    assert ag["agent_id"][0] == 500 and len(np.unique(ag["agent_id"])) == 500
+    assert (ag["developable_agent_weight"] <= ag["customers_in_bin"]).all()
+    # the default (all states) stream is unchanged by the pool option
+    a = make_population("national_mixed", 300, seed=9, n_res_shapes=8, n_com_shapes=4, n_cf=4,
+                        n_counties=4, n_tariffs=8)
+    b = make_population("national_mixed", 300, seed=9, n_res_shapes=8, n_com_shapes=4, n_cf=4,
+                        n_counties=4, n_tariffs=8, state_pool=np.arange(len(STATES)))
+    assert all(np.array_equal(a.cols[k], b.cols[k]) for k in a.cols)
+
+
+def _loop_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dgen_amd.year_loop import merge_state_rows, rank_states
+    mine = rank_states(rank, world)
+    rows = torch.stack([torch.tensor([float(s), 10.0 * s + rank, 1.0], dtype=torch.float64)
+                        for s in mine])
+    full = merge_state_rows(rows, mine.tolist(), 51)
+    q.put((rank, full.numpy().tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_merge_state_rows_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loop_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    a, b = np.array(res[0]), np.array(res[1])
+    assert np.array_equal(a, b)                       # every rank holds the full table
+    for s in range(51):
+        assert a[s].tolist() == [float(s), 10.0 * s + (s % 2), 1.0]
+
+
+def test_merge_state_rows_single_process():
+    from dgen_amd.year_loop import merge_state_rows
+    t = merge_state_rows(torch.ones((2, 3), dtype=torch.float64), [4, 7], 10)
+    assert t.shape == (10, 3) and t[4].tolist() == [1.0] * 3 and t.sum().item() == 6.0
