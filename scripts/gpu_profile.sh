@@ -9,7 +9,7 @@ AGENTS=${AGENTS:-1000000}
 PMC_BENCH="bench.py --agents $AGENTS --steps 2 --warmup 1 --no-cpu"
 stop() { case "$1" in 0) return 0;; 124|134|137|139) echo "STOP: exit $1"; exit "$1";; *) echo "(non-fatal exit $1)"; return 0;; esac; }
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 500 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   echo "pytest gpu rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
   case $rc in 0|1) ;; *) echo STOP; exit $rc;; esac
 fi
