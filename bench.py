@@ -86,7 +86,8 @@ def cpu_baseline(pop, seconds: float, threads: int):
     chunk = max(64, 32 * threads)
     n_take = min(pop.cols["load_kwh"].size, 200_000)
     sub = {k: v[:n_take] for k, v in pop.cols.items()}
-    opop = oracle_population(sub, pop.tariffs, pop.switches, pop.shapes, pop.cfs, pop.wholesale)
+    opop = oracle_population(sub, pop.tariffs, pop.switches, pop.shapes, pop.cfs, pop.wholesale,
+                             demand=pop.demand)
     done, t0 = 0, time.perf_counter()
     while True:
         idx = list(range(done % n_take, min(done % n_take + chunk, n_take)))
@@ -108,17 +109,20 @@ def main():
     if ws > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from dgen_amd.config import EngineConfig
     from dgen_amd.engine import Engine, profile_order
     from dgen_amd.synth import make_population
 
     pop = make_population(args.config, args.agents, seed=20260000 + 3 + 7919 * rank)
-    eng = Engine(local if ws > 1 else 0)
+    # demand-charge configs run the extension mode; every other config the
+    # reference's switch (SKIP_DEMAND_CHARGES = True, ff:35)
+    eng = Engine(local if ws > 1 else 0, EngineConfig(skip_demand_charges=pop.skip_demand_charges))
     if args.chunks is not None:
         eng.set_pipeline(args.chunks)
     if args.hb_months is not None:
         eng.set_hourly_segment(args.hb_months)
     eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
-    eng.set_tariffs(pop.tariffs)
+    eng.set_tariffs(pop.tariffs, pop.demand)
     eng.set_switches(pop.switches)
     order = None if args.caller_order else profile_order(pop.cols, args.order_major)
     batch = eng.upload_agents(pop.cols, pop.n_scratch, order=order)
@@ -192,6 +196,7 @@ def main():
             "config": {"workload": args.config, "agents_per_gpu": args.agents,
                        "global_agents": args.agents * ws,
                        "hourly_outputs": not args.no_hourly,
+                       "demand_charges": not pop.skip_demand_charges,
                        "pipeline_chunks": eng.chunks, "hourly_months_per_launch": eng.hb_months,
                        "device_order": "caller" if args.caller_order else
                        ("profile (cf_row, load_row)" if args.order_major == "cf" else "profile (load_row, cf_row)"),

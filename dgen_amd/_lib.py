@@ -25,7 +25,8 @@ ST_UNIT = 0x08
 ST_YEARS = 0x10
 ST_SCRATCH = 0x20
 ST_ZERO_LOAD = 0x40
-ST_FATAL = ST_BOUNDS | ST_TARIFF | ST_YEARS | ST_SCRATCH | ST_UNIT
+ST_DEMAND = 0x80
+ST_FATAL = ST_BOUNDS | ST_TARIFF | ST_YEARS | ST_SCRATCH | ST_UNIT | ST_DEMAND
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -51,6 +52,7 @@ class Tables(ctypes.Structure):
         ("wholesale", _vp), ("tariffs", _vp), ("switches", _vp),
         ("n_shapes", _i64), ("n_cfs", _i64), ("n_wholesale", _i64), ("n_switches", _i64),
         ("n_tariffs", _i32), ("max_periods", _i32),
+        ("demand", _vp), ("n_demand", _i32), ("pad", _i32),
     ]
 
 
@@ -97,7 +99,7 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
-ABI_VERSION = 2   # include/dgen_hip.h DGEN_ABI_VERSION
+ABI_VERSION = 3   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
 

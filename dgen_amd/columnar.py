@@ -112,8 +112,10 @@ def empty_columns(n: int) -> Dict[str, np.ndarray]:
 class PopulationBuilder:
     """Accumulates agents into SoA columns + the tables they index."""
 
-    def __init__(self, switch_table=None):
-        self.tariffs = TariffTable()
+    def __init__(self, switch_table=None, skip_demand_charges: Optional[bool] = None):
+        """skip_demand_charges: None/True = the reference (ff:35); False =
+        extension mode (tariffs with demand charges get dgen_demand records)."""
+        self.tariffs = TariffTable(skip_demand_charges)
         self.switches = SwitchIndex(switch_table, self.tariffs)
         self.wholesale = WholesaleIndex()
         self.rows: List[Dict[str, Any]] = []
@@ -152,9 +154,10 @@ class PopulationBuilder:
 
 def assign_scratch(cols: Dict[str, np.ndarray], tariffs: np.ndarray, switches: np.ndarray) -> int:
     """Give an hourly scratch slot to every agent whose battery-case tariff can
-    be net billing (mo 2): its initial tariff or any rate-switch candidate."""
+    be net billing (mo 2) or carry demand charges (both bill hourly imports):
+    its initial tariff or any rate-switch candidate."""
     n = len(cols["load_kwh"])
-    mo2 = tariffs["mo"] == 2 if tariffs.size else np.zeros(0, bool)
+    mo2 = (tariffs["mo"] == 2) | (tariffs["dc"] > 0) if tariffs.size else np.zeros(0, bool)
     need = mo2[cols["tariff0"]] if n else np.zeros(0, bool)
     if switches.size:
         sw_mo2 = mo2[switches["tariff"]]

@@ -16,7 +16,8 @@ from . import _lib
 
 @dataclass
 class EngineConfig:
-    skip_demand_charges: int = 1        # financial_functions.py:35
+    skip_demand_charges: int = 1        # financial_functions.py:35 (0: extension mode,
+                                        # demand charges billed; parity unpinned)
     force_net_billing: int = 0          # financial_functions.py:38
     nm_yearend_sell_rate: float = 0.02  # $/kWh   Utilityrate5 ur_nm_yearend_sell_rate
     loan_rate_pct: float = 7.5          # %       Cashloan loan_rate (ff no longer sets it)

@@ -41,6 +41,8 @@ constexpr int MAXP = DGEN_MAXP;
 constexpr int MAXT = DGEN_MAXT;
 constexpr int MAXY = DGEN_MAXY;
 constexpr int NBIN = 12 * MAXP;
+constexpr int DCP = DGEN_DCP;
+constexpr int DCT = DGEN_DCT;
 constexpr int BLOCK = 128;   // threads per block for the per-agent kernels
 constexpr int HB_DAY_BYTES = 12 * 1024;   // k_hourly_batt day buffer per wave (LDS)
 typedef __attribute__((address_space(3))) char* lds_ptr_t;
@@ -230,6 +232,17 @@ __device__ __forceinline__ double depr_frac(int type, int year, int sl) {
 }
 
 // apply_rate_switch (elec.py:838-863): exactly one row with min <= size < max.
+// the tariff's demand-charge record when demand charges are billed (extension mode)
+__device__ __forceinline__ const dgen_demand* tariff_demand(const dgen_demand* table, int n_demand,
+                                                            bool dc_on, const dgen_tariff& t) {
+    const int dc = t.dc;
+    return (dc_on && dc > 0 && dc <= n_demand) ? table + (dc - 1) : nullptr;
+}
+__device__ __forceinline__ const dgen_demand* tariff_demand(const dgen_tables& T, const dgen_cfg& cfg,
+                                                            const dgen_tariff& t) {
+    return tariff_demand(T.demand, T.n_demand, cfg.skip_demand_charges == 0, t);
+}
+
 __device__ __forceinline__ double rate_switch(const dgen_switch* rows, int cnt, double size,
                                               int* new_tariff) {
     int hit = -1, k = 0;
@@ -618,9 +631,12 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const int P = t.P;
     const bool mo2 = (t.mo == 2);
     const int slot = A.scratch_slot[i];
-    const bool put_sys = mo2 && slot >= 0;
+    // the battery-case bill reads the hourly system output for net billing and
+    // for demand charges (both need hourly imports, not bins)
+    const bool need_sys = mo2 || tariff_demand(T, cfg, t) != nullptr;
+    const bool put_sys = need_sys && slot >= 0;
     int status = O.status[i] | t.flags;
-    if (mo2 && slot < 0) status |= DGEN_ST_SCRATCH;
+    if (need_sys && slot < 0) status |= DGEN_ST_SCRATCH;
 
     const double inv_eta_in = 1.0 / cfg.batt_eta_in;
     const double in_per_bank = bank > 0.0 ? cfg.batt_eta_in / bank : 0.0;
@@ -732,9 +748,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                         q16 += row16;
                     }
                 }
-                if (put_sys) {
-                    st_f64(osc + ho8, off8, st.sys);         // plane [h][slot]
-                } else if (!mo2) {
+                if (put_sys) st_f64(osc + ho8, off8, st.sys);   // plane [h][slot]
+                if (!mo2) {   // NEM energy bill from bins (demand charges also read the plane)
                     const int p = (int)((sched[hh >> 3] >> (8 * (hh & 7))) & 0xffu);
                     double2 b = bins[p * BLOCK];
                     b.x += ld;
@@ -1222,6 +1237,74 @@ __device__ __forceinline__ double yl_bill_net(const dgen_tariff& t, const YSrc& 
     return (t.P <= PREG) ? yl_bill_mo2_reg(t, src, s, with_gen) : yl_bill_mo2(t, src, s, with_gen, S);
 }
 
+// ---------------------------------------------------------------------------
+// Demand charges (extension mode; the reference keeps them off, ff:35):
+// monthly flat + TOU peaks of hourly grid import, tiered (oracle/orc.c
+// year_demand, same order: flat tiers, then periods 0..DCP-1).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double dc_tier_charge(double peak, const double* cap, const double* price,
+                                                 int nt) {
+    double charge = 0.0, prev = 0.0;
+    for (int k = 0; k < nt; k++) {
+        double hi = (k == nt - 1) ? INFINITY : cap[k];
+        double top = peak < hi ? peak : hi;
+        double amt = top - prev;
+        if (amt < 0.0) amt = 0.0;
+        if (hi > prev) prev = hi;
+        charge += amt * price[k];
+    }
+    return charge;
+}
+
+// One lane's year of demand charges (system output x s; no system when
+// !with_gen).  Peaks are maxima, so they are exact whatever the hour order;
+// only the imports' own rounding differs from the oracle.  The TOU peaks live
+// in the lane's LDS column (S.at(0 .. DCP-1); the host sizes it, see
+// dgen_size_agents): held in registers they pushed k_size into spills.
+__device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& src, double s,
+                                           bool with_gen, const YLds& S) {
+    double total = 0.0;
+    int h = 0;
+    for (int m = 0; m < 12; m++) {
+        double flat = 0.0;
+        for (int q = 0; q < DCP; q++) S.at(q) = 0.0;
+        for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
+            const uint8_t* sched = ((d % 7) >= 5) ? D->wkend[m] : D->wkday[m];
+#pragma unroll 1
+            for (int c0 = 0; c0 < 24; c0 += 4, h += 4) {
+                const float4 sv = *reinterpret_cast<const float4*>(src.shape + h);
+                const uint32_t pq = *reinterpret_cast<const uint32_t*>(sched + c0);
+                const float shv[4] = {sv.x, sv.y, sv.z, sv.w};
+                double g[4] = {0.0, 0.0, 0.0, 0.0};
+                if (with_gen) {
+                    if (src.sysgen) {
+#pragma unroll
+                        for (int k = 0; k < 4; k++) g[k] = src.sysgen[(int64_t)(h + k) * src.sys_stride];
+                    } else {
+                        const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
+                        g[0] = ((double)cv.x / 1e6) * src.gen_scale;
+                        g[1] = ((double)cv.y / 1e6) * src.gen_scale;
+                        g[2] = ((double)cv.z / 1e6) * src.gen_scale;
+                        g[3] = ((double)cv.w / 1e6) * src.gen_scale;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const double imp = (double)shv[k] * src.load_scale - g[k] * s;
+                    const int p = (int)((pq >> (8 * k)) & 0xffu);
+                    flat = imp > flat ? imp : flat;
+                    double& pk = S.at(p < DCP ? p : 0);
+                    pk = imp > pk ? imp : pk;
+                }
+            }
+        }
+        double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
+        for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
+        total += c;
+    }
+    return total;
+}
+
 // bins of a tariff from a row's slot sums, one (month, period) cell per lane
 template <int LPA>
 __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
@@ -1358,6 +1441,9 @@ struct YCtx {
     const dgen_tariff* tariffs;
     const dgen_tariff* tp;      // current tariff (global record or LDS copy)
     const dgen_switch* sw_rows;
+    const dgen_demand* dem_table;
+    const dgen_demand* dem;     // current tariff's demand charges (or nullptr)
+    int n_dem;
     int sw_cnt;
     int tariff, switched, status;
     double capex, ccm, kwh, yearend, load_scale;
@@ -1375,7 +1461,7 @@ struct YCtx {
     __device__ explicit YCtx(int lane) : g(lane) {}
 };
 
-template <int LPA>
+template <int LPA, bool DC>
 __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
     c.tp = stage_tariff(c.tariffs + tix, c.S, c.g);
     const dgen_tariff& t = *c.tp;
@@ -1388,12 +1474,16 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
     } else {
         c.wo1 = yl_bill_mo2(t, c.src, 1.0, false, c.S);
     }
+    if constexpr (DC) {
+        c.dem = tariff_demand(c.dem_table, c.n_dem, true, t);
+        if (c.dem) c.wo1 += yl_demand(c.dem, c.src, 1.0, false, c.S);
+    }
 }
 
 // calc_system_performance(kw, en_batt=False) with lanes = years; returns -NPV
 // (wave-uniform).  Every evaluation leaves its per-lane results in `c.last`:
 // after the search they are the outputs of the last evaluation (ff:449-474).
-template <int LPA>
+template <int LPA, bool DC>
 __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double otc = 0.0;
     if (kw > 0.0) {
@@ -1401,7 +1491,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
         otc = rate_switch(c.sw_rows, c.sw_cnt, kw, &nt);
         if (nt >= 0) {
             c.switched = 1;
-            if (nt != c.tariff) yl_set_tariff(c, nt);
+            if (nt != c.tariff) yl_set_tariff<LPA, DC>(c, nt);
         }
     }
     const dgen_tariff& t = *c.tp;
@@ -1413,6 +1503,12 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     } else {
         c.src.gen_scale = kws;
         wb = yl_bill_mo2(t, c.src, c.s_y, true, c.S);
+    }
+    if constexpr (DC) {
+        if (c.dem) {
+            c.src.gen_scale = kws;
+            wb += yl_demand(c.dem, c.src, c.s_y, true, c.S);
+        }
     }
     double w = wb * c.r_y;
     double wo = c.wo1 * c.r_y;
@@ -1428,7 +1524,9 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 
 // occupancy floor of 3 waves per SIMD (<= 168 VGPRs): the 32-lane variant
 // otherwise takes 181 and runs 2 (measured 23.3 -> 18.6 ms at 1M agents)
-template <int LPA>
+// DC: demand charges billed (extension mode) -- a separate instantiation so
+// the reference mode's register allocation is untouched
+template <int LPA, bool DC>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1) {
     const int lane = threadIdx.x;
@@ -1440,6 +1538,9 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.y = sl + 1;
     c.S = ylds_make(dyn_lds, half, c.g);
     c.tariffs = T.tariffs;
+    c.dem_table = T.demand;
+    c.n_dem = T.n_demand;
+    c.dem = nullptr;
     c.sw_rows = T.switches + A.sw_solar_off[i];
     c.sw_cnt = A.sw_solar_cnt[i];
     c.status = 0;
@@ -1493,12 +1594,12 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         }
         return;
     }
-    yl_set_tariff(c, t0);
+    yl_set_tariff<LPA, DC>(c, t0);
     int nfev = 0;
     double x_last = 0.0;
     double kw_star = brent_bounded(
         [&](double x) __attribute__((always_inline)) {
-            return yl_objective(c, x);
+            return yl_objective<LPA, DC>(c, x);
         },
         low, high, xatol, &nfev, &x_last);
     const YLast& l = c.last;
@@ -1535,7 +1636,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
 }
 
 // Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
-template <int LPA>
+template <int LPA, bool DC>
 __global__ void __launch_bounds__(WAVE)
 k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
                  int64_t n_scratch, int64_t i0, int64_t i1) {
@@ -1567,6 +1668,21 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     double total = ((system_costs + batt_costs) * A.ccm[i]) + 0.0 + otc;
     const double vor = A.vor[i];
     const bool mo2 = t.mo == 2;
+    const dgen_demand* dem = DC ? tariff_demand(T, cfg, t) : nullptr;
+    YSrc src;
+    {
+        const int lr = A.load_row[i];
+        src.shape = T.shapes + (int64_t)lr * NH;
+        src.cf = nullptr;
+        src.load_scale = A.load_kwh[i] / T.shape_sum[lr];
+        src.gen_scale = 0.0;
+        src.sys_stride = n_scratch;
+        const int slot = A.scratch_slot[i];
+        src.sysgen = (slot >= 0) ? W.scratch + slot : nullptr;
+        const int wr = A.wholesale_row[i];
+        src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+        src.ts_mult = A.price_mult[i];
+    }
     double wo1, wb;
     if (!mo2) {
         const double2* lg = W.LGb + (int64_t)i * NBIN;
@@ -1580,20 +1696,12 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         wo1 = same_tariff ? O.first_without[i] : yl_bill_nem(t, S, 0.0, cfg.nm_yearend_sell_rate);
         wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
     } else {
-        YSrc src;
-        const int lr = A.load_row[i];
-        src.shape = T.shapes + (int64_t)lr * NH;
-        src.cf = nullptr;
-        src.load_scale = A.load_kwh[i] / T.shape_sum[lr];
-        src.gen_scale = 0.0;
-        src.sys_stride = n_scratch;
-        const int slot = A.scratch_slot[i];
-        src.sysgen = (slot >= 0) ? W.scratch + slot : nullptr;
-        const int wr = A.wholesale_row[i];
-        src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
-        src.ts_mult = A.price_mult[i];
         wo1 = same_tariff ? O.first_without[i] : yl_bill_net(t, src, 1.0, false, S);
         wb = yl_bill_net(t, src, s_y, true, S);
+    }
+    if (DC && dem) {   // k_size's first_without already carries the no-system demand charge
+        if (!same_tariff) wo1 += yl_demand(dem, src, 1.0, false, S);
+        wb += yl_demand(dem, src, s_y, true, S);
     }
     double w = wb * r_y;
     double wo = wo1 * r_y;
@@ -2037,10 +2145,9 @@ int32_t dgen_last_error(char* buf, size_t n) {
 
 int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     if (!cfg || !out) { set_err("dgen_open: null argument"); return DGEN_E_ARG; }
-    if (cfg->skip_demand_charges != 1) {
-        set_err("dgen_open: demand charges are disabled in the reference (ff:35); "
-                "skip_demand_charges must be 1");
-        return DGEN_E_UNSUPPORTED;
+    if (cfg->skip_demand_charges != 0 && cfg->skip_demand_charges != 1) {
+        set_err("dgen_open: skip_demand_charges must be 1 (the reference, ff:35) or 0 (extension)");
+        return DGEN_E_ARG;
     }
     if (!(cfg->batt_v_nom > 0.0) || !(cfg->batt_q_full > 0.0) || !(cfg->batt_eta_in > 0.0) ||
         !(cfg->batt_eta_out > 0.0) || cfg->depr_sl_years < 1) {
@@ -2132,7 +2239,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     if (!c || !T || !A || !O) { set_err("dgen_size_agents: null argument"); return DGEN_E_ARG; }
     if (n <= 0) return DGEN_OK;
     if (!T->shapes || !T->shape_sum || !T->shape_slots || !T->cfs || !T->cf_naep || !T->cf_slots ||
-        !T->tariffs || T->n_tariffs <= 0) {
+        !T->tariffs || T->n_tariffs <= 0 || T->n_demand < 0 || (T->n_demand > 0 && !T->demand)) {
         set_err("dgen_size_agents: incomplete tables");
         return DGEN_E_ARG;
     }
@@ -2166,6 +2273,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 dgen_workspace_bytes(n, n_scratch));
         return DGEN_E_ARG;
     }
+    // the year-lane kernels keep the TOU demand peaks in the lane's LDS column
+    // (4 x half slots): with demand charges billed it must hold DGEN_DCP
+    dgen_tables Tk = *T;
+    const bool dc = c->cfg.skip_demand_charges == 0 && Tk.n_demand > 0;
+    if (dc && 4 * lds_half(Tk.max_periods) < DCP) Tk.max_periods = (DCP + 3) / 4;
+    T = &Tk;
     HIP_TRY(hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)stream;
     if (c->pending == dgen_ctx::RING) {   // fold the oldest record before reuse
@@ -2201,10 +2314,14 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         hipEvent_t* e = c->ev[slot][j];
         HIP_TRY(hipEventRecord(e[0], s));
         const dim3 ygrid((unsigned)((m + apb - 1) / apb));
-        if (lpa == 32)
-            hipLaunchKernelGGL(k_size_w<32>, ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+        if (lpa == 32 && !dc)
+            hipLaunchKernelGGL((k_size_w<32, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+        else if (lpa == 32)
+            hipLaunchKernelGGL((k_size_w<32, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+        else if (!dc)
+            hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
         else
-            hipLaunchKernelGGL(k_size_w<WAVE>, ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+            hipLaunchKernelGGL((k_size_w<WAVE, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
         HIP_TRY(hipEventRecord(e[2], s2));
@@ -2219,12 +2336,18 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                                    ws, n_scratch, i0, i1, m0, m1);
         }
         HIP_TRY(hipEventRecord(e[3], s2));
-        if (lpa == 32)
-            hipLaunchKernelGGL(k_batt_finance_w<32>, ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg, n,
-                               ws, n_scratch, i0, i1);
-        else
-            hipLaunchKernelGGL(k_batt_finance_w<WAVE>, ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
+        if (lpa == 32 && !dc)
+            hipLaunchKernelGGL((k_batt_finance_w<32, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
                                n, ws, n_scratch, i0, i1);
+        else if (lpa == 32)
+            hipLaunchKernelGGL((k_batt_finance_w<32, true>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
+                               n, ws, n_scratch, i0, i1);
+        else if (!dc)
+            hipLaunchKernelGGL((k_batt_finance_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O,
+                               c->cfg, n, ws, n_scratch, i0, i1);
+        else
+            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O,
+                               c->cfg, n, ws, n_scratch, i0, i1);
         HIP_TRY(hipEventRecord(e[4], s2));
     }
     HIP_TRY(hipEventRecord(c->join, s2));

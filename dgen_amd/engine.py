@@ -131,11 +131,24 @@ class Engine:
         T.n_shapes, T.n_cfs = R, C
         T.n_wholesale = 0 if ws is None else ws.shape[0]
 
-    def set_tariffs(self, records: np.ndarray):
-        from .tariff import TARIFF_DTYPE
+    def set_tariffs(self, records: np.ndarray, demand: Optional[np.ndarray] = None):
+        """Upload compiled tariff records (+ the demand-charge records their
+        ``dc`` field indexes, TariffTable.demand_array(); billed only when the
+        engine's cfg.skip_demand_charges is 0)."""
+        from .tariff import DEMAND_DTYPE, TARIFF_DTYPE
         recs = np.ascontiguousarray(records, dtype=TARIFF_DTYPE)
         if recs.size == 0:
             raise ValueError("empty tariff table")
+        dem = np.zeros(0, DEMAND_DTYPE) if demand is None else np.ascontiguousarray(demand, DEMAND_DTYPE)
+        if int(recs["dc"].max()) > dem.size or int(recs["dc"].min()) < 0:
+            raise ValueError("tariff dc index outside the demand table")
+        self.tables.n_demand = int(dem.size)
+        self.tables.demand = None
+        self._keep.pop("demand", None)
+        if dem.size:
+            d = self._to_dev(np.frombuffer(dem.tobytes(), dtype=np.uint8), _torch().uint8)
+            self._keep["demand"] = d
+            self.tables.demand = _ptr(d)
         raw = np.frombuffer(recs.tobytes(), dtype=np.uint8)
         t = self._to_dev(raw, _torch().uint8)
         self._keep["tariffs"] = t

@@ -125,6 +125,9 @@ def _raise_for_status(status: np.ndarray, agent_ids) -> None:
                              "(the reference would price it with stale PySAM state)")
     if s & _lib.ST_UNIT:
         raise _lib.DgenError(f"agent {who}: tariff usage unit kWh/kW is not supported")
+    if s & _lib.ST_DEMAND:
+        raise _lib.DgenError(f"agent {who}: demand-charge matrix outside SSC's limits "
+                             "(0-based month, 1-based period <= 8, contiguous tiers <= 4)")
     raise _lib.DgenError(f"agent {who}: sizing failed with status 0x{s:x}")
 
 

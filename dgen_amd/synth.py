@@ -28,6 +28,9 @@ CONFIGS = {
     "ca_res_storage": (2, "res", "ca", "CA-like residential PV+storage stand-in (200k)"),
     "res_1m_nem_tou": (3, "res", "nem", "synthetic 1M residential, NEM TOU tariffs"),
     "com_8m": (4, "com", "nem", "synthetic commercial with battery"),
+    # C4 extension mode: the reference keeps demand charges off (ff:35); here
+    # they are compiled and billed (parity unpinned)
+    "com_dc_batt": (4, "com", "nem_dc", "synthetic commercial, demand charges billed, with battery"),
     "national_mixed": (5, "mixed", "mixed", "national mixed population"),
 }
 
@@ -43,6 +46,12 @@ class Population:
     n_scratch: int
     config: str
     state_ix: Optional[np.ndarray] = None   # int16 index into STATES per agent
+    demand: Optional[np.ndarray] = None     # DEMAND_DTYPE (demand-charge configs)
+
+    @property
+    def skip_demand_charges(self) -> int:
+        """EngineConfig.skip_demand_charges the population is meant for."""
+        return 0 if self.demand is not None and self.demand.size else 1
 
 
 def load_shapes(rng, n_rows: int, commercial: bool) -> np.ndarray:
@@ -114,7 +123,7 @@ def random_tariffs(rng, n: int, metering: str):
         for p in range(1, P):
             wk[:, (on0 + 2 * p) % 24:(on0 + 2 * p + 3) % 24 or 24] = p
         we = np.zeros((12, 24), dtype=int)
-        mo = 0 if metering == "nem" else (2 if metering == "nb" else int(rng.random() < 0.2) * 2)
+        mo = 0 if metering in ("nem", "nem_dc") else (2 if metering == "nb" else int(rng.random() < 0.2) * 2)
         lv = None
         if T > 1:
             lv = np.sort(rng.choice([250.0, 400.0, 600.0, 900.0], size=(T, P)), axis=0)
@@ -130,6 +139,20 @@ def random_tariffs(rng, n: int, metering: str):
             d = {"ur_ec_tou_mat": rows, "ur_ec_sched_weekday": (wk + 1).tolist(),
                  "ur_ec_sched_weekend": (we + 1).tolist(), "ur_monthly_fixed_charge": fixed,
                  "ur_metering_option": mo}
+        if metering == "nem_dc":
+            # monthly flat demand charge (1-2 tiers, $/kW) on every tariff, a
+            # 2-period TOU demand charge (afternoon peak) on half of them
+            nt = int(rng.integers(1, 3))
+            fp = np.round(rng.uniform(4.0, 16.0, nt), 2)
+            caps = [float(rng.choice([50.0, 100.0, 250.0]))] if nt == 2 else []
+            d["ur_dc_flat_mat"] = [[m, t + 1, (caps + [1e38])[t], float(fp[t])]
+                                   for m in range(12) for t in range(nt)]
+            if rng.random() < 0.5:
+                on = int(rng.integers(11, 15))
+                d["ur_dc_tou_mat"] = [[1, 1, 1e38, float(np.round(rng.uniform(0.0, 3.0), 2))],
+                                      [2, 1, 1e38, float(np.round(rng.uniform(5.0, 18.0), 2))]]
+                d["ur_dc_sched_weekday"] = [[2 if on <= h < on + 6 else 1 for h in range(24)]] * 12
+                d["ur_dc_sched_weekend"] = [[1] * 24 for _ in range(12)]
         out.append(d)
     return out
 
@@ -159,7 +182,7 @@ def make_population(config: str, n_agents: int, seed: Optional[int] = None,
     cfs = solar_cfs(rng, n_cf)
     wholesale = wholesale_rows(rng, n_counties)
 
-    tt = TariffTable()
+    tt = TariffTable(skip_demand_charges=False if metering == "nem_dc" else None)
     raw = random_tariffs(rng, n_tariffs, "nem" if metering in ("nem", "ca") else metering)
     base_idx = np.array([tt.add(d, False) for d in raw], dtype=np.int32)
     ca_idx = np.array([tt.add(d, True) for d in raw], dtype=np.int32)
@@ -247,4 +270,5 @@ def make_population(config: str, n_agents: int, seed: Optional[int] = None,
         state_ix = pool[srng.integers(0, len(pool), n)]
     return Population(shapes=shapes, cfs=cfs, wholesale=wholesale, tariffs=tariffs,
                       switches=switches, cols=cols, n_scratch=n_scratch, config=config,
-                      state_ix=state_ix.astype(np.int16))
+                      state_ix=state_ix.astype(np.int16),
+                      demand=tt.demand_array() if metering == "nem_dc" else None)

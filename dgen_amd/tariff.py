@@ -18,6 +18,14 @@ once per distinct (tariff, CA?) pair and the result is packed into the
 pinned by tests/golden/tariffs.json (bit-exact, float32 rounding included):
 period ids remapped in the matrix but not in the schedules (ids > P clamp to 1),
 one cap per tier (the smallest finite one), unit code = the mode, BIG = 1e38.
+
+Demand charges (extension mode).  The reference compiles the ``ur_dc_*`` mats
+but never passes them (SKIP_DEMAND_CHARGES = True, ff:35,601-603).  With
+``skip_demand_charges=False`` the compiler takes process_tariff's other branch
+(ff:604-615; its field output is pinned by tests/golden/tariffs_dc.json,
+captured from the reference with the switch flipped) and packs the mats into a
+``dgen_demand`` record (include/dgen_hip.h) that the kernels bill.  The SSC
+demand arithmetic itself is parity unpinned.
 """
 from __future__ import annotations
 
@@ -313,9 +321,11 @@ def normalize_tariff(raw, net_sell_rate_scalar=0.0, debug=False) -> Dict[str, An
 
 
 def rate_fields(td: Dict[str, Any], net_billing_sell_rate=0.0, ts_sell_rate=None,
-                ts_buy_rate=None) -> Dict[str, Any]:
+                ts_buy_rate=None, skip_demand_charges: Optional[bool] = None) -> Dict[str, Any]:
     """The ElectricityRates fields process_tariff (ff:575-648) writes, as a dict
-    in write order."""
+    in write order.  ``skip_demand_charges`` None = the reference's module
+    switch (ff:35)."""
+    skip_dc = SKIP_DEMAND_CHARGES if skip_demand_charges is None else bool(skip_demand_charges)
     f: Dict[str, Any] = {}
     mo_in = int(td.get("ur_metering_option", 0))
     mo = 2 if FORCE_NET_BILLING else mo_in
@@ -325,10 +335,10 @@ def rate_fields(td: Dict[str, Any], net_billing_sell_rate=0.0, ts_sell_rate=None
     f["ur_monthly_min_charge"] = 0.0
     flat_raw, tou_raw = td.get("ur_dc_flat_mat"), td.get("ur_dc_tou_mat")
     dc_on = bool(td.get("ur_dc_enable", 0)) or bool(flat_raw) or bool(tou_raw)
-    if SKIP_DEMAND_CHARGES or not dc_on:
+    if skip_dc or not dc_on:
         f["ur_dc_enable"] = 0
         f["ur_enable_billing_demand"] = 0
-    else:  # pragma: no cover - unreachable with the reference's switches
+    else:   # ff:604-615 (extension mode)
         flat, tou = small_f32_matrix(flat_raw), small_f32_matrix(tou_raw)
         enable = bool(flat) or bool(tou)
         f["ur_dc_sched_weekday"] = fit_12x24(td.get("ur_dc_sched_weekday"))
@@ -364,11 +374,12 @@ def rate_fields(td: Dict[str, Any], net_billing_sell_rate=0.0, ts_sell_rate=None
 
 
 def process_tariff(utilityrate, tariff_dict, net_billing_sell_rate, ts_sell_rate=None,
-                   ts_buy_rate=None):
+                   ts_buy_rate=None, skip_demand_charges: Optional[bool] = None):
     """Drop-in for financial_functions.process_tariff: writes the fields onto
     ``utilityrate.ElectricityRates`` (any attribute bag) and returns it."""
     er = utilityrate.ElectricityRates
-    for k, v in rate_fields(tariff_dict, net_billing_sell_rate, ts_sell_rate, ts_buy_rate).items():
+    for k, v in rate_fields(tariff_dict, net_billing_sell_rate, ts_sell_rate, ts_buy_rate,
+                            skip_demand_charges).items():
         setattr(er, k, v)
     return utilityrate
 
@@ -390,12 +401,24 @@ def apply_ca_nem3(td: Dict[str, Any]) -> Dict[str, Any]:
 TARIFF_DTYPE = np.dtype([
     ("P", "<i4"), ("T", "<i4"), ("mo", "<i4"), ("unit", "<i4"), ("fixed", "<f8"),
     ("cap", "<f8", (MAXT,)), ("buy", "<f8", (MAXP, MAXT)), ("sell", "<f8", (MAXP, MAXT)),
-    ("wkday", "u1", (12, 24)), ("wkend", "u1", (12, 24)), ("flags", "<i4"), ("pad", "<i4"),
+    ("wkday", "u1", (12, 24)), ("wkend", "u1", (12, 24)), ("flags", "<i4"), ("dc", "<i4"),
 ])
 assert TARIFF_DTYPE.itemsize == 1808
 
+# dgen_demand (include/dgen_hip.h): demand-charge mats of one tariff
+DCP = 8     # TOU demand periods
+DCT = 4     # demand tiers
+DEMAND_DTYPE = np.dtype([
+    ("tou_nt", "<i4", (DCP,)), ("flat_nt", "<i4", (12,)), ("flags", "<i4"), ("pad", "<i4"),
+    ("tou_cap", "<f8", (DCP, DCT)), ("tou_price", "<f8", (DCP, DCT)),
+    ("flat_cap", "<f8", (12, DCT)), ("flat_price", "<f8", (12, DCT)),
+    ("wkday", "u1", (12, 24)), ("wkend", "u1", (12, 24)),
+])
+assert DEMAND_DTYPE.itemsize == 1944
+
 ST_EMPTY_EC = 0x04
 ST_UNIT = 0x08
+ST_DEMAND = 0x80
 
 
 class TariffError(ValueError):
@@ -406,6 +429,7 @@ class TariffError(ValueError):
 class CompiledTariff:
     fields: Dict[str, Any]          # ElectricityRates fields (ts variant: no TS series)
     record: np.ndarray              # one TARIFF_DTYPE element
+    demand: Optional[np.ndarray] = None   # one DEMAND_DTYPE element (demand charges on)
 
 
 def pack_record(fields: Dict[str, Any]) -> np.ndarray:
@@ -451,13 +475,69 @@ def pack_record(fields: Dict[str, Any]) -> np.ndarray:
     return rec
 
 
-def compile_tariff(raw, is_ca: bool) -> CompiledTariff:
-    """normalize_tariff -> CA NEM3 -> process_tariff -> device record."""
+def _dc_tiers(rows: np.ndarray, n_groups: int, cap: np.ndarray, price: np.ndarray,
+              nt: np.ndarray, group_base: int) -> int:
+    """Rows [group, tier, max kW, $/kW] -> per-group tier arrays.  SSC reads the
+    group column as a 0-based month (flat mat) or a 1-based period (TOU mat) and
+    tiers 1..k; the last tier of a group is unbounded above.  Returns
+    ST_DEMAND when a row falls outside the record's limits."""
+    flags = 0
+    seen: Dict[int, Dict[int, Tuple[float, float]]] = {}
+    for r in rows:
+        if r.shape[0] < 4:
+            return ST_DEMAND
+        g, t = int(r[0]) - group_base, int(r[1]) - 1
+        if not (0 <= g < n_groups) or not (0 <= t < DCT):
+            flags |= ST_DEMAND
+            continue
+        seen.setdefault(g, {})[t] = (float(r[2]), float(r[3]))
+    for g, tiers in seen.items():
+        k = max(tiers) + 1
+        if sorted(tiers) != list(range(k)):
+            flags |= ST_DEMAND          # a gap in the tier numbers
+            continue
+        nt[g] = k
+        for t, (c, pr) in tiers.items():
+            cap[g, t] = c
+            price[g, t] = pr
+    return flags
+
+
+def pack_demand(fields: Dict[str, Any]) -> Optional[np.ndarray]:
+    """ElectricityRates demand fields (ff:604-615) -> dgen_demand record, or
+    None when demand charges are off for the tariff."""
+    if not int(fields.get("ur_dc_enable", 0)):
+        return None
+    rec = np.zeros((), dtype=DEMAND_DTYPE)
+    flags = 0
+    flat = np.asarray(fields.get("ur_dc_flat_mat") or [], dtype=np.float64)
+    tou = np.asarray(fields.get("ur_dc_tou_mat") or [], dtype=np.float64)
+    if flat.size:
+        flags |= _dc_tiers(flat.reshape(flat.shape[0], -1), 12, rec["flat_cap"], rec["flat_price"],
+                           rec["flat_nt"], 0)
+    if tou.size:
+        flags |= _dc_tiers(tou.reshape(tou.shape[0], -1), DCP, rec["tou_cap"], rec["tou_price"],
+                           rec["tou_nt"], 1)
+    for name, key in (("wkday", "ur_dc_sched_weekday"), ("wkend", "ur_dc_sched_weekend")):
+        s = np.asarray(fit_12x24(fields.get(key)), dtype=np.int64).reshape(12, 24)
+        if tou.size and ((s < 1) | (s > DCP)).any():
+            flags |= ST_DEMAND          # SSC rejects a schedule period outside 1..n
+        rec[name] = (np.clip(s, 1, DCP) - 1).astype(np.uint8)
+    rec["flags"] = flags
+    return rec
+
+
+def compile_tariff(raw, is_ca: bool, skip_demand_charges: Optional[bool] = None) -> CompiledTariff:
+    """normalize_tariff -> CA NEM3 -> process_tariff -> device record(s)."""
     td = normalize_tariff(raw, net_sell_rate_scalar=0.0)
     if is_ca:
         td = apply_ca_nem3(td)
-    fields = rate_fields(td, 0.0, ts_sell_rate=None)
-    return CompiledTariff(fields=fields, record=pack_record(fields))
+    fields = rate_fields(td, 0.0, ts_sell_rate=None, skip_demand_charges=skip_demand_charges)
+    rec = pack_record(fields)
+    dem = pack_demand(fields)
+    if dem is not None:
+        rec["flags"] = int(rec["flags"]) | int(dem["flags"])
+    return CompiledTariff(fields=fields, record=rec, demand=dem)
 
 
 def tariff_key(raw) -> str:
@@ -470,12 +550,16 @@ def tariff_key(raw) -> str:
 
 
 class TariffTable:
-    """Deduplicating table of compiled tariffs (one entry per (tariff, CA?))."""
+    """Deduplicating table of compiled tariffs (one entry per (tariff, CA?)).
+    With demand charges on, tariffs that carry them get a ``dgen_demand``
+    record; the tariff record's ``dc`` field is 1 + its index (0 = none)."""
 
-    def __init__(self):
+    def __init__(self, skip_demand_charges: Optional[bool] = None):
         self._index: Dict[Tuple[str, bool], int] = {}
         self.records: List[np.ndarray] = []
+        self.demand: List[np.ndarray] = []
         self.raw: List[Any] = []
+        self.skip_demand_charges = skip_demand_charges
 
     def add(self, raw, is_ca: bool, key: Optional[str] = None) -> int:
         """Index of the compiled (raw, is_ca) tariff; `key` overrides the
@@ -484,7 +568,10 @@ class TariffTable:
         hit = self._index.get(key)
         if hit is not None:
             return hit
-        ct = compile_tariff(raw, bool(is_ca))
+        ct = compile_tariff(raw, bool(is_ca), self.skip_demand_charges)
+        if ct.demand is not None:
+            self.demand.append(ct.demand)
+            ct.record["dc"] = len(self.demand)
         idx = len(self.records)
         self._index[key] = idx
         self.records.append(ct.record)
@@ -498,3 +585,8 @@ class TariffTable:
         if not self.records:
             return np.zeros(0, dtype=TARIFF_DTYPE)
         return np.stack(self.records).astype(TARIFF_DTYPE)
+
+    def demand_array(self) -> np.ndarray:
+        if not self.demand:
+            return np.zeros(0, dtype=DEMAND_DTYPE)
+        return np.stack(self.demand).astype(DEMAND_DTYPE)

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 2
+#define DGEN_ABI_VERSION 3
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_NH    8760   /* hours per year                                    */
@@ -47,6 +47,8 @@ extern "C" {
 #define DGEN_MAXP  12     /* TOU periods                                        */
 #define DGEN_MAXT  6      /* tiers                                              */
 #define DGEN_MAXY  50     /* analysis years                                     */
+#define DGEN_DCP   8      /* demand-charge TOU periods (extension mode)         */
+#define DGEN_DCT   4      /* demand-charge tiers (extension mode)               */
 
 /* error codes */
 #define DGEN_OK            0
@@ -62,12 +64,16 @@ extern "C" {
 #define DGEN_ST_YEARS        0x10  /* analysis period outside 1..DGEN_MAXY            */
 #define DGEN_ST_SCRATCH      0x20  /* mo=2 battery run without a scratch slot         */
 #define DGEN_ST_ZERO_LOAD    0x40  /* load_kwh == 0: reference divides by zero (ff:549)*/
+#define DGEN_ST_DEMAND       0x80  /* demand-charge mat outside SSC's / the record's   */
+                                   /* limits (month, period, tier numbering)          */
 
 /* Engine configuration: the PySAM config defaults the reference never sets
  * (CustomGenerationBattery{Residential,Commercial}, ff:59-80) plus the
  * reference's module switches (ff:35,38).                                     */
 typedef struct {
-    int32_t skip_demand_charges;   /* must be 1 (ff:35 SKIP_DEMAND_CHARGES=True)   */
+    int32_t skip_demand_charges;   /* 1 = the reference (ff:35 SKIP_DEMAND_CHARGES  */
+                                   /* = True): tariffs' demand records are ignored; */
+                                   /* 0 = extension mode: they are billed           */
     int32_t force_net_billing;     /* ff:38; applied by the host tariff compiler    */
     double  nm_yearend_sell_rate;  /* $/kWh, Utilityrate5 ur_nm_yearend_sell_rate  */
     double  loan_rate_pct;         /* Cashloan loan_rate (%)                        */
@@ -97,9 +103,30 @@ typedef struct {
     double  sell[DGEN_MAXP][DGEN_MAXT];
     uint8_t wkday[12][24];         /* 0-based period per (month, hour)             */
     uint8_t wkend[12][24];
-    int32_t flags;                 /* DGEN_ST_EMPTY_EC / DGEN_ST_UNIT if applicable*/
-    int32_t pad;
+    int32_t flags;                 /* DGEN_ST_EMPTY_EC / _UNIT / _DEMAND if so      */
+    int32_t dc;                    /* 1 + index into dgen_tables.demand; 0 = none  */
 } dgen_tariff;
+
+/* Demand charges of one tariff (extension mode): the ur_dc_flat_mat /
+ * ur_dc_tou_mat / ur_dc_sched_* fields process_tariff writes when
+ * SKIP_DEMAND_CHARGES is off (ff:604-615), packed on the host.  Per month the
+ * flat peak is the max hourly grid import (kW = kWh per hour; 0 without
+ * import) and each TOU peak the max over that period's hours; each peak is
+ * billed through its tier table (tier upper bounds in kW, the last tier
+ * unbounded above), escalated with the energy charges.  SSC semantics
+ * restated from SAM's published methodology: parity unpinned.                */
+typedef struct {
+    int32_t tou_nt[DGEN_DCP];      /* tiers per TOU period (0 = no charge)          */
+    int32_t flat_nt[12];           /* tiers per month (0 = no charge)               */
+    int32_t flags;                 /* DGEN_ST_DEMAND when the mats were out of range*/
+    int32_t pad;
+    double  tou_cap[DGEN_DCP][DGEN_DCT];
+    double  tou_price[DGEN_DCP][DGEN_DCT];   /* $/kW                              */
+    double  flat_cap[12][DGEN_DCT];
+    double  flat_price[12][DGEN_DCT];
+    uint8_t wkday[12][24];         /* 0-based demand period per (month, hour)       */
+    uint8_t wkend[12][24];
+} dgen_demand;
 
 /* One row of diffusion_shared.rate_switch_lkup_2020 (elec.py:828-836), already
  * filtered to one agent's (tech, eia_id, res_com) on the host.                */
@@ -123,6 +150,9 @@ typedef struct {
     int64_t n_shapes, n_cfs, n_wholesale, n_switches;
     int32_t n_tariffs;
     int32_t max_periods;           /* max P over tariffs (sizes LDS; 0 = DGEN_MAXP) */
+    const dgen_demand* demand;     /* [n_demand] (may be NULL when n_demand == 0)   */
+    int32_t n_demand;
+    int32_t pad;
 } dgen_tables;
 
 /* Agent batch, structure of arrays (device pointers, length n).  Column
@@ -136,7 +166,8 @@ typedef struct {
     const int32_t* sw_solar_cnt;
     const int32_t* sw_storage_off; /* rate-switch candidates, tech = 'storage'        */
     const int32_t* sw_storage_cnt;
-    const int32_t* scratch_slot;   /* hourly scratch slot for mo=2 battery runs or -1 */
+    const int32_t* scratch_slot;   /* hourly scratch slot for mo=2 or demand-charge   */
+                                   /* battery runs, or -1                             */
     const uint8_t* flags;          /* bit0 sector_abbr == 'res', bit1 state == 'CA'  */
     const int32_t* econ_life;      /* economic_lifetime_yrs                           */
     const int32_t* loan_term;      /* loan_term_yrs                                   */

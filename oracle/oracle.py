@@ -19,6 +19,8 @@ LIB_PATH = os.path.join(HERE, "build", "liborc.so")
 NH = 8760
 MAXP = 12
 MAXT = 6
+DCP = 8
+DCT = 4
 MAXY = 50
 
 _c_double = ctypes.c_double
@@ -35,6 +37,12 @@ class Tariff(ctypes.Structure):
         ("sell", (_c_double * MAXT) * MAXP),
         ("wkday", (ctypes.c_uint8 * 24) * 12),
         ("wkend", (ctypes.c_uint8 * 24) * 12),
+        ("dc_on", _c_int32),
+        ("dc_tou_nt", _c_int32 * DCP), ("dc_flat_nt", _c_int32 * 12),
+        ("dc_tou_cap", (_c_double * DCT) * DCP), ("dc_tou_price", (_c_double * DCT) * DCP),
+        ("dc_flat_cap", (_c_double * DCT) * 12), ("dc_flat_price", (_c_double * DCT) * 12),
+        ("dc_wkday", (ctypes.c_uint8 * 24) * 12),
+        ("dc_wkend", (ctypes.c_uint8 * 24) * 12),
     ]
 
 

@@ -223,6 +223,47 @@ static void bin_year(const orc_tariff* t, const int* mon, const int* per, const 
     }
 }
 
+/* Demand charge of one tier table: the last tier is unbounded above. */
+static double dc_tier_charge(double peak, const double* cap, const double* price, int nt) {
+    double charge = 0.0, prev = 0.0;
+    for (int k = 0; k < nt; k++) {
+        double hi = (k == nt - 1) ? INFINITY : cap[k];
+        double top = peak < hi ? peak : hi;
+        double amt = top - prev;
+        if (amt < 0.0) amt = 0.0;
+        if (hi > prev) prev = hi;
+        charge += amt * price[k];
+    }
+    return charge;
+}
+
+/* One year's demand charges (extension mode, parity unpinned): per month the
+ * flat peak = max hourly grid import, and per TOU demand period the max over
+ * that period's hours; no import -> peak 0.  Hours in time order, the calendar
+ * of hour_calendar.  Month charge = flat tiers, then periods 0..ORC_DCP-1. */
+static double year_demand(const orc_tariff* t, const double* gen, const double* load, double s) {
+    double total = 0.0;
+    int i = 0;
+    for (int m = 0; m < 12; m++) {
+        double flat = 0.0, pk[ORC_DCP];
+        for (int p = 0; p < ORC_DCP; p++) pk[p] = 0.0;
+        for (int d = 0; d < kDaysInMonth[m]; d++)
+            for (int h = 0; h < 24; h++, i++) {
+                int weekend = (i % 168) >= 120;
+                int p = weekend ? t->dc_wkend[m][h] : t->dc_wkday[m][h];
+                double g = gen ? gen[i] * s : 0.0;
+                double imp = load[i] - g;
+                if (imp > flat) flat = imp;
+                if (imp > pk[p]) pk[p] = imp;
+            }
+        double c = dc_tier_charge(flat, t->dc_flat_cap[m], t->dc_flat_price[m], t->dc_flat_nt[m]);
+        for (int p = 0; p < ORC_DCP; p++)
+            c += dc_tier_charge(pk[p], t->dc_tou_cap[p], t->dc_tou_price[p], t->dc_tou_nt[p]);
+        total += c;
+    }
+    return total;
+}
+
 /* cmod_utilityrate5 as driven at ff:364-368,258-270: analysis_period years,
  * system_use_lifetime_output = 0, degradation (%/yr, compounding),
  * rate escalation (1 + inflation + escalation)^i, outputs index 0 = 0. */
@@ -240,12 +281,15 @@ int orc_ur5(const orc_tariff* t, const orc_cfg* cfg, const double* gen, const do
 
     bin_year(t, mon, per, NULL, load, tsp, 1.0, net, imp, exv);
     double wo1 = year_bill(t, cfg, net, imp, exv, ts);
+    if (t->dc_on) wo1 += year_demand(t, NULL, load, 1.0);
     bill_w[0] = bill_wo[0] = aev[0] = 0.0;
     for (int i = 0; i < nyears; i++) {
         double r = pow_int(rate_base, i);
         double s = pow_int(sys_base, i);
         bin_year(t, mon, per, gen, load, tsp, s, net, imp, exv);
-        double w = year_bill(t, cfg, net, imp, exv, ts) * r;
+        double wb = year_bill(t, cfg, net, imp, exv, ts);
+        if (t->dc_on) wb += year_demand(t, gen, load, s);
+        double w = wb * r;
         double wo = wo1 * r;
         bill_w[i + 1] = w;
         bill_wo[i + 1] = wo;

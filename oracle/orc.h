@@ -37,6 +37,8 @@ extern "C" {
 #define ORC_MAXP  12
 #define ORC_MAXT  6
 #define ORC_MAXY  50
+#define ORC_DCP   8     /* demand-charge TOU periods (extension mode) */
+#define ORC_DCT   4     /* demand-charge tiers                        */
 
 /* Compiled tariff: what process_tariff() (financial_functions.py:575-648) leaves
  * in Utilityrate5.ElectricityRates for the energy-charge path.               */
@@ -50,6 +52,16 @@ typedef struct {
     double  sell[ORC_MAXP][ORC_MAXT];
     uint8_t wkday[12][24];   /* 0-based period id                              */
     uint8_t wkend[12][24];
+    /* demand charges (extension mode; the reference keeps them off, ff:35):
+     * monthly flat and TOU peaks of hourly grid import, tiered per month /
+     * period, the last tier unbounded.  dc_on = 0: no demand charge.        */
+    int32_t dc_on;
+    int32_t dc_tou_nt[ORC_DCP];      /* tiers per TOU period (0 = no charge)  */
+    int32_t dc_flat_nt[12];          /* tiers per month (0 = no charge)       */
+    double  dc_tou_cap[ORC_DCP][ORC_DCT], dc_tou_price[ORC_DCP][ORC_DCT];
+    double  dc_flat_cap[12][ORC_DCT], dc_flat_price[12][ORC_DCT];
+    uint8_t dc_wkday[12][24];        /* 0-based demand period                 */
+    uint8_t dc_wkend[12][24];
 } orc_tariff;
 
 /* PySAM config defaults the reference never sets (parity unpinned). */

@@ -20,3 +20,13 @@ def engine():
     eng = Engine(0)
     yield eng
     eng.close()
+
+
+@pytest.fixture(scope="session")
+def engine_dc():
+    """Engine in demand-charge extension mode (cfg.skip_demand_charges = 0)."""
+    from dgen_amd.config import EngineConfig
+    from dgen_amd.engine import Engine
+    eng = Engine(0, EngineConfig(skip_demand_charges=0))
+    yield eng
+    eng.close()

@@ -58,7 +58,8 @@ def golden_population():
     return b, cols, arr["shapes"], arr["cfs"], b.wholesale.array()
 
 
-def oracle_tariffs(records):
+def oracle_tariffs(records, demand=None):
+    """Device tariff records (+ the dgen_demand table) -> orc.Tariff list."""
     from oracle import oracle as orc
     out = []
     for r in records:
@@ -75,11 +76,28 @@ def oracle_tariffs(records):
             for h in range(24):
                 t.wkday[m][h] = int(r["wkday"][m, h])
                 t.wkend[m][h] = int(r["wkend"][m, h])
+        dc = int(r["dc"])
+        if dc > 0:
+            d = demand[dc - 1]
+            t.dc_on = 1
+            for p in range(orc.DCP):
+                t.dc_tou_nt[p] = int(d["tou_nt"][p])
+                for k in range(orc.DCT):
+                    t.dc_tou_cap[p][k] = float(d["tou_cap"][p, k])
+                    t.dc_tou_price[p][k] = float(d["tou_price"][p, k])
+            for m in range(12):
+                t.dc_flat_nt[m] = int(d["flat_nt"][m])
+                for k in range(orc.DCT):
+                    t.dc_flat_cap[m][k] = float(d["flat_cap"][m, k])
+                    t.dc_flat_price[m][k] = float(d["flat_price"][m, k])
+                for h in range(24):
+                    t.dc_wkday[m][h] = int(d["wkday"][m, h])
+                    t.dc_wkend[m][h] = int(d["wkend"][m, h])
         out.append(t)
     return out
 
 
-def oracle_population(cols, tariff_records, switches, shapes, cfs, wholesale):
+def oracle_population(cols, tariff_records, switches, shapes, cfs, wholesale, demand=None):
     """orc.Population mirroring product columns (same tables, same indices)."""
     from oracle import oracle as orc
     n = len(cols["load_kwh"])
@@ -101,7 +119,7 @@ def oracle_population(cols, tariff_records, switches, shapes, cfs, wholesale):
         "is_res": (cols["flags"] & 1).astype(int), "is_ca": ((cols["flags"] >> 1) & 1).astype(int),
         "econ_life": cols["econ_life"], "loan_term": cols["loan_term"], "tariff0": cols["tariff0"],
     }
-    return orc.Population(ocols, shapes, cfs, wholesale, oracle_tariffs(tariff_records),
+    return orc.Population(ocols, shapes, cfs, wholesale, oracle_tariffs(tariff_records, demand),
                           sw_solar, sw_storage)
 
 
@@ -170,3 +188,11 @@ def golden_finance():
     for c in meta["cases"]:
         c["rows"] = [{k: _dec(v) for k, v in r.items()} for r in c["rows"]]
     return meta
+
+
+@lru_cache(maxsize=None)
+def golden_tariffs_dc():
+    """tariffs_dc.json: the reference's compile with SKIP_DEMAND_CHARGES
+    flipped (tests/golden/make_golden_demand.py)."""
+    with open(os.path.join(GOLDEN, "tariffs_dc.json")) as f:
+        return json.load(f)

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(L, name), name
     assert set(names) == set(_lib.EXPORTED)
-    assert L.dgen_abi_version() == _lib.ABI_VERSION == 2
+    assert L.dgen_abi_version() == _lib.ABI_VERSION == 3
     m = re.search(r"#define DGEN_DEFAULT_CHUNKS\s+(\d+)", open(HEADER).read())
     assert m and int(m.group(1)) == _lib.DEFAULT_CHUNKS
     m = re.search(r"#define DGEN_DEFAULT_HOURLY_MONTHS\s+(\d+)", open(HEADER).read())
@@ -60,7 +60,8 @@ int main(void) {
   S(dgen_attach_in) S(dgen_attach_out) S(dgen_diffusion_in) S(dgen_diffusion_out)
   O(dgen_cfg, batt_v_nom) O(dgen_cfg, batt_eta_out) O(dgen_tariff, fixed) O(dgen_tariff, buy)
   O(dgen_tariff, sell) O(dgen_tariff, wkday) O(dgen_tariff, flags) O(dgen_tables, n_shapes)
-  O(dgen_tables, n_tariffs) O(dgen_agents, vor) O(dgen_outputs, baseline) O(dgen_outputs, net_with_batt)
+  O(dgen_tables, n_tariffs) O(dgen_tables, demand) S(dgen_demand) O(dgen_demand, tou_cap)
+  O(dgen_demand, flat_price) O(dgen_demand, wkend) O(dgen_agents, vor) O(dgen_outputs, baseline) O(dgen_outputs, net_with_batt)
   return 0;
 }
 """
@@ -98,6 +99,11 @@ def test_struct_offsets(layout):
         assert layout[f"dgen_tariff.{f}"] == TARIFF_DTYPE.fields[f][1], f
     assert layout["dgen_tables.n_shapes"] == _lib.Tables.n_shapes.offset
     assert layout["dgen_tables.n_tariffs"] == _lib.Tables.n_tariffs.offset
+    assert layout["dgen_tables.demand"] == _lib.Tables.demand.offset
+    from dgen_amd.tariff import DEMAND_DTYPE
+    assert layout["dgen_demand"] == DEMAND_DTYPE.itemsize
+    for f in ("tou_cap", "flat_price", "wkend"):
+        assert layout[f"dgen_demand.{f}"] == DEMAND_DTYPE.fields[f][1], f
     assert layout["dgen_agents.vor"] == _lib.Agents.vor.offset
     assert layout["dgen_outputs.baseline"] == _lib.Outputs.baseline.offset
     assert layout["dgen_outputs.net_with_batt"] == _lib.Outputs.net_with_batt.offset

@@ -1,0 +1,79 @@
+"""Demand charges (extension mode; the reference keeps them off, ff:35): GPU vs
+the CPU oracle's restatement on seeded commercial populations whose tariffs
+carry monthly flat and TOU demand charges (dgen_amd.synth 'com_dc_batt'), NEM
+and net billing, with the battery run.  The compile of the demand mats is
+pinned to the reference (tests/test_tariff.py, tariffs_dc.json); the SSC
+demand arithmetic is parity unpinned, so this checks GPU == restatement."""
+import numpy as np
+import pytest
+import torch
+
+from dgen_amd.columnar import assign_scratch
+from dgen_amd.engine import outputs_to_host
+from dgen_amd.synth import make_population
+from oracle import oracle as orc
+from tests import helpers
+
+pytestmark = pytest.mark.gpu
+
+
+def _pop(n, net_billing=False, seed=7):
+    pop = make_population("com_dc_batt", n, seed=20260000 + seed, n_res_shapes=16, n_com_shapes=32,
+                          n_cf=32, n_counties=16, n_tariffs=24)
+    if net_billing:          # every other tariff bills net (mo 2): hourly imports + demand
+        t = pop.tariffs.copy()
+        t["mo"][1::2] = 2
+        pop.tariffs = t
+        pop.n_scratch = assign_scratch(pop.cols, pop.tariffs, pop.switches)
+    return pop
+
+
+def _run(eng, pop, demand):
+    eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    eng.set_tariffs(pop.tariffs, demand)
+    eng.set_switches(pop.switches)
+    batch = eng.upload_agents(pop.cols, pop.n_scratch)
+    out = eng.alloc_outputs(batch.n, hourly=True)
+    eng.size(batch, out)
+    torch.cuda.synchronize()
+    return outputs_to_host(out)
+
+
+def _check(o, ref, life):
+    for i, r in enumerate(ref):
+        assert o["status"][i] == 0 and r["status"] == 0, i
+        assert o["nfev"][i] == r["nfev"], (i, o["nfev"][i], r["nfev"])
+        assert o["tariff_final"][i] == r["tariff_final"], i
+        assert abs(o["system_kw"][i] - r["system_kw"]) <= 1e-9 * max(1.0, r["system_kw"]), i
+        for k in ("npv", "first_with", "first_without", "batt_kwh", "npv_pv_batt"):
+            assert np.isclose(o[k][i], r[k], rtol=1e-6, atol=1e-6), (i, k, o[k][i], r[k])
+        assert o["payback_period"][i] == r["payback_period"], i
+        N1 = int(life[i]) + 1
+        for k_o, k_r in (("bill_w_pv", "bill_w_pv_only"), ("bill_wo_pv", "bill_wo_pv_only"),
+                         ("bill_w_batt", "bill_w_pv_batt"), ("bill_wo_batt", "bill_wo_pv_batt"),
+                         ("cash_flow", "cash_flow")):
+            assert np.allclose(o[k_o][i, :N1], r[k_r], rtol=1e-6, atol=1e-5), (i, k_o)
+
+
+@pytest.mark.parametrize("net_billing", [False, True])
+def test_demand_charges_match_oracle(engine_dc, net_billing):
+    pop = _pop(160, net_billing)
+    assert pop.demand.size and (pop.tariffs["dc"] > 0).all()
+    o = _run(engine_dc, pop, pop.demand)
+    opop = helpers.oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs,
+                                     pop.wholesale, demand=pop.demand)
+    _check(o, opop.run(orc.make_cfg()), pop.cols["econ_life"])
+
+
+def test_reference_mode_ignores_demand_records(engine, engine_dc):
+    """skip_demand_charges = 1 (the reference) bills exactly as if the tariffs
+    had no demand records; billing them raises every no-system bill."""
+    pop = _pop(96, seed=9)
+    o_ref = _run(engine, pop, pop.demand)
+    stripped = pop.tariffs.copy()
+    stripped["dc"] = 0
+    o_plain = _run(engine, type(pop)(**{**pop.__dict__, "tariffs": stripped}), None)
+    for k in ("system_kw", "npv", "first_without", "npv_pv_batt"):
+        assert np.array_equal(o_ref[k], o_plain[k]), k
+    o_dc = _run(engine_dc, pop, pop.demand)
+    assert (o_dc["first_without"] > o_ref["first_without"]).all()

@@ -126,3 +126,36 @@ def test_golden_covers_edge_cases():
 def test_payback_nonfinite_maps_to_30_1():
     assert orc.np_round1(30.1) == 30.1
     assert not math.isfinite(float("nan"))
+
+
+def test_oracle_demand_charge_known_answer():
+    """Flat load L kW every hour, no system: each month's flat peak is L, so a
+    $10/kW flat charge adds 12 * 10 * L to the year-1 no-system bill; a TOU
+    charge of $4/kW on period 2 (hours 12-17, every day) adds 12 * 4 * L."""
+    from tests.helpers import oracle_tariffs
+    from dgen_amd.tariff import TariffTable
+    L = 7.25
+    raw = {"e_prices": [[0.1]], "ur_dc_flat_mat": [[m, 1, 1e38, 10.0] for m in range(12)],
+           "ur_dc_tou_mat": [[1, 1, 1e38, 0.0], [2, 1, 1e38, 4.0]],
+           "ur_dc_sched_weekday": [[2 if 12 <= h < 18 else 1 for h in range(24)]] * 12,
+           "ur_dc_sched_weekend": [[2 if 12 <= h < 18 else 1 for h in range(24)]] * 12}
+    tt = TariffTable(skip_demand_charges=False)
+    tt.add(raw, False)
+    tt.add({"e_prices": [[0.1]]}, False)
+    t_dc, t_plain = oracle_tariffs(tt.array(), tt.demand_array())
+    cfg = orc.make_cfg()
+    load = np.full(orc.NH, L)
+    gen = np.zeros(orc.NH)
+    a = orc.ur5(t_dc, cfg, gen, load, None, 3, 2.5, 0.0, 0.5)
+    b = orc.ur5(t_plain, cfg, gen, load, None, 3, 2.5, 0.0, 0.5)
+    assert a["bill_wo"][1] - b["bill_wo"][1] == pytest.approx(12 * 14.0 * L, rel=1e-12)
+    # escalated with the energy charges: year 2 = year 1 x (1 + 2.5 %)
+    assert a["bill_wo"][2] == pytest.approx(a["bill_wo"][1] * 1.025, rel=1e-14)
+    # with a system covering the load in hours 12-17 only, the TOU peak of
+    # period 2 falls to 0 and the flat peak stays L
+    gen2 = np.zeros(orc.NH)
+    hod = np.arange(orc.NH) % 24
+    gen2[(hod >= 12) & (hod < 18)] = L
+    c = orc.ur5(t_dc, cfg, gen2, load, None, 1, 2.5, 0.0, 0.0)
+    d = orc.ur5(t_plain, cfg, gen2, load, None, 1, 2.5, 0.0, 0.0)
+    assert c["bill_w"][1] - d["bill_w"][1] == pytest.approx(12 * 10.0 * L, rel=1e-12)

@@ -97,3 +97,57 @@ def test_too_many_periods_rejected():
     raw = {"e_prices": [[0.1] * 13], "e_wkday_12by24": [[0] * 24] * 12}
     with pytest.raises(T.TariffError):
         T.compile_tariff(raw, is_ca=False)
+
+
+# ---------------------------------------------------------------------------
+# demand charges (extension mode): the reference's process_tariff demand branch
+# (ff:604-615) captured with SKIP_DEMAND_CHARGES flipped -> tariffs_dc.json
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("case", helpers.golden_tariffs_dc(), ids=lambda c: c["name"])
+def test_demand_compile_matches_reference(case):
+    td = T.normalize_tariff(case["raw"], 0.0)
+    assert _eq(_roundtrip(td), case["normalized"]), case["name"]
+    got = _roundtrip(T.rate_fields(td, 0.0, ts_sell_rate=None, skip_demand_charges=False))
+    assert _eq(got, case["process"]), case["name"]
+    # the reference's own switch value keeps demand charges off
+    off = T.rate_fields(td, 0.0, ts_sell_rate=None)
+    assert off["ur_dc_enable"] == 0 and "ur_dc_tou_mat" not in off
+
+
+def _dc(name):
+    case = next(c for c in helpers.golden_tariffs_dc() if c["name"] == name)
+    return T.compile_tariff(case["raw"], is_ca=False, skip_demand_charges=False)
+
+
+def test_demand_record_packing():
+    ct = _dc("dc_tou_ur")
+    d = ct.demand
+    assert d is not None and int(d["flags"]) == 0
+    assert list(d["tou_nt"][:3]) == [2, 2, 0] and list(d["flat_nt"]) == [0] * 12
+    assert d["tou_cap"][0, 0] == 50.0 and d["tou_price"][1, 1] == np.float32(14.25)
+    assert int(d["wkday"][0, 12]) == 1 and int(d["wkday"][0, 11]) == 0 and int(d["wkend"][5, 15]) == 0
+    both = _dc("dc_both_ur").demand
+    assert list(both["flat_nt"]) == [2] * 12 and both["flat_price"][7, 1] == 7.0
+    assert list(both["tou_nt"][:4]) == [1, 1, 1, 0]
+
+
+def test_demand_flags_outside_ssc_limits():
+    # the legacy flat builder numbers months 1..12 (ff:805-806); SSC's month
+    # column is 0-based, so month 12 is rejected
+    assert int(_dc("dc_legacy_flat_12").record["flags"]) & T.ST_DEMAND
+    assert int(_dc("dc_tier_gap").record["flags"]) & T.ST_DEMAND
+    assert int(_dc("dc_period9").record["flags"]) & T.ST_DEMAND
+    assert int(_dc("dc_ragged_sched").record["flags"]) & T.ST_DEMAND      # zero-padded schedule
+    assert _dc("dc_flag_only").demand is None and _dc("dc_nonfinite").demand is None
+    assert int(_dc("dc_legacy_tou").record["flags"]) == 0
+
+
+def test_demand_table_indices():
+    tt = T.TariffTable(skip_demand_charges=False)
+    a = tt.add(next(c["raw"] for c in helpers.golden_tariffs_dc() if c["name"] == "dc_tou_ur"), False)
+    b = tt.add({"e_prices": [[0.1]]}, False)
+    c = tt.add(next(c["raw"] for c in helpers.golden_tariffs_dc() if c["name"] == "dc_flat_ur"), False)
+    arr = tt.array()
+    assert [int(arr[k]["dc"]) for k in (a, b, c)] == [1, 0, 2]
+    assert tt.demand_array().shape == (2,)
+    assert T.TariffTable().add(next(c["raw"] for c in helpers.golden_tariffs_dc()), False) == 0
