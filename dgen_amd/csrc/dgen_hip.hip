@@ -1268,30 +1268,41 @@ __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& sr
     for (int m = 0; m < 12; m++) {
         double flat = 0.0;
         for (int q = 0; q < DCP; q++) S.at(q) = 0.0;
+        // half a day per step: the 12 hours of every input are loaded
+        // together (one memory latency per 12 hours, not one per 4)
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
-            const uint8_t* sched = ((d % 7) >= 5) ? D->wkend[m] : D->wkday[m];
+            const uint32_t* sq = reinterpret_cast<const uint32_t*>(((d % 7) >= 5) ? D->wkend[m] : D->wkday[m]);
 #pragma unroll 1
-            for (int c0 = 0; c0 < 24; c0 += 4, h += 4) {
-                const float4 sv = *reinterpret_cast<const float4*>(src.shape + h);
-                const uint32_t pq = *reinterpret_cast<const uint32_t*>(sched + c0);
-                const float shv[4] = {sv.x, sv.y, sv.z, sv.w};
-                double g[4] = {0.0, 0.0, 0.0, 0.0};
-                if (with_gen) {
-                    if (src.sysgen) {
+            for (int half12 = 0; half12 < 2; half12++, h += 12) {
+                uint32_t pq[3];
+                float sh[12];
+                double g[12];
 #pragma unroll
-                        for (int k = 0; k < 4; k++) g[k] = src.sysgen[(int64_t)(h + k) * src.sys_stride];
-                    } else {
-                        const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
-                        g[0] = ((double)cv.x / 1e6) * src.gen_scale;
-                        g[1] = ((double)cv.y / 1e6) * src.gen_scale;
-                        g[2] = ((double)cv.z / 1e6) * src.gen_scale;
-                        g[3] = ((double)cv.w / 1e6) * src.gen_scale;
+                for (int k = 0; k < 3; k++) {
+                    pq[k] = sq[3 * half12 + k];
+                    const float4 a = *reinterpret_cast<const float4*>(src.shape + h + 4 * k);
+                    sh[4 * k] = a.x; sh[4 * k + 1] = a.y; sh[4 * k + 2] = a.z; sh[4 * k + 3] = a.w;
+                }
+                if (with_gen && src.sysgen) {
+#pragma unroll
+                    for (int k = 0; k < 12; k++) g[k] = src.sysgen[(int64_t)(h + k) * src.sys_stride];
+                } else if (with_gen) {
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const int4 cv = *reinterpret_cast<const int4*>(src.cf + h + 4 * k);
+                        g[4 * k] = ((double)cv.x / 1e6) * src.gen_scale;
+                        g[4 * k + 1] = ((double)cv.y / 1e6) * src.gen_scale;
+                        g[4 * k + 2] = ((double)cv.z / 1e6) * src.gen_scale;
+                        g[4 * k + 3] = ((double)cv.w / 1e6) * src.gen_scale;
                     }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 12; k++) g[k] = 0.0;
                 }
 #pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const double imp = (double)shv[k] * src.load_scale - g[k] * s;
-                    const int p = (int)((pq >> (8 * k)) & 0xffu);
+                for (int k = 0; k < 12; k++) {
+                    const double imp = (double)sh[k] * src.load_scale - g[k] * s;
+                    const int p = (int)((pq[k >> 2] >> (8 * (k & 3))) & 0xffu);
                     flat = imp > flat ? imp : flat;
                     double& pk = S.at(p < DCP ? p : 0);
                     pk = imp > pk ? imp : pk;
@@ -1444,6 +1455,7 @@ struct YCtx {
     const dgen_demand* dem_table;
     const dgen_demand* dem;     // current tariff's demand charges (or nullptr)
     int n_dem;
+    bool dem_wo_pending;        // wo1 still lacks the new tariff's demand charge
     int sw_cnt;
     int tariff, switched, status;
     double capex, ccm, kwh, yearend, load_scale;
@@ -1474,9 +1486,9 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
     } else {
         c.wo1 = yl_bill_mo2(t, c.src, 1.0, false, c.S);
     }
-    if constexpr (DC) {
+    if constexpr (DC) {   // its no-system charge is added by the next objective
         c.dem = tariff_demand(c.dem_table, c.n_dem, true, t);
-        if (c.dem) c.wo1 += yl_demand(c.dem, c.src, 1.0, false, c.S);
+        c.dem_wo_pending = c.dem != nullptr;
     }
 }
 
@@ -1506,8 +1518,16 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     }
     if constexpr (DC) {
         if (c.dem) {
+            // one inlined demand pass for both uses: the no-system charge of a
+            // newly set tariff (pass 0, once), then this evaluation's (pass 1)
             c.src.gen_scale = kws;
-            wb += yl_demand(c.dem, c.src, c.s_y, true, c.S);
+            for (int pass = c.dem_wo_pending ? 0 : 1; pass < 2; pass++) {
+                const bool wg = pass == 1;
+                const double v = yl_demand(c.dem, c.src, wg ? c.s_y : 1.0, wg, c.S);
+                if (wg) wb += v;
+                else c.wo1 += v;
+            }
+            c.dem_wo_pending = false;
         }
     }
     double w = wb * c.r_y;
@@ -1527,7 +1547,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 // DC: demand charges billed (extension mode) -- a separate instantiation so
 // the reference mode's register allocation is untouched
 template <int LPA, bool DC>
-__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1) {
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
@@ -1541,6 +1561,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.dem_table = T.demand;
     c.n_dem = T.n_demand;
     c.dem = nullptr;
+    c.dem_wo_pending = false;
     c.sw_rows = T.switches + A.sw_solar_off[i];
     c.sw_cnt = A.sw_solar_cnt[i];
     c.status = 0;
@@ -1700,8 +1721,12 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         wb = yl_bill_net(t, src, s_y, true, S);
     }
     if (DC && dem) {   // k_size's first_without already carries the no-system demand charge
-        if (!same_tariff) wo1 += yl_demand(dem, src, 1.0, false, S);
-        wb += yl_demand(dem, src, s_y, true, S);
+        for (int pass = same_tariff ? 1 : 0; pass < 2; pass++) {
+            const bool wg = pass == 1;
+            const double v = yl_demand(dem, src, wg ? s_y : 1.0, wg, S);
+            if (wg) wb += v;
+            else wo1 += v;
+        }
     }
     double w = wb * r_y;
     double wo = wo1 * r_y;
