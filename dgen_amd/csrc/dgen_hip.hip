@@ -1316,6 +1316,145 @@ __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& sr
     return total;
 }
 
+// ---------------------------------------------------------------------------
+// Demand-charge envelopes (PV-only search).  Within one (month, demand
+// period) group the import of hour h at generation scale t is the line
+// L_h - g_h t, and the group's peak is max(0, max_h line).  The search only
+// evaluates t in [t_lo, t_hi] (the Brent bracket's kW x the analysis years'
+// degradation factors), where a line can reach the max only if it beats
+// M(t) = max(A(t), B(t)) -- A, B the maxima at t_lo and t_hi -- at the point
+// t* where A and B cross (M is their convex hull: a line below M at t_lo, t*
+// and t_hi is below it on the whole interval).  So each group keeps A, B and
+// the lines above M(t*) (a relative slack of 1e-10 keeps the set a superset
+// under rounding); an evaluation then takes the max over <= DC_NL lines per
+// group instead of re-scanning 8760 hours, with the hourly pass's arithmetic
+// per line (L = shape x load_scale, g = cf / 1e6, import = L - (g x kW') x s),
+// so the peaks are the hourly pass's peaks.  A group that needs more lines
+// sends the agent back to the hourly pass (yl_demand).
+// ---------------------------------------------------------------------------
+constexpr int DC_NL = 8;
+struct DcEnv {
+    double2* lines;   // [12][DCP][DC_NL] (L, g)
+    double* maxl;     // [12][DCP] max load (the no-system peak)
+    int* cnt;         // [12][DCP] lines kept (0 = period absent from the month)
+};
+constexpr size_t DCW_BYTES = (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double) + sizeof(int));
+
+__device__ __forceinline__ DcEnv dc_env_at(void* base, int64_t i) {
+    char* b = reinterpret_cast<char*>(base) + (size_t)i * DCW_BYTES;
+    DcEnv e;
+    e.lines = reinterpret_cast<double2*>(b);
+    e.maxl = reinterpret_cast<double*>(b + (size_t)12 * DCP * DC_NL * sizeof(double2));
+    e.cnt = reinterpret_cast<int*>(b + (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double)));
+    return e;
+}
+
+// Build the agent's envelopes: segment lane m < 12 takes month m (two passes
+// over the month per demand period present).  Returns true when every group
+// fit in DC_NL lines (segment-uniform).
+template <int LPA>
+__device__ bool yl_dc_build(const dgen_demand* D, const YSrc& src, double tlo, double thi,
+                            const DcEnv& E, const Seg<LPA>& g) {
+    bool ok = true;
+    const int m = g.sl;
+    if (m < 12) {
+        uint32_t mask = 0;
+        for (int h = 0; h < 24; h++) mask |= (1u << D->wkday[m][h]) | (1u << D->wkend[m][h]);
+        const int d0 = c_month_start_day[m], d1 = c_month_start_day[m + 1];
+        for (int p = 0; p < DCP; p++) {
+            int n_l = 0;
+            double mL = 0.0;
+            if ((mask >> p) & 1u) {
+                double aL = 0.0, ag = 0.0, av = -INFINITY, bL = 0.0, bg = 0.0, bv = -INFINITY;
+                int ah = -1, bh = -1;
+                for (int pass = 0; pass < 2; pass++) {
+                    double ts = tlo, Ms = 0.0, slack = 0.0;
+                    if (pass == 1) {
+                        if (ag > bg) {
+                            ts = (aL - bL) / (ag - bg);
+                            ts = ts < tlo ? tlo : (ts > thi ? thi : ts);
+                        }
+                        const double va = aL - ag * ts, vb = bL - bg * ts;
+                        Ms = va > vb ? va : vb;
+                        slack = 1e-10 * (fabs(aL) + fabs(bL) + 1.0);
+                        E.lines[(m * DCP + p) * DC_NL] = make_double2(aL, ag);
+                        E.lines[(m * DCP + p) * DC_NL + 1] = make_double2(bL, bg);
+                        n_l = 2;
+                    }
+                    for (int d = d0; d < d1; d++) {
+                        const uint8_t* sc = ((d % 7) >= 5) ? D->wkend[m] : D->wkday[m];
+#pragma unroll 1
+                        for (int c0 = 0; c0 < 24; c0 += 4) {
+                            const int h0 = d * 24 + c0;
+                            const uint32_t pq = *reinterpret_cast<const uint32_t*>(sc + c0);
+                            const float4 sv = *reinterpret_cast<const float4*>(src.shape + h0);
+                            const int4 cv = *reinterpret_cast<const int4*>(src.cf + h0);
+                            const float shv[4] = {sv.x, sv.y, sv.z, sv.w};
+                            const int cfv[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+                            for (int k = 0; k < 4; k++) {
+                                if ((int)((pq >> (8 * k)) & 0xffu) != p) continue;
+                                const double L = (double)shv[k] * src.load_scale;
+                                const double gp = (double)cfv[k] / 1e6;
+                                if (pass == 0) {
+                                    mL = L > mL ? L : mL;
+                                    const double vlo = L - gp * tlo, vhi = L - gp * thi;
+                                    if (vlo > av) { av = vlo; aL = L; ag = gp; ah = h0 + k; }
+                                    if (vhi > bv) { bv = vhi; bL = L; bg = gp; bh = h0 + k; }
+                                } else if (h0 + k != ah && h0 + k != bh && L - gp * ts > Ms - slack) {
+                                    if (n_l < DC_NL) E.lines[(m * DCP + p) * DC_NL + n_l++] = make_double2(L, gp);
+                                    else ok = false;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            E.cnt[m * DCP + p] = n_l;
+            E.maxl[m * DCP + p] = mL;
+        }
+    }
+    // the other lanes of the wave read these groups: stores complete and
+    // visible to the work-group (one wave) before any lane reads them
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return g.first(!ok) < 0;
+}
+
+// One lane's year of demand charges from the envelopes (same month / period /
+// tier order as yl_demand): system output x s at generation kW' kws, or the
+// no-system peaks (max load) when !with_gen.
+__device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& E, double kws, double s,
+                                             bool with_gen, const YLds& S) {
+    double total = 0.0;
+    for (int m = 0; m < 12; m++) {
+        double flat = 0.0;
+        for (int q = 0; q < DCP; q++) {
+            const int n_l = E.cnt[m * DCP + q];
+            double pk = 0.0;
+            if (n_l > 0) {
+                if (with_gen) {
+                    const double2* ln = E.lines + (m * DCP + q) * DC_NL;
+                    for (int k = 0; k < n_l; k++) {
+                        const double2 v = ln[k];
+                        const double imp = v.x - (v.y * kws) * s;
+                        pk = imp > pk ? imp : pk;
+                    }
+                } else {
+                    pk = E.maxl[m * DCP + q];
+                }
+            }
+            S.at(q) = pk;
+            flat = pk > flat ? pk : flat;
+        }
+        double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
+        for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
+        total += c;
+    }
+    return total;
+}
+
 // bins of a tariff from a row's slot sums, one (month, period) cell per lane
 template <int LPA>
 __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
@@ -1456,6 +1595,9 @@ struct YCtx {
     const dgen_demand* dem;     // current tariff's demand charges (or nullptr)
     int n_dem;
     bool dem_wo_pending;        // wo1 still lacks the new tariff's demand charge
+    bool env_ok;                // the demand envelopes of the current tariff fit
+    DcEnv env;                  // the agent's envelope storage
+    double tlo, thi;            // generation-scale range of the search
     int sw_cnt;
     int tariff, switched, status;
     double capex, ccm, kwh, yearend, load_scale;
@@ -1521,9 +1663,12 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
             // one inlined demand pass for both uses: the no-system charge of a
             // newly set tariff (pass 0, once), then this evaluation's (pass 1)
             c.src.gen_scale = kws;
+            if (c.dem_wo_pending) c.env_ok = c.env.lines && yl_dc_build(c.dem, c.src, c.tlo, c.thi, c.env, c.g);
             for (int pass = c.dem_wo_pending ? 0 : 1; pass < 2; pass++) {
                 const bool wg = pass == 1;
-                const double v = yl_demand(c.dem, c.src, wg ? c.s_y : 1.0, wg, c.S);
+                const double s = wg ? c.s_y : 1.0;
+                const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kws, s, wg, c.S)
+                                          : yl_demand(c.dem, c.src, s, wg, c.S);
                 if (wg) wb += v;
                 else c.wo1 += v;
             }
@@ -1548,7 +1693,8 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 // the reference mode's register allocation is untouched
 template <int LPA, bool DC>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
-k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1) {
+k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
+         void* dcws) {
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -1562,6 +1708,11 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.n_dem = T.n_demand;
     c.dem = nullptr;
     c.dem_wo_pending = false;
+    c.env_ok = false;
+    c.env.lines = nullptr;
+    if constexpr (DC) {
+        if (dcws) c.env = dc_env_at(dcws, i);
+    }
     c.sw_rows = T.switches + A.sw_solar_off[i];
     c.sw_cnt = A.sw_solar_cnt[i];
     c.status = 0;
@@ -1614,6 +1765,13 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
             O.tariff_final[i] = t0; O.switched[i] = 0;
         }
         return;
+    }
+    if constexpr (DC) {   // generation-scale range the search can evaluate (envelopes)
+        const int ln = (c.N >= 1 && c.N <= LPA) ? c.N - 1 : 0;
+        const double sN = c.g.bcast(c.s_y, ln);
+        const double s_lo = sN < 1.0 ? sN : 1.0, s_hi = sN > 1.0 ? sN : 1.0;
+        c.tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
+        c.thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
     }
     yl_set_tariff<LPA, DC>(c, t0);
     int nfev = 0;
@@ -2139,6 +2297,8 @@ struct dgen_ctx {
     int pending;       // recorded, not yet folded
     double sum_ms[3];
     int64_t count;
+    void* dc_buf = nullptr;   // demand-charge envelopes, DCW_BYTES per agent (grown on demand)
+    size_t dc_cap = 0;
 };
 
 static int fold_one(dgen_ctx* c, int slot) {
@@ -2215,6 +2375,7 @@ int32_t dgen_close(dgen_ctx* c) {
     (void)hipEventDestroy(c->fork);
     (void)hipEventDestroy(c->join);
     (void)hipStreamDestroy(c->s2);
+    if (c->dc_buf) (void)hipFree(c->dc_buf);
     delete c;
     return DGEN_OK;
 }
@@ -2305,6 +2466,17 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     if (dc && 4 * lds_half(Tk.max_periods) < DCP) Tk.max_periods = (DCP + 3) / 4;
     T = &Tk;
     HIP_TRY(hipSetDevice(c->device));
+    if (dc && (size_t)n * DCW_BYTES > c->dc_cap) {   // envelope storage (context-owned)
+        if (c->dc_buf) HIP_TRY(hipFree(c->dc_buf));
+        c->dc_buf = nullptr;
+        c->dc_cap = 0;
+        if (hipMalloc(&c->dc_buf, (size_t)n * DCW_BYTES) != hipSuccess) {
+            c->dc_buf = nullptr;   // no envelopes: the kernels fall back to the hourly pass
+            (void)hipGetLastError();
+        } else {
+            c->dc_cap = (size_t)n * DCW_BYTES;
+        }
+    }
     hipStream_t s = (hipStream_t)stream;
     if (c->pending == dgen_ctx::RING) {   // fold the oldest record before reuse
         int r = fold_one(c, c->head);
@@ -2340,13 +2512,17 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipEventRecord(e[0], s));
         const dim3 ygrid((unsigned)((m + apb - 1) / apb));
         if (lpa == 32 && !dc)
-            hipLaunchKernelGGL((k_size_w<32, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+            hipLaunchKernelGGL((k_size_w<32, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
+                               nullptr);
         else if (lpa == 32)
-            hipLaunchKernelGGL((k_size_w<32, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+            hipLaunchKernelGGL((k_size_w<32, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
+                               c->dc_buf);
         else if (!dc)
-            hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+            hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
+                               nullptr);
         else
-            hipLaunchKernelGGL((k_size_w<WAVE, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1);
+            hipLaunchKernelGGL((k_size_w<WAVE, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
+                               c->dc_buf);
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
         HIP_TRY(hipEventRecord(e[2], s2));
