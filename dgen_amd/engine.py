@@ -184,6 +184,14 @@ class Engine:
             if order.shape != (n,) or not np.array_equal(np.sort(order), np.arange(n)):
                 raise ValueError("order must be a permutation of range(n)")
             cols = {k: np.asarray(v)[order] for k, v in cols.items()}
+            # scratch slots renumbered in device order: the workspace plane is
+            # [8760][n_scratch], so neighbouring lanes then store to neighbouring
+            # slots (one line per wave-hour, not one partial line per lane)
+            sl = np.asarray(cols["scratch_slot"])
+            need = sl >= 0
+            renum = np.full(n, -1, dtype=np.int32)
+            renum[need] = np.arange(int(need.sum()), dtype=np.int32)
+            cols["scratch_slot"] = renum
         dev = {}
         tmap = {"int32": torch.int32, "uint8": torch.uint8, "float64": torch.float64}
         for name, dt in _lib.AGENT_COLUMNS:

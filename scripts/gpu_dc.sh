@@ -12,3 +12,7 @@ timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu > gpurun_out/ben
 cut -c1-300 gpurun_out/bench_res.log | tail -1
 timeout -k 10 400 python bench.py --config com_dc_batt --agents 200000 --steps 3 --warmup 1 --no-cpu > gpurun_out/bench_dc.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_dc.log | grep -o '"value": [0-9.]*\|"kernel_ms": {[^}]*}'
+if [ -n "$COM" ]; then
+  timeout -k 10 400 python bench.py --config com_8m --agents 200000 --steps 3 --warmup 1 --no-cpu > gpurun_out/bench_com.log 2>&1 || exit $?
+  tail -1 gpurun_out/bench_com.log | grep -o '"value": [0-9.]*\|"kernel_ms": {[^}]*}'
+fi
