@@ -1414,11 +1414,15 @@ __device__ bool yl_dc_build(const dgen_demand* D, const YSrc& src, double tlo, d
             E.maxl[m * DCP + p] = mL;
         }
     }
-    // the other lanes of the wave read these groups: stores complete and
-    // visible to the work-group (one wave) before any lane reads them
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    // the other lanes of the wave read these groups.  A work-group-scope
+    // release emits no vmcnt wait for a one-wave work-group (checked in the
+    // ISA: the loads could overtake the stores), so: wait for every store
+    // to complete, then drop the CU's L1 lines (a rebuild after a rate switch
+    // rewrites lines the evaluations have cached) -- s_waitcnt vmcnt(0) +
+    // buffer_inv sc1, once per build.
+    __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     return g.first(!ok) < 0;
 }
 
