@@ -1104,7 +1104,7 @@ __device__ __forceinline__ double reg_month_charge(const dgen_tariff& t, int m, 
 // (and system output / sell-rate) values are loaded together before use, and
 // each hour adds dd (or the export credit) into its period's register, the
 // others adding an exact +0.0 -- the same sums in the same hour order.
-constexpr int MO2_CH = 4;
+constexpr int MO2_CH = 8;
 __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YSrc& src, double s,
                                                   bool with_gen) {
     const int P = t.P;
@@ -1115,10 +1115,12 @@ __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YS
 #pragma unroll
         for (int p = 0; p < PREG; p++) { imp[p] = 0.0; exv[p] = 0.0; }
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++, h += 24) {
-            const uint64_t* sr = reinterpret_cast<const uint64_t*>(((d % 7) >= 5) ? t.wkend[m] : t.wkday[m]);
+            const uint32_t* sr = reinterpret_cast<const uint32_t*>(((d % 7) >= 5) ? t.wkend[m] : t.wkday[m]);
 #pragma unroll 1
             for (int c0 = 0; c0 < 24; c0 += MO2_CH) {
-                const uint64_t sch = sr[c0 / 8] >> (8 * (c0 % 8));
+                uint32_t pq[MO2_CH / 4];
+#pragma unroll
+                for (int j = 0; j < MO2_CH / 4; j++) pq[j] = sr[c0 / 4 + j];
                 float sh[MO2_CH];
                 double g[MO2_CH], tsv[MO2_CH];
 #pragma unroll
@@ -1151,7 +1153,7 @@ __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YS
                 for (int k = 0; k < MO2_CH; k++) {
                     const double load = (double)sh[k] * src.load_scale;
                     const double dd = load - g[k] * s;
-                    const int p = (int)((sch >> (8 * k)) & 0xffu);
+                    const int p = (int)((pq[k >> 2] >> (8 * (k & 3))) & 0xffu);
                     const bool pos = dd > 0.0;
                     double e = -dd;
                     if (src.ts) e *= (double)(float)(tsv[k] * src.ts_mult);
@@ -1180,6 +1182,12 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
     int h = 0;
     for (int m = 0; m < 12; m++) {
         for (int p = 0; p < P; p++) { S.at(p) = 0.0; S.at(half + p) = 0.0; }
+        // the running import / export sums of the current period live in
+        // registers (cur, ci, ce) and go through LDS only when the period
+        // changes: the same additions in the same hour order, without an LDS
+        // read-modify-write round trip per hour
+        int cur = 0;
+        double ci = 0.0, ce = 0.0;
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             const uint8_t* sched = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
 #pragma unroll 1
@@ -1210,16 +1218,25 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
                     double load = (double)shv[k] * src.load_scale;
                     double dd = load - g[k] * s;
                     int p = (int)((pq >> (8 * k)) & 0xffu);
+                    if (p != cur) {
+                        S.at(cur) = ci;
+                        S.at(half + cur) = ce;
+                        cur = p;
+                        ci = S.at(p);
+                        ce = S.at(half + p);
+                    }
                     if (dd > 0.0) {
-                        S.at(p) += dd;
+                        ci += dd;
                     } else {
                         double e = -dd;
                         if (src.ts) e *= (double)(float)(tsv[k] * src.ts_mult);
-                        S.at(half + p) += e;
+                        ce += e;
                     }
                 }
             }
         }
+        S.at(cur) = ci;
+        S.at(half + cur) = ce;
         double cr = 0.0;
         for (int p = 0; p < P; p++) {
             double e = S.at(half + p);
