@@ -70,6 +70,19 @@ void set_err(const char* fmt, ...) {
         }                                                                          \
     } while (0)
 
+// gen_per_kw = cf / 1e6 (ff:350) without the per-hour IEEE division: the
+// reciprocal product corrected by one FMA residual step (Markstein) equals
+// the correctly rounded quotient for every |cf| <= 2e7 (checked for each of
+// those integers, tests/check_cf_div.c); larger values divide.
+__device__ __forceinline__ double cf_per_kw(int32_t x) {
+    const double a = (double)x;
+    if (x > 20000000 || x < -20000000) return a / 1e6;
+    constexpr double inv = 1.0 / 1e6;
+    const double q = a * inv;
+    const double r = __builtin_fma(-q, 1e6, a);
+    return __builtin_fma(r, inv, q);
+}
+
 // ---------------------------------------------------------------------------
 // numpy pairwise summation (loops_utils.h.src), chunked by the 8192-element
 // reduction buffer; identical association order => bit-identical to np.sum.
@@ -1138,10 +1151,10 @@ __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YS
 #pragma unroll
                         for (int k = 0; k < MO2_CH; k += 4) {
                             const int4 a = *reinterpret_cast<const int4*>(src.cf + h + c0 + k);
-                            g[k] = ((double)a.x / 1e6) * src.gen_scale;
-                            g[k + 1] = ((double)a.y / 1e6) * src.gen_scale;
-                            g[k + 2] = ((double)a.z / 1e6) * src.gen_scale;
-                            g[k + 3] = ((double)a.w / 1e6) * src.gen_scale;
+                            g[k] = cf_per_kw(a.x) * src.gen_scale;
+                            g[k + 1] = cf_per_kw(a.y) * src.gen_scale;
+                            g[k + 2] = cf_per_kw(a.z) * src.gen_scale;
+                            g[k + 3] = cf_per_kw(a.w) * src.gen_scale;
                         }
                     }
                 }
@@ -1203,10 +1216,10 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
                         for (int k = 0; k < 4; k++) g[k] = src.sysgen[(int64_t)(h + k) * src.sys_stride];
                     } else {
                         const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
-                        g[0] = ((double)cv.x / 1e6) * src.gen_scale;
-                        g[1] = ((double)cv.y / 1e6) * src.gen_scale;
-                        g[2] = ((double)cv.z / 1e6) * src.gen_scale;
-                        g[3] = ((double)cv.w / 1e6) * src.gen_scale;
+                        g[0] = cf_per_kw(cv.x) * src.gen_scale;
+                        g[1] = cf_per_kw(cv.y) * src.gen_scale;
+                        g[2] = cf_per_kw(cv.z) * src.gen_scale;
+                        g[3] = cf_per_kw(cv.w) * src.gen_scale;
                     }
                 }
                 if (src.ts) {
@@ -1307,10 +1320,10 @@ __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& sr
 #pragma unroll
                     for (int k = 0; k < 3; k++) {
                         const int4 cv = *reinterpret_cast<const int4*>(src.cf + h + 4 * k);
-                        g[4 * k] = ((double)cv.x / 1e6) * src.gen_scale;
-                        g[4 * k + 1] = ((double)cv.y / 1e6) * src.gen_scale;
-                        g[4 * k + 2] = ((double)cv.z / 1e6) * src.gen_scale;
-                        g[4 * k + 3] = ((double)cv.w / 1e6) * src.gen_scale;
+                        g[4 * k] = cf_per_kw(cv.x) * src.gen_scale;
+                        g[4 * k + 1] = cf_per_kw(cv.y) * src.gen_scale;
+                        g[4 * k + 2] = cf_per_kw(cv.z) * src.gen_scale;
+                        g[4 * k + 3] = cf_per_kw(cv.w) * src.gen_scale;
                     }
                 } else {
 #pragma unroll
@@ -1412,7 +1425,7 @@ __device__ bool yl_dc_build(const dgen_demand* D, const YSrc& src, double tlo, d
                             for (int k = 0; k < 4; k++) {
                                 if ((int)((pq >> (8 * k)) & 0xffu) != p) continue;
                                 const double L = (double)shv[k] * src.load_scale;
-                                const double gp = (double)cfv[k] / 1e6;
+                                const double gp = cf_per_kw(cfv[k]);
                                 if (pass == 0) {
                                     mL = L > mL ? L : mL;
                                     const double vlo = L - gp * tlo, vhi = L - gp * thi;
@@ -2520,8 +2533,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->nch[slot] = nch;
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK +
                        (size_t)(BLOCK / 64) * HB_DAY_BYTES;
-    // two agents per wave when every analysis period fits 32 lanes
-    const int lpa = (A->max_years >= 1 && A->max_years <= 32) ? 32 : WAVE;
+    // two agents per wave when every analysis period fits 32 lanes.  The
+    // demand-charge build runs one agent per wave: its two-agent instantiation
+    // (256 VGPRs + spills) returned wrong peaks, deterministically and
+    // build-dependent, while the one-agent build (224 VGPRs, no spills) of the
+    // same source matched the oracle -- see DESIGN.md section 3.
+    const int lpa = (!dc && A->max_years >= 1 && A->max_years <= 32) ? 32 : WAVE;
     const size_t ylds = ylds_bytes(lds_half(T->max_periods), lpa);
     const int apb = WAVE / lpa;   // agents per year-lane block
     hipStream_t s2 = c->s2;
@@ -2535,9 +2552,6 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         if (lpa == 32 && !dc)
             hipLaunchKernelGGL((k_size_w<32, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
                                nullptr);
-        else if (lpa == 32)
-            hipLaunchKernelGGL((k_size_w<32, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               c->dc_buf);
         else if (!dc)
             hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
                                nullptr);
@@ -2560,9 +2574,6 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipEventRecord(e[3], s2));
         if (lpa == 32 && !dc)
             hipLaunchKernelGGL((k_batt_finance_w<32, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
-                               n, ws, n_scratch, i0, i1);
-        else if (lpa == 32)
-            hipLaunchKernelGGL((k_batt_finance_w<32, true>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
                                n, ws, n_scratch, i0, i1);
         else if (!dc)
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O,
