@@ -498,9 +498,6 @@ __device__ __forceinline__ void st_f32x4(char* row, uint32_t off, const float (&
     const f32x4 v = {q[0], q[1], q[2], q[3]};
     asm volatile("global_store_dwordx4 %0, %1, %2 nt" :: "v"(off), "v"(v), "s"(row) : "memory");
 }
-__device__ __forceinline__ void st_f64(char* row, uint32_t off, double v) {
-    *reinterpret_cast<double*>(row + off) = v;
-}
 
 // One hour of the dispatch (same arithmetic as the oracle's branchy
 // orc_batt_dispatch, written without divergence): charge when the net load is
@@ -661,13 +658,17 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const int d_lo = c_month_start_day[m_lo];
     // hour rows: wave-uniform bases advanced per row; per-lane 32-bit byte
     // offsets (host guarantees n < 2^28, n_scratch < 2^28)
-    const uint32_t off8 = (uint32_t)(put_sys ? slot : 0) * 8u;
-    const size_t row8 = (size_t)n_scratch * 8u;
+    // system-output scratch plane in hour-quad tiles [2190][n_scratch][4] f64:
+    // a lane stores its 4 hours as 32 contiguous bytes, a reader loads them
+    // as two 16-B loads (sys_quad)
+    const size_t off32 = (size_t)(put_sys ? slot : 0) * 32u;
+    const size_t row32 = (size_t)n_scratch * 32u;
     char* const ob = reinterpret_cast<char*>(O.baseline);
     char* const op = reinterpret_cast<char*>(O.net_pvonly);
     char* const ow = reinterpret_cast<char*>(O.net_with_batt);
     char* const osc = reinterpret_cast<char*>(W.scratch);
-    size_t ho8 = (size_t)d_lo * 24 * row8;
+    size_t hq32 = (size_t)d_lo * 6 * row32;
+    double qs[4] = {0.0, 0.0, 0.0, 0.0};
     // hourly planes in hour-quad tiles (include/dgen_hip.h): (hour h, agent i)
     // at ((h / 4) * n + i) * 4 + h % 4, so a lane stores 16 B and a wave 1 KB
     // contiguous per plane every 4 hours (measured 29.3 -> 27.9 ms vs one
@@ -761,7 +762,15 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                         q16 += row16;
                     }
                 }
-                if (put_sys) st_f64(osc + ho8, off8, st.sys);   // plane [h][slot]
+                qs[hh & 3] = st.sys;
+                if ((hh & 3) == 3) {
+                    if (put_sys) {                              // tile [h / 4][slot][4]
+                        double2* q = reinterpret_cast<double2*>(osc + hq32 + off32);
+                        q[0] = make_double2(qs[0], qs[1]);
+                        q[1] = make_double2(qs[2], qs[3]);
+                    }
+                    hq32 += row32;
+                }
                 if (!mo2) {   // NEM energy bill from bins (demand charges also read the plane)
                     const int p = (int)((sched[hh >> 3] >> (8 * (hh & 7))) & 0xffu);
                     double2 b = bins[p * BLOCK];
@@ -769,7 +778,6 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     b.y += st.sys;
                     bins[p * BLOCK] = b;
                 }
-                ho8 += row8;
             }
             sched[0] = nsched[0]; sched[1] = nsched[1]; sched[2] = nsched[2];
         }
@@ -1077,6 +1085,14 @@ struct YSrc {
     double ts_mult;
 };
 
+// The 4 system-output values of hours h .. h + 3 (h % 4 == 0) from the
+// hour-quad scratch tiles (src.sysgen = scratch + 4 x slot, stride n_scratch).
+__device__ __forceinline__ void sys_quad(const YSrc& src, int h, double* g) {
+    const double2* q = reinterpret_cast<const double2*>(src.sysgen + (int64_t)(h >> 2) * src.sys_stride * 4);
+    const double2 a = q[0], b = q[1];
+    g[0] = a.x; g[1] = a.y; g[2] = b.x; g[3] = b.y;
+}
+
 // Month energy charge from register-held billed kWh (P <= PREG), the same
 // arithmetic and order as yl_month_charge.
 __device__ __forceinline__ double reg_month_charge(const dgen_tariff& t, int m, const double (&u)[PREG]) {
@@ -1146,7 +1162,7 @@ __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YS
                 if (with_gen) {
                     if (src.sysgen) {
 #pragma unroll
-                        for (int k = 0; k < MO2_CH; k++) g[k] = src.sysgen[(int64_t)(h + c0 + k) * src.sys_stride];
+                        for (int k = 0; k < MO2_CH; k += 4) sys_quad(src, h + c0 + k, g + k);
                     } else {
 #pragma unroll
                         for (int k = 0; k < MO2_CH; k += 4) {
@@ -1212,8 +1228,7 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
                 double g[4] = {0.0, 0.0, 0.0, 0.0}, tsv[4] = {0.0, 0.0, 0.0, 0.0};
                 if (with_gen) {
                     if (src.sysgen) {
-#pragma unroll
-                        for (int k = 0; k < 4; k++) g[k] = src.sysgen[(int64_t)(h + k) * src.sys_stride];
+                        sys_quad(src, h, g);
                     } else {
                         const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
                         g[0] = cf_per_kw(cv.x) * src.gen_scale;
@@ -1315,7 +1330,7 @@ __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& sr
                 }
                 if (with_gen && src.sysgen) {
 #pragma unroll
-                    for (int k = 0; k < 12; k++) g[k] = src.sysgen[(int64_t)(h + k) * src.sys_stride];
+                    for (int k = 0; k < 12; k += 4) sys_quad(src, h + k, g + k);
                 } else if (with_gen) {
 #pragma unroll
                     for (int k = 0; k < 3; k++) {
@@ -1891,7 +1906,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         src.gen_scale = 0.0;
         src.sys_stride = n_scratch;
         const int slot = A.scratch_slot[i];
-        src.sysgen = (slot >= 0) ? W.scratch + slot : nullptr;
+        src.sysgen = (slot >= 0) ? W.scratch + (int64_t)slot * 4 : nullptr;
         const int wr = A.wholesale_row[i];
         src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
         src.ts_mult = A.price_mult[i];
