@@ -1226,11 +1226,32 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
                 const uint32_t pq = *reinterpret_cast<const uint32_t*>(sched + c0);
                 const float shv[4] = {sv.x, sv.y, sv.z, sv.w};
                 double g[4] = {0.0, 0.0, 0.0, 0.0}, tsv[4] = {0.0, 0.0, 0.0, 0.0};
+                int4 cv = make_int4(0, 0, 0, 0);
+                if (with_gen && !src.sysgen) cv = *reinterpret_cast<const int4*>(src.cf + h);
+                if ((!with_gen || !src.sysgen) && (cv.x | cv.y | cv.z | cv.w) == 0) {
+                    // no PV in these 4 hours (night, or the no-system bill): the
+                    // import is the load itself (load - 0 * s == load) and a zero
+                    // load adds a signed zero to the export sum -- the general
+                    // path's result, without its generation / sell-rate work
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const double load = (double)shv[k] * src.load_scale;
+                        const int p = (int)((pq >> (8 * k)) & 0xffu);
+                        if (p != cur) {
+                            S.at(cur) = ci;
+                            S.at(half + cur) = ce;
+                            cur = p;
+                            ci = S.at(p);
+                            ce = S.at(half + p);
+                        }
+                        if (load > 0.0) ci += load;
+                    }
+                    continue;
+                }
                 if (with_gen) {
                     if (src.sysgen) {
                         sys_quad(src, h, g);
                     } else {
-                        const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
                         g[0] = cf_per_kw(cv.x) * src.gen_scale;
                         g[1] = cf_per_kw(cv.y) * src.gen_scale;
                         g[2] = cf_per_kw(cv.z) * src.gen_scale;
