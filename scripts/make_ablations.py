@@ -71,6 +71,11 @@ VARIANTS = {
                       "    double total = 0.0;\n#pragma unroll 2\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn")],
     "bill_unroll12": [("    double total = 0.0;\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn",
                        "    double total = 0.0;\n#pragma unroll\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn")],
+    # hourly-plane store cache policy (MI355X_MICROARCH.md: plain / sc0 / nt keep the
+    # line in the XCD's L2, sc1 / sc0 sc1 write through and drop it)
+    "st_sc1": [('global_store_dwordx4 %0, %1, %2 nt"', 'global_store_dwordx4 %0, %1, %2 sc1"')],
+    "st_sc0sc1": [('global_store_dwordx4 %0, %1, %2 nt"', 'global_store_dwordx4 %0, %1, %2 sc0 sc1"')],
+    "st_plain4": [('global_store_dwordx4 %0, %1, %2 nt"', 'global_store_dwordx4 %0, %1, %2"')],
     "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
                  "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
 }
