@@ -1760,9 +1760,12 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 // occupancy floor of 3 waves per SIMD (<= 168 VGPRs): the 32-lane variant
 // otherwise takes 181 and runs 2 (measured 23.3 -> 18.6 ms at 1M agents)
 // DC: demand charges billed (extension mode) -- a separate instantiation so
-// the reference mode's register allocation is untouched
+// the reference mode's register allocation is untouched.  The two-agent DC
+// build runs at 1 wave per SIMD: capped at 2 it spilled (156-180 B/lane) and
+// those builds returned wrong, build-dependent Brent results (DESIGN.md
+// section 3); with no scratch it matches the oracle.
 template <int LPA, bool DC>
-__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
+__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
          void* dcws) {
     const int lane = threadIdx.x;
@@ -2569,12 +2572,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->nch[slot] = nch;
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK +
                        (size_t)(BLOCK / 64) * HB_DAY_BYTES;
-    // two agents per wave when every analysis period fits 32 lanes.  The
-    // demand-charge build runs one agent per wave: its two-agent instantiation
-    // (256 VGPRs + spills) returned wrong peaks, deterministically and
-    // build-dependent, while the one-agent build (224 VGPRs, no spills) of the
-    // same source matched the oracle -- see DESIGN.md section 3.
-    const int lpa = (!dc && A->max_years >= 1 && A->max_years <= 32) ? 32 : WAVE;
+    // two agents per wave when every analysis period fits 32 lanes
+    const int lpa = (A->max_years >= 1 && A->max_years <= 32) ? 32 : WAVE;
     const size_t ylds = ylds_bytes(lds_half(T->max_periods), lpa);
     const int apb = WAVE / lpa;   // agents per year-lane block
     hipStream_t s2 = c->s2;
@@ -2588,6 +2587,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         if (lpa == 32 && !dc)
             hipLaunchKernelGGL((k_size_w<32, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
                                nullptr);
+        else if (lpa == 32)
+            hipLaunchKernelGGL((k_size_w<32, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
+                               c->dc_buf);
         else if (!dc)
             hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
                                nullptr);
@@ -2610,6 +2612,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipEventRecord(e[3], s2));
         if (lpa == 32 && !dc)
             hipLaunchKernelGGL((k_batt_finance_w<32, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
+                               n, ws, n_scratch, i0, i1);
+        else if (lpa == 32)
+            hipLaunchKernelGGL((k_batt_finance_w<32, true>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
                                n, ws, n_scratch, i0, i1);
         else if (!dc)
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O,
