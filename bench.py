@@ -170,14 +170,19 @@ def main():
             traffic = float(pm["k_hourly_batt"]["hbm_bytes_per_agent"]) * args.agents
         except Exception:
             traffic = None
+    n_launch = -(-12 // eng.hb_months) * eng.chunks
     roof = {"bound": "hbm", "kernel": "k_hourly_batt", "achieved": achieved, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": traffic, "algorithmic_bytes_per_launch": bytes_launch,
+            # traffic and algorithmic bytes per launch (the year's bytes split evenly
+            # over the month launches); the per-step totals beside them
+            "traffic": (traffic / n_launch) if traffic else None,
+            "algorithmic_bytes_per_launch": bytes_launch / n_launch,
+            "traffic_per_step": traffic, "algorithmic_bytes_per_step": bytes_launch,
             "kernel_ms": {"k_size": ms_size, "k_hourly_batt": ms_hourly, "k_batt_finance": ms_fin},
             "dominant_kernel": dom, "event_samples": cnt,
             # k_hourly_batt sweeps the year in month segments: kernel_ms is the
             # per-step sum over these launches (rocprof reports per launch)
-            "hourly_launches_per_step": -(-12 // eng.hb_months) * eng.chunks}
+            "hourly_launches_per_step": n_launch}
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
