@@ -45,6 +45,9 @@ constexpr int DCP = DGEN_DCP;
 constexpr int DCT = DGEN_DCT;
 constexpr int BLOCK = 128;   // threads per block for the per-agent kernels
 constexpr int HB_DAY_BYTES = 12 * 1024;   // k_hourly_batt day buffer per wave (LDS)
+// hourly-plane stores every k_hourly_batt<true> day issues after its next-day
+// DMA: 6 hour quads x 3 planes (the counted wait of the day pipeline)
+constexpr int HB_STORES_AFTER_DMA = (24 / 4) * 3;
 typedef __attribute__((address_space(3))) char* lds_ptr_t;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -274,9 +277,94 @@ __device__ __forceinline__ double np_sign(double v) {
 }
 
 // scipy 1.15.3 _minimize_scalar_bounded, op for op (maxfun 500).
-template <class Obj>
+//
+// LOCKSTEP (two agents per wave): the loop runs until BOTH agents have
+// converged, wave-uniformly; an agent that is done re-evaluates its last
+// point, which the objective makes idempotent (the sticky rate switch at the
+// same kW selects the tariff it already holds, and the same inputs give the
+// same per-lane results), and its search state is left untouched.  The
+// objective -- the expensive, register-heavy part -- then never runs with
+// the two agents' loop iterations out of step (see DESIGN.md section 3 on
+// the two-agent demand-charge build).
+template <bool LOCKSTEP = false, class Obj>
 __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, double xatol, int* nfev,
                                 double* x_last) {
+    if constexpr (LOCKSTEP) {
+        const double sqrt_eps = 1.4832396974191326e-08;     // sqrt(2.2e-16)
+        const double golden_mean = 0.3819660112501051;      // 0.5 * (3 - sqrt(5))
+        double a = x1, b = x2;
+        double fulc = a + golden_mean * (b - a);
+        double nfc = fulc, xf = fulc;
+        double rat = 0.0, e = 0.0;
+        double x = xf;
+        double fx = f(x);
+        *x_last = x;
+        int num = 1;
+        double ffulc = fx, fnfc = fx;
+        double xm = 0.5 * (a + b);
+        double tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+        double tol2 = 2.0 * tol1;
+        bool go = fabs(xf - xm) > (tol2 - 0.5 * (b - a));
+        while (__ballot(go) != 0ull) {
+            if (go) {
+                bool golden = true;
+                if (fabs(e) > tol1) {
+                    golden = false;
+                    double r = (xf - nfc) * (fx - ffulc);
+                    double q = (xf - fulc) * (fx - fnfc);
+                    double p = (xf - fulc) * q - (xf - nfc) * r;
+                    q = 2.0 * (q - r);
+                    if (q > 0.0) p = -p;
+                    q = fabs(q);
+                    r = e;
+                    e = rat;
+                    if ((fabs(p) < fabs(0.5 * q * r)) && (p > q * (a - xf)) && (p < q * (b - xf))) {
+                        rat = (p + 0.0) / q;
+                        x = xf + rat;
+                        if (((x - a) < tol2) || ((b - x) < tol2)) {
+                            double si = np_sign(xm - xf) + (((xm - xf) == 0.0) ? 1.0 : 0.0);
+                            rat = tol1 * si;
+                        }
+                    } else {
+                        golden = true;
+                    }
+                }
+                if (golden) {
+                    if (xf >= xm) e = a - xf; else e = b - xf;
+                    rat = golden_mean * e;
+                }
+                double si = np_sign(rat) + ((rat == 0.0) ? 1.0 : 0.0);
+                double ar = fabs(rat);
+                x = xf + si * (ar > tol1 ? ar : tol1);
+            }
+            const double xe = go ? x : *x_last;   // a converged agent repeats its last point
+            double fu = f(xe);
+            if (go) {
+                *x_last = x;
+                num += 1;
+                if (fu <= fx) {
+                    if (x >= xf) a = xf; else b = xf;
+                    fulc = nfc; ffulc = fnfc;
+                    nfc = xf; fnfc = fx;
+                    xf = x; fx = fu;
+                } else {
+                    if (x < xf) a = x; else b = x;
+                    if ((fu <= fnfc) || (nfc == xf)) {
+                        fulc = nfc; ffulc = fnfc;
+                        nfc = x; fnfc = fu;
+                    } else if ((fu <= ffulc) || (fulc == xf) || (fulc == nfc)) {
+                        fulc = x; ffulc = fu;
+                    }
+                }
+                xm = 0.5 * (a + b);
+                tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+                tol2 = 2.0 * tol1;
+                go = (num < 500) && (fabs(xf - xm) > (tol2 - 0.5 * (b - a)));
+            }
+        }
+        *nfev = num;
+        return xf;
+    }
     const double sqrt_eps = 1.4832396974191326e-08;     // sqrt(2.2e-16)
     const double golden_mean = 0.3819660112501051;      // 0.5 * (3 - sqrt(5))
     double a = x1, b = x2;
@@ -354,6 +442,7 @@ struct WsLayout {
     double2* LGb;     // [n][NBIN] (load, system) bins, battery case, final tariff (2 NBIN planes)
     double* otc_b;    // 1 plane: storage one-time charge
     double* scratch;  // [8760][n_scratch] battery system output (mo 2)
+    char* nb;         // [n_scratch][NB_BYTES] net-billing split records (k_size)
 };
 
 __host__ __device__ inline WsLayout ws_layout(void* base, int64_t n) {
@@ -365,6 +454,10 @@ __host__ __device__ inline WsLayout ws_layout(void* base, int64_t n) {
     w.otc_b = p; p += n;
     w.scratch = p;
     return w;
+}
+__host__ __device__ inline char* ws_nb(void* base, int64_t n, int64_t n_scratch) {
+    return reinterpret_cast<char*>(base) + sizeof(double) * ((size_t)4 * NBIN * (size_t)n + (size_t)n +
+                                                            (size_t)NH * (size_t)n_scratch);
 }
 
 // ---------------------------------------------------------------------------
@@ -681,13 +774,19 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // Software pipeline over days through LDS: the next day's raw profile
     // values (96 B of the shape row + 96 B of the cf row per lane) are DMA'd
     // global -> LDS (global_load_lds_dwordx4: no VGPRs held in flight) at the
-    // start of the current day, BEFORE the day's 72 hourly stores.  vmcnt is
+    // start of the current day, BEFORE the day's hourly stores.  vmcnt is
     // shared by loads and stores and retires in issue order, so at the next
-    // day start vmcnt(48) already implies the DMA landed while the last 48
-    // stores may still be in flight (a wait on a load issued after the stores
-    // would drain them all).  DMA and read-back are inline asm: the compiler
-    // would otherwise order every LDS access of the kernel (the bins) behind
-    // a vmcnt(0).  Per wave: 12 chunks x 64 lanes x 16 B = HB_DAY_BYTES.
+    // day start vmcnt(HB_STORES_AFTER_DMA) implies the DMA landed while the
+    // day's last stores may still be in flight: every day issues at least
+    // HB_STORES_AFTER_DMA = 6 hour quads x 3 planes asm stores after its DMA
+    // (plus 12 scratch stores with put_sys, which only make the wait
+    // stricter).  The day loop issues no compiler-visible load (the period
+    // schedule is loaded per month, below): the compiler's own waits count
+    // only the ops it sees, so a load pending in the loop would get a
+    // vmcnt(0) at its first use that drains every store of the day.  DMA and
+    // read-back are inline asm: the compiler would otherwise order every LDS
+    // access of the kernel (the bins) behind a vmcnt(0).  Per wave: 12 chunks
+    // x 64 lanes x 16 B = HB_DAY_BYTES.  (ISA check: DESIGN.md section 5.)
     const uint32_t dbase = (uint32_t)(size_t)(lds_ptr_t)(reinterpret_cast<char*>(dyn_lds) +
                            (size_t)16 * lds_half(T.max_periods) * BLOCK +
                            (size_t)(threadIdx.x / 64) * HB_DAY_BYTES);
@@ -700,14 +799,6 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             lds_dma16(cfp + dd * 24 + 4 * q, dbase_s + (6 + q) * 1024u);
         }
     };
-    // the day's period schedule (24 bytes, 8-aligned rows) in 3 registers,
-    // loaded one day ahead as well (issued before the day's stores)
-    uint64_t sched[3];
-    {
-        const uint64_t* sr = reinterpret_cast<const uint64_t*>(((d_lo % 7) >= 5) ? t.wkend[m_lo]
-                                                                             : t.wkday[m_lo]);
-        sched[0] = sr[0]; sched[1] = sr[1]; sched[2] = sr[2];
-    }
     // settle every load before the day loop: the waitcnt pass merges the
     // loop entry with the back edge, and a pending entry load would put a
     // vmcnt wait (which also drains the in-flight day DMA) into hour 0
@@ -717,14 +808,23 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     DayRaw r;
     for (int m = m_lo; m < m_hi; m++) {
         for (int p = 0; p < P; p++) bins[p * BLOCK] = make_double2(0.0, 0.0);
+        // the month's weekday / weekend period rows (24 bytes each, 8-aligned)
+        // in 6 registers, loaded once per month: the day loop below then
+        // issues no compiler-visible load (see the pipeline note above); the
+        // compiler's wait for these lands in the month's first hour
+        uint64_t swd[3], swe[3];
+        {
+            const uint64_t* a = reinterpret_cast<const uint64_t*>(t.wkday[m]);
+            const uint64_t* b = reinterpret_cast<const uint64_t*>(t.wkend[m]);
+            swd[0] = a[0]; swd[1] = a[1]; swd[2] = a[2];
+            swe[0] = b[0]; swe[1] = b[1]; swe[2] = b[2];
+        }
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
-            if (HOURLY && d > d_lo) day_read<48>(dlane, r);
+            if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA>(dlane, r);
             else day_read<0>(dlane, r);
-            const int dx = d < d_last ? d + 1 : d;
-            const int mx = dx < c_month_start_day[m + 1] ? m : (m < 11 ? m + 1 : 11);
-            const uint64_t* nsr =
-                reinterpret_cast<const uint64_t*>(((dx % 7) >= 5) ? t.wkend[mx] : t.wkday[mx]);
-            const uint64_t nsched[3] = {nsr[0], nsr[1], nsr[2]};
+            const bool wkend = (d % 7) >= 5;
+            const uint64_t sched[3] = {wkend ? swe[0] : swd[0], wkend ? swe[1] : swd[1],
+                                       wkend ? swe[2] : swd[2]};
             double target = 0.0;
             if (has_batt) {
                 // the day's deficits d_h = max(load_h - pv_h, 0), sorted; the raw
@@ -779,7 +879,6 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     bins[p * BLOCK] = b;
                 }
             }
-            sched[0] = nsched[0]; sched[1] = nsched[1]; sched[2] = nsched[2];
         }
         if (!mo2) {
             // agent-major (load, system) pairs: k_batt_finance's lanes read the
@@ -1525,6 +1624,195 @@ __device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& 
     return total;
 }
 
+// ---------------------------------------------------------------------------
+// Net-billing split (PV-only search, mo 2).  The hourly pass of yl_bill_mo2
+// bills max(L_h - g_h t, 0) as import and the rest as export, with t the
+// generation scale (kW' x the year's degradation factor).  The search only
+// evaluates t in [tlo, thi] (bracket x degradation range), and over that
+// interval most hours never change side: an hour whose import is positive at
+// both ends (beyond a 1e-10 relative slack that covers the rounding of the
+// per-hour product) imports at every evaluated t, one negative at both ends
+// always exports.  Their contributions are linear in t, so per (month,
+// period) the build keeps four sums -- import load and generation, export
+// generation x sell weight and load x sell weight -- and the M hours in
+// between as a list.  An evaluation then bills
+//     import_p = SA_L - (SA_g kW') s + sum over the period's M hours
+//     export_p = (SX_gw kW') s - SX_Lw + sum over the period's M hours
+// with the hourly pass's own per-hour arithmetic on the M hours: the same
+// quantities as the hourly pass up to rounding (re-associated sums), on
+// ~700 of 8760 hours for the synthetic CA population.  Month lane m builds
+// month m once per tariff; a month with more than NB_CAPM M hours sends the
+// agent back to the hourly pass.  Storage per scratch slot: NB_BYTES in the
+// caller's workspace.
+// ---------------------------------------------------------------------------
+constexpr int NB_CAPM = 192;
+constexpr size_t NB_SUMS_BYTES = (size_t)12 * MAXP * 4 * sizeof(double);
+constexpr size_t NB_BYTES = NB_SUMS_BYTES + 64 + (size_t)12 * NB_CAPM * sizeof(uint16_t);
+static_assert(NB_BYTES % 16 == 0, "per-slot net-billing records stay 16-B aligned");
+static_assert(NB_BYTES == DGEN_NB_BYTES, "include/dgen_hip.h DGEN_NB_BYTES");
+// an M entry: hour within the month (< 744) | period << 10
+constexpr int NB_HBITS = 10;
+
+struct NbRec {
+    double* sums;        // [12][MAXP][4]: SA_L, SA_g, SX_gw, SX_Lw
+    int* cnt;            // [12] M hours per month
+    uint16_t* ent;       // [12][NB_CAPM]
+};
+__device__ __forceinline__ NbRec nb_rec(char* p) {
+    NbRec r;
+    r.sums = reinterpret_cast<double*>(p);
+    r.cnt = reinterpret_cast<int*>(p + NB_SUMS_BYTES);
+    r.ent = reinterpret_cast<uint16_t*>(p + NB_SUMS_BYTES + 64);
+    return r;
+}
+
+// The sell weight of an exported kWh: the float32-rounded TS sell rate
+// (ff:756) when the reference enables it, else 1 (the period's sell column is
+// applied per month).
+__device__ __forceinline__ double nb_weight(const YSrc& src, int h) {
+    return src.ts ? (double)(float)(src.ts[h] * src.ts_mult) : 1.0;
+}
+
+// Month lane m < 12 of the segment builds month m (accumulators in its LDS
+// column, at(4 p + q), 4 P <= 4 half).  Returns true when every month's M
+// hours fit (segment-uniform).
+template <int LPA>
+__device__ bool yl_nb_build(const dgen_tariff& t, const YSrc& src, double tlo, double thi, char* nbp,
+                            const YLds& S, const Seg<LPA>& g) {
+    bool ok = true;
+    const int m = g.sl;
+    const NbRec R = nb_rec(nbp);
+    if (m < 12) {
+        const int P = t.P;
+        for (int k = 0; k < 4 * P; k++) S.at(k) = 0.0;
+        int n_m = 0;
+        const int h0m = c_month_start_day[m] * 24;
+        uint16_t* ent = R.ent + m * NB_CAPM;
+        for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
+            const uint8_t* sc = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
+#pragma unroll 1
+            for (int c0 = 0; c0 < 24; c0 += 4) {
+                const int h = d * 24 + c0;
+                const uint32_t pq = *reinterpret_cast<const uint32_t*>(sc + c0);
+                const float4 sv = *reinterpret_cast<const float4*>(src.shape + h);
+                const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
+                const float shv[4] = {sv.x, sv.y, sv.z, sv.w};
+                const int cfv[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int p = (int)((pq >> (8 * k)) & 0xffu);
+                    const double L = (double)shv[k] * src.load_scale;
+                    const double gk = cf_per_kw(cfv[k]);
+                    const double vlo = L - gk * tlo, vhi = L - gk * thi;
+                    const double slack = 1e-10 * (fabs(L) + fabs(gk) * thi);
+                    if (fmin(vlo, vhi) > slack) {               // imports at every t
+                        S.at(4 * p) += L;
+                        S.at(4 * p + 1) += gk;
+                    } else if (fmax(vlo, vhi) < -slack) {       // exports at every t
+                        const double w = nb_weight(src, h + k);
+                        S.at(4 * p + 2) += gk * w;
+                        S.at(4 * p + 3) += L * w;
+                    } else {
+                        if (n_m < NB_CAPM) ent[n_m] = (uint16_t)((p << NB_HBITS) | (h + k - h0m));
+                        n_m++;
+                    }
+                }
+            }
+        }
+        ok = n_m <= NB_CAPM;
+        R.cnt[m] = n_m;
+        for (int p = 0; p < P; p++)
+            for (int q = 0; q < 4; q++) R.sums[(m * MAXP + p) * 4 + q] = S.at(4 * p + q);
+    }
+    // hand-off to the other lanes through global memory, as yl_dc_build
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return g.first(!ok) < 0;
+}
+
+// Net-billing bill of the lane's year from the split (generation kW' =
+// src.gen_scale, degradation factor s): yl_bill_mo2's result up to the
+// rounding of the re-associated import / export sums.
+__device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& src, double s, char* nbp,
+                                             const YLds& S) {
+    const NbRec R = nb_rec(nbp);
+    const int P = t.P, half = S.half;
+    const double kws = src.gen_scale;
+    double total = 0.0;
+    for (int m = 0; m < 12; m++) {
+        for (int p = 0; p < P; p++) {
+            const double* q = R.sums + (m * MAXP + p) * 4;
+            S.at(p) = q[0] - (q[1] * kws) * s;
+            S.at(half + p) = (q[2] * kws) * s - q[3];
+        }
+        const int h0m = c_month_start_day[m] * 24;
+        const int n_m = R.cnt[m];
+        const uint16_t* ent = R.ent + m * NB_CAPM;
+        int cur = 0;
+        double ci = S.at(0), ce = S.at(half);
+#pragma unroll 1
+        for (int j = 0; j < n_m; j += 4) {
+            // four entries in one 8-B load, then their inputs together
+            const uint2 e2 = *reinterpret_cast<const uint2*>(ent + j);
+            const uint32_t ev[4] = {e2.x & 0xffffu, e2.x >> 16, e2.y & 0xffffu, e2.y >> 16};
+            float sh[4];
+            int32_t cf[4];
+            double tsv[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int hh = h0m + ((j + k < n_m) ? (int)(ev[k] & ((1u << NB_HBITS) - 1u)) : 0);
+                sh[k] = src.shape[hh];
+                cf[k] = src.cf[hh];
+                tsv[k] = src.ts ? src.ts[hh] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (j + k >= n_m) break;
+                const int p = (int)(ev[k] >> NB_HBITS);
+                const double load = (double)sh[k] * src.load_scale;
+                const double gg = cf_per_kw(cf[k]) * kws;
+                const double dd = load - gg * s;
+                if (p != cur) {
+                    S.at(cur) = ci;
+                    S.at(half + cur) = ce;
+                    cur = p;
+                    ci = S.at(p);
+                    ce = S.at(half + p);
+                }
+                if (dd > 0.0) {
+                    ci += dd;
+                } else {
+                    double e = -dd;
+                    if (src.ts) e *= (double)(float)(tsv[k] * src.ts_mult);
+                    ce += e;
+                }
+            }
+        }
+        S.at(cur) = ci;
+        S.at(half + cur) = ce;
+        double cr = 0.0;
+        for (int p = 0; p < P; p++) {
+            const double e = S.at(half + p);
+            cr += src.ts ? e : e * t.sell[p][0];
+        }
+        total += t.fixed + yl_month_charge(t, m, S, 0) - cr;
+    }
+    return total;
+}
+
+// Net-billing (mo 2) bill with no system: every hour imports its load, so the
+// (month, period) imports are the slot-sum load bins (yl_build_bins).
+__device__ __forceinline__ double yl_bill_mo2_nogen(const dgen_tariff& t, const YLds& S) {
+    const int P = t.P, half = S.half;
+    double total = 0.0;
+    for (int m = 0; m < 12; m++) {
+        for (int p = 0; p < P; p++) S.at(p) = S.L[m * half + p];
+        total += t.fixed + yl_month_charge(t, m, S, 0);
+    }
+    return total;
+}
+
 // bins of a tariff from a row's slot sums, one (month, period) cell per lane
 template <int LPA>
 __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
@@ -1667,6 +1955,8 @@ struct YCtx {
     bool dem_wo_pending;        // wo1 still lacks the new tariff's demand charge
     bool env_ok;                // the demand envelopes of the current tariff fit
     DcEnv env;                  // the agent's envelope storage
+    char* nb;                   // the agent's net-billing split record (or nullptr)
+    bool nb_ok;                 // the split of the current (mo 2) tariff fits
     double tlo, thi;            // generation-scale range of the search
     int sw_cnt;
     int tariff, switched, status;
@@ -1696,7 +1986,12 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);
     } else {
-        c.wo1 = yl_bill_mo2(t, c.src, 1.0, false, c.S);
+        // net billing: the no-system bill from the load bins, then the split
+        // of the search's hours for this tariff's periods
+        wave_lds_sync();
+        yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
+        c.wo1 = yl_bill_mo2_nogen(t, c.S);
+        c.nb_ok = c.nb && yl_nb_build(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g);
     }
     if constexpr (DC) {   // its no-system charge is added by the next objective
         c.dem = tariff_demand(c.dem_table, c.n_dem, true, t);
@@ -1726,7 +2021,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
         wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
     } else {
         c.src.gen_scale = kws;
-        wb = yl_bill_mo2(t, c.src, c.s_y, true, c.S);
+        wb = c.nb_ok ? yl_bill_nb(t, c.src, c.s_y, c.nb, c.S) : yl_bill_mo2(t, c.src, c.s_y, true, c.S);
     }
     if constexpr (DC) {
         if (c.dem) {
@@ -1767,7 +2062,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 template <int LPA, bool DC>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
-         void* dcws) {
+         void* dcws, char* nbws) {
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -1785,6 +2080,11 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.env.lines = nullptr;
     if constexpr (DC) {
         if (dcws) c.env = dc_env_at(dcws, i);
+    }
+    {
+        const int slot = A.scratch_slot[i];
+        c.nb = (nbws && slot >= 0) ? nbws + (size_t)slot * NB_BYTES : nullptr;
+        c.nb_ok = false;
     }
     c.sw_rows = T.switches + A.sw_solar_off[i];
     c.sw_cnt = A.sw_solar_cnt[i];
@@ -1839,7 +2139,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         }
         return;
     }
-    if constexpr (DC) {   // generation-scale range the search can evaluate (envelopes)
+    {   // generation-scale range the search can evaluate (envelopes, net-billing split)
         const int ln = (c.N >= 1 && c.N <= LPA) ? c.N - 1 : 0;
         const double sN = c.g.bcast(c.s_y, ln);
         const double s_lo = sN < 1.0 ? sN : 1.0, s_hi = sN > 1.0 ? sN : 1.0;
@@ -1849,7 +2149,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     yl_set_tariff<LPA, DC>(c, t0);
     int nfev = 0;
     double x_last = 0.0;
-    double kw_star = brent_bounded(
+    double kw_star = brent_bounded<(LPA < WAVE)>(
         [&](double x) __attribute__((always_inline)) {
             return yl_objective<LPA, DC>(c, x);
         },
@@ -2489,7 +2789,8 @@ int32_t dgen_prep_cfs(dgen_ctx* c, const int32_t* cfs, int64_t n_rows, double* r
 
 size_t dgen_workspace_bytes(int64_t n, int64_t n_scratch) {
     if (n < 0 || n_scratch < 0) return 0;
-    return sizeof(double) * ((size_t)4 * NBIN * (size_t)n + (size_t)n + (size_t)NH * (size_t)n_scratch);
+    return sizeof(double) * ((size_t)4 * NBIN * (size_t)n + (size_t)n + (size_t)NH * (size_t)n_scratch) +
+           NB_BYTES * (size_t)n_scratch;
 }
 
 int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A,
@@ -2523,8 +2824,11 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         set_err("dgen_size_agents: hourly planes must be all set or all NULL");
         return DGEN_E_ARG;
     }
-    if (n >= ((int64_t)1 << 29) || n_scratch >= ((int64_t)1 << 28)) {
-        set_err("dgen_size_agents: batch too large (n < 2^29, n_scratch < 2^28 per call)");
+    // k_hourly_batt forms a 32-bit per-lane byte offset i x 16 into the hourly tiles
+    if (n >= ((int64_t)1 << 29) || n_scratch >= ((int64_t)1 << 28) ||
+        (hourly && n >= ((int64_t)1 << 28))) {
+        set_err("dgen_size_agents: batch too large (n < 2^29, n < 2^28 with hourly planes, "
+                "n_scratch < 2^28 per call)");
         return DGEN_E_ARG;
     }
     if (!ws || ws_bytes < dgen_workspace_bytes(n, n_scratch)) {
@@ -2577,6 +2881,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     const size_t ylds = ylds_bytes(lds_half(T->max_periods), lpa);
     const int apb = WAVE / lpa;   // agents per year-lane block
     hipStream_t s2 = c->s2;
+    char* const nbws = n_scratch > 0 ? ws_nb(ws, n, n_scratch) : nullptr;
     HIP_TRY(hipEventRecord(c->fork, s));
     HIP_TRY(hipStreamWaitEvent(s2, c->fork, 0));
     for (int j = 0; j < nch; j++) {
@@ -2586,16 +2891,16 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         const dim3 ygrid((unsigned)((m + apb - 1) / apb));
         if (lpa == 32 && !dc)
             hipLaunchKernelGGL((k_size_w<32, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               nullptr);
+                               nullptr, nbws);
         else if (lpa == 32)
             hipLaunchKernelGGL((k_size_w<32, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               c->dc_buf);
+                               c->dc_buf, nbws);
         else if (!dc)
             hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               nullptr);
+                               nullptr, nbws);
         else
             hipLaunchKernelGGL((k_size_w<WAVE, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               c->dc_buf);
+                               c->dc_buf, nbws);
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
         HIP_TRY(hipEventRecord(e[2], s2));

@@ -244,7 +244,11 @@ int32_t dgen_prep_shapes(dgen_ctx* ctx, const float* shapes, int64_t n_rows, dou
 int32_t dgen_prep_cfs(dgen_ctx* ctx, const int32_t* cfs, int64_t n_rows, double* row_naep,
                       double* row_slots, void* stream);
 
-/* Workspace bytes for a batch of n agents with n_scratch mo=2 scratch slots. */
+/* Workspace bytes for a batch of n agents with n_scratch scratch slots (agents
+ * whose tariffs can bill net or carry demand charges):
+ *   8 x (4 x 144 n + n + 8760 n_scratch)   bins, carries, battery output plane
+ *   + DGEN_NB_BYTES x n_scratch             net-billing split records (k_size)  */
+#define DGEN_NB_BYTES 9280
 size_t dgen_workspace_bytes(int64_t n, int64_t n_scratch);
 
 /* Size a batch: Brent over PV kW with 25-year bills + cash flow per

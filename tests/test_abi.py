@@ -40,7 +40,8 @@ def test_library_exports_every_declared_symbol():
 def test_workspace_bytes_formula():
     L = _lib.load()
     assert L.dgen_workspace_bytes(1000, 0) == 8 * (4 * 144 * 1000 + 1000)
-    assert L.dgen_workspace_bytes(10, 3) == 8 * (4 * 144 * 10 + 10 + 8760 * 3)
+    nb = int(re.search(r"#define DGEN_NB_BYTES\s+(\d+)", open(HEADER).read()).group(1))
+    assert L.dgen_workspace_bytes(10, 3) == 8 * (4 * 144 * 10 + 10 + 8760 * 3) + nb * 3
     assert L.dgen_workspace_bytes(-1, 0) == 0
 
 
