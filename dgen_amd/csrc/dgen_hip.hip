@@ -277,94 +277,9 @@ __device__ __forceinline__ double np_sign(double v) {
 }
 
 // scipy 1.15.3 _minimize_scalar_bounded, op for op (maxfun 500).
-//
-// LOCKSTEP (two agents per wave): the loop runs until BOTH agents have
-// converged, wave-uniformly; an agent that is done re-evaluates its last
-// point, which the objective makes idempotent (the sticky rate switch at the
-// same kW selects the tariff it already holds, and the same inputs give the
-// same per-lane results), and its search state is left untouched.  The
-// objective -- the expensive, register-heavy part -- then never runs with
-// the two agents' loop iterations out of step (see DESIGN.md section 3 on
-// the two-agent demand-charge build).
-template <bool LOCKSTEP = false, class Obj>
+template <class Obj>
 __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, double xatol, int* nfev,
                                 double* x_last) {
-    if constexpr (LOCKSTEP) {
-        const double sqrt_eps = 1.4832396974191326e-08;     // sqrt(2.2e-16)
-        const double golden_mean = 0.3819660112501051;      // 0.5 * (3 - sqrt(5))
-        double a = x1, b = x2;
-        double fulc = a + golden_mean * (b - a);
-        double nfc = fulc, xf = fulc;
-        double rat = 0.0, e = 0.0;
-        double x = xf;
-        double fx = f(x);
-        *x_last = x;
-        int num = 1;
-        double ffulc = fx, fnfc = fx;
-        double xm = 0.5 * (a + b);
-        double tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
-        double tol2 = 2.0 * tol1;
-        bool go = fabs(xf - xm) > (tol2 - 0.5 * (b - a));
-        while (__ballot(go) != 0ull) {
-            if (go) {
-                bool golden = true;
-                if (fabs(e) > tol1) {
-                    golden = false;
-                    double r = (xf - nfc) * (fx - ffulc);
-                    double q = (xf - fulc) * (fx - fnfc);
-                    double p = (xf - fulc) * q - (xf - nfc) * r;
-                    q = 2.0 * (q - r);
-                    if (q > 0.0) p = -p;
-                    q = fabs(q);
-                    r = e;
-                    e = rat;
-                    if ((fabs(p) < fabs(0.5 * q * r)) && (p > q * (a - xf)) && (p < q * (b - xf))) {
-                        rat = (p + 0.0) / q;
-                        x = xf + rat;
-                        if (((x - a) < tol2) || ((b - x) < tol2)) {
-                            double si = np_sign(xm - xf) + (((xm - xf) == 0.0) ? 1.0 : 0.0);
-                            rat = tol1 * si;
-                        }
-                    } else {
-                        golden = true;
-                    }
-                }
-                if (golden) {
-                    if (xf >= xm) e = a - xf; else e = b - xf;
-                    rat = golden_mean * e;
-                }
-                double si = np_sign(rat) + ((rat == 0.0) ? 1.0 : 0.0);
-                double ar = fabs(rat);
-                x = xf + si * (ar > tol1 ? ar : tol1);
-            }
-            const double xe = go ? x : *x_last;   // a converged agent repeats its last point
-            double fu = f(xe);
-            if (go) {
-                *x_last = x;
-                num += 1;
-                if (fu <= fx) {
-                    if (x >= xf) a = xf; else b = xf;
-                    fulc = nfc; ffulc = fnfc;
-                    nfc = xf; fnfc = fx;
-                    xf = x; fx = fu;
-                } else {
-                    if (x < xf) a = x; else b = x;
-                    if ((fu <= fnfc) || (nfc == xf)) {
-                        fulc = nfc; ffulc = fnfc;
-                        nfc = x; fnfc = fu;
-                    } else if ((fu <= ffulc) || (fulc == xf) || (fulc == nfc)) {
-                        fulc = x; ffulc = fu;
-                    }
-                }
-                xm = 0.5 * (a + b);
-                tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
-                tol2 = 2.0 * tol1;
-                go = (num < 500) && (fabs(xf - xm) > (tol2 - 0.5 * (b - a)));
-            }
-        }
-        *nfev = num;
-        return xf;
-    }
     const double sqrt_eps = 1.4832396974191326e-08;     // sqrt(2.2e-16)
     const double golden_mean = 0.3819660112501051;      // 0.5 * (3 - sqrt(5))
     double a = x1, b = x2;
@@ -1695,14 +1610,21 @@ __device__ bool yl_nb_build(const dgen_tariff& t, const YSrc& src, double tlo, d
                 const int h = d * 24 + c0;
                 const uint32_t pq = *reinterpret_cast<const uint32_t*>(sc + c0);
                 const float4 sv = *reinterpret_cast<const float4*>(src.shape + h);
-                const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
                 const float shv[4] = {sv.x, sv.y, sv.z, sv.w};
-                const int cfv[4] = {cv.x, cv.y, cv.z, cv.w};
+                // per-kW PV output (search) or the battery case's system output
+                double gq[4];
+                if (src.sysgen) {
+                    sys_quad(src, h, gq);
+                } else {
+                    const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
+                    gq[0] = cf_per_kw(cv.x); gq[1] = cf_per_kw(cv.y);
+                    gq[2] = cf_per_kw(cv.z); gq[3] = cf_per_kw(cv.w);
+                }
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
                     const int p = (int)((pq >> (8 * k)) & 0xffu);
                     const double L = (double)shv[k] * src.load_scale;
-                    const double gk = cf_per_kw(cfv[k]);
+                    const double gk = gq[k];
                     const double vlo = L - gk * tlo, vhi = L - gk * thi;
                     const double slack = 1e-10 * (fabs(L) + fabs(gk) * thi);
                     if (fmin(vlo, vhi) > slack) {               // imports at every t
@@ -1732,8 +1654,9 @@ __device__ bool yl_nb_build(const dgen_tariff& t, const YSrc& src, double tlo, d
 }
 
 // Net-billing bill of the lane's year from the split (generation kW' =
-// src.gen_scale, degradation factor s): yl_bill_mo2's result up to the
-// rounding of the re-associated import / export sums.
+// src.gen_scale, degradation factor s; battery case: src.sysgen with
+// gen_scale 1): yl_bill_mo2's result up to the rounding of the re-associated
+// import / export sums.
 __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& src, double s, char* nbp,
                                              const YLds& S) {
     const NbRec R = nb_rec(nbp);
@@ -1757,13 +1680,15 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
             const uint2 e2 = *reinterpret_cast<const uint2*>(ent + j);
             const uint32_t ev[4] = {e2.x & 0xffffu, e2.x >> 16, e2.y & 0xffffu, e2.y >> 16};
             float sh[4];
-            int32_t cf[4];
-            double tsv[4];
+            double gv[4], tsv[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 const int hh = h0m + ((j + k < n_m) ? (int)(ev[k] & ((1u << NB_HBITS) - 1u)) : 0);
                 sh[k] = src.shape[hh];
-                cf[k] = src.cf[hh];
+                // the hourly pass's generation term: cf / 1e6 x kW', or the
+                // battery case's system output as is
+                gv[k] = src.sysgen ? src.sysgen[(int64_t)(hh >> 2) * src.sys_stride * 4 + (hh & 3)]
+                                   : (double)src.cf[hh];
                 tsv[k] = src.ts ? src.ts[hh] : 0.0;
             }
 #pragma unroll
@@ -1771,7 +1696,7 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
                 if (j + k >= n_m) break;
                 const int p = (int)(ev[k] >> NB_HBITS);
                 const double load = (double)sh[k] * src.load_scale;
-                const double gg = cf_per_kw(cf[k]) * kws;
+                const double gg = src.sysgen ? gv[k] : cf_per_kw((int32_t)gv[k]) * kws;
                 const double dd = load - gg * s;
                 if (p != cur) {
                     S.at(cur) = ci;
@@ -2149,7 +2074,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     yl_set_tariff<LPA, DC>(c, t0);
     int nfev = 0;
     double x_last = 0.0;
-    double kw_star = brent_bounded<(LPA < WAVE)>(
+    double kw_star = brent_bounded(
         [&](double x) __attribute__((always_inline)) {
             return yl_objective<LPA, DC>(c, x);
         },
@@ -2191,7 +2116,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
 template <int LPA, bool DC>
 __global__ void __launch_bounds__(WAVE)
 k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-                 int64_t n_scratch, int64_t i0, int64_t i1) {
+                 int64_t n_scratch, int64_t i0, int64_t i1, char* nbws) {
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -2248,8 +2173,29 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         wo1 = same_tariff ? O.first_without[i] : yl_bill_nem(t, S, 0.0, cfg.nm_yearend_sell_rate);
         wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
     } else {
-        wo1 = same_tariff ? O.first_without[i] : yl_bill_net(t, src, 1.0, false, S);
-        wb = yl_bill_net(t, src, s_y, true, S);
+        if (same_tariff) {
+            wo1 = O.first_without[i];
+        } else {   // k_size's no-system form: the slot-sum load bins
+            const int lr = A.load_row[i], cr = A.cf_row[i];
+            yl_build_bins(t, T.shape_slots + (int64_t)lr * NSLOT, T.cf_slots + (int64_t)cr * NSLOT,
+                          src.load_scale, S, g);
+            wo1 = yl_bill_mo2_nogen(t, S);
+        }
+        // the split of the battery-case hours over the lanes' degradation
+        // factors [s_lo, s_hi] (the agent's net-billing record is free: its
+        // search finished in k_size)
+        const int slot = A.scratch_slot[i];
+        bool nb_ok = false;
+        if (nbws && slot >= 0 && src.sysgen) {
+            const int ln = (N >= 1 && N <= LPA) ? N - 1 : 0;
+            const double sN = g.bcast(s_y, ln);
+            const double s_lo = sN < 1.0 ? sN : 1.0, s_hi = sN > 1.0 ? sN : 1.0;
+            src.gen_scale = 1.0;
+            char* nbp = nbws + (size_t)slot * NB_BYTES;
+            nb_ok = yl_nb_build(t, src, s_lo, s_hi, nbp, S, g);
+            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S);
+        }
+        if (!nb_ok) wb = yl_bill_net(t, src, s_y, true, S);
     }
     if (DC && dem) {   // k_size's first_without already carries the no-system demand charge
         for (int pass = same_tariff ? 1 : 0; pass < 2; pass++) {
@@ -2917,16 +2863,16 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipEventRecord(e[3], s2));
         if (lpa == 32 && !dc)
             hipLaunchKernelGGL((k_batt_finance_w<32, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
-                               n, ws, n_scratch, i0, i1);
+                               n, ws, n_scratch, i0, i1, nbws);
         else if (lpa == 32)
             hipLaunchKernelGGL((k_batt_finance_w<32, true>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
-                               n, ws, n_scratch, i0, i1);
+                               n, ws, n_scratch, i0, i1, nbws);
         else if (!dc)
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O,
-                               c->cfg, n, ws, n_scratch, i0, i1);
+                               c->cfg, n, ws, n_scratch, i0, i1, nbws);
         else
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, true>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O,
-                               c->cfg, n, ws, n_scratch, i0, i1);
+                               c->cfg, n, ws, n_scratch, i0, i1, nbws);
         HIP_TRY(hipEventRecord(e[4], s2));
     }
     HIP_TRY(hipEventRecord(c->join, s2));
