@@ -30,15 +30,53 @@ sys.path.insert(0, REPO)
 METRIC = "agents sized/sec (8760-h bill+NPV) at 1/2/4/8 GPU; % HBM roofline"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md chip table (spec)
 NH = 8760
-# algorithmic bytes per agent of k_hourly_batt: read the agent's
-# load-shape row (f32) and cf row (i32), write baseline / PV-only / with-battery
-# hourly planes (f32), plus the bins and scalars it reads / writes
-BYTES_HOURLY = NH * 4 * 2 + NH * 4 * 3 + 2 * 144 * 8 + 16 * 8
-# k_size: row slot sums for the agent (load + cf, f64) + 4 yearly planes x 51 x 8 B
-# + the bins it builds (2 x 12 P x 8 B, P<=12) + ~24 scalars in/out
-BYTES_SIZE = 576 * 8 * 2 + 4 * 51 * 8 + 2 * 144 * 8 + 24 * 8
-# k_batt_finance: battery bins (2 x 144 x 8) + 3 yearly planes + scalars
-BYTES_FIN = 2 * 144 * 8 + 3 * 51 * 8 + 24 * 8
+ROW_BYTES = NH * 4              # one f32 load-shape row or one i32 cf row
+PLANE_BYTES = NH * 4            # one f32 hourly output plane per agent
+SYS_BYTES = NH * 8              # the battery case's f64 system-output plane per agent
+NB_BYTES = 9280                 # net-billing split record per scratch slot (DGEN_NB_BYTES)
+
+
+def algorithmic_bytes(cols, hourly: bool, battery: bool):
+    """ALGORITHMIC bytes per step of each sizing kernel for this population
+    (DESIGN.md section 5): what the algorithm must read and write once,
+    whatever the caches serve.
+      k_size          576 (month, daytype, hour) slot sums of both profile rows
+                      (f64) + ~24 scalars + 4 yearly output arrays of N+1 f64;
+                      agents that bill hourly imports (net billing / demand
+                      charges, the scratch-slot agents) also read both profile
+                      rows once (the split / envelope build) and write the
+                      split record
+      k_hourly_batt   both profile rows + the (month, period) bins + scalars,
+                      the three f32 hourly planes when requested, and the f64
+                      system-output plane of the scratch-slot agents
+      k_batt_finance  the bins + scalars + 3 yearly arrays; scratch-slot agents
+                      read the system-output plane and the load-shape row"""
+    n = len(cols["load_kwh"])
+    yearly = 8.0 * (np.asarray(cols["econ_life"], np.int64) + 1).sum()
+    nh = int((np.asarray(cols["scratch_slot"]) >= 0).sum())
+    k_size = n * (2 * 576 * 8 + 24 * 8) + 4 * yearly + nh * (2 * ROW_BYTES + NB_BYTES)
+    k_hourly = n * (2 * ROW_BYTES + 2 * 144 * 8 + 16 * 8)
+    if hourly:
+        k_hourly += n * 3 * PLANE_BYTES
+    if battery:
+        k_hourly += nh * SYS_BYTES
+    k_fin = (n * (2 * 144 * 8 + 24 * 8) + 3 * yearly + nh * (SYS_BYTES + ROW_BYTES)) if battery else 0.0
+    return {"k_size": float(k_size), "k_hourly_batt": float(k_hourly), "k_batt_finance": float(k_fin)}
+
+
+def pmc_traffic(pmc_dir: str, workload: str):
+    """Per-agent HBM bytes per kernel measured by rocprofv3 PMC on THIS workload
+    (profiles/pmc/<workload>.json, written by scripts/pmc_summary.py), or {}."""
+    path = os.path.join(pmc_dir, f"{workload}.json")
+    if not os.path.exists(path):
+        return {}, None
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+        return {k.replace("_w", "") if k.endswith("_w") else k: float(v["hbm_bytes_per_agent"])
+                for k, v in pm.items() if "hbm_bytes_per_agent" in v}, os.path.relpath(path, REPO)
+    except Exception:
+        return {}, None
 
 
 def parse():
@@ -60,7 +98,10 @@ def parse():
                     help="profile_order grouping: by (cf_row, load_row) or (load_row, cf_row)")
     ap.add_argument("--caller-order", action="store_true",
                     help="keep the generator's agent order on device (no profile_order grouping)")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_bytes_per_agent.json"))
+    ap.add_argument("--no-batt", action="store_true",
+                    help="PV-only variant: no PV+battery forward run (SURVEY 8(d)); the reference always runs it")
+    ap.add_argument("--pmc-dir", default=os.path.join(REPO, "profiles", "pmc"),
+                    help="per-workload PMC summaries (traffic field); none -> traffic null")
     return ap.parse_args()
 
 
@@ -101,6 +142,28 @@ def cpu_baseline(pop, seconds: float, threads: int):
                       f"oracle/orc.c full per-agent driver, OpenMP x{threads}, {el:.1f} s"}
 
 
+def timed_region(step, steps: int, sync, dist_mod=None, device=None) -> float:
+    """The contract's timed region: barrier + device sync on both sides of
+    exactly `steps` calls of `step`, then the MAX over ranks (one all-reduce;
+    gloo on CPU in tests/test_dist.py, RCCL on GPU tensors here)."""
+    if dist_mod is not None:
+        dist_mod.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist_mod is not None:
+        dist_mod.barrier()
+    el = time.perf_counter() - t0
+    if dist_mod is not None:
+        import torch
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist_mod.all_reduce(t, op=dist_mod.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -121,6 +184,8 @@ def main():
         eng.set_pipeline(args.chunks)
     if args.hb_months is not None:
         eng.set_hourly_segment(args.hb_months)
+    if args.no_batt:
+        eng.set_battery(False)
     eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     eng.set_tariffs(pop.tariffs, pop.demand)
     eng.set_switches(pop.switches)
@@ -135,20 +200,8 @@ def main():
     torch.cuda.synchronize()
     eng.kernel_times()                      # drop warmup events
 
-    if ws > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.size(batch, out, c_out)
-    torch.cuda.synchronize()
-    if ws > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if ws > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=eng.dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = timed_region(lambda: eng.size(batch, out, c_out), args.steps, torch.cuda.synchronize,
+                      dist if ws > 1 else None, eng.dev)
     ms_size, ms_hourly, ms_fin, cnt = eng.kernel_times()
 
     st = out["status"].cpu().numpy()
@@ -156,33 +209,33 @@ def main():
     total_agents = args.agents * ws * args.steps
     value = total_agents / el
 
-    kern = {"k_size": (ms_size, BYTES_SIZE), "k_hourly_batt": (ms_hourly, BYTES_HOURLY),
-            "k_batt_finance": (ms_fin, BYTES_FIN)}
-    dom = max(kern, key=lambda k: kern[k][0])
-    hb_ms = ms_hourly
-    bytes_launch = BYTES_HOURLY * args.agents if not args.no_hourly else (NH * 8 + 2 * 144 * 8) * args.agents
-    achieved = bytes_launch / (hb_ms * 1e-3) / 1e9 if hb_ms > 0 else None
-    traffic = None
-    if os.path.exists(args.pmc):
-        try:
-            with open(args.pmc) as f:
-                pm = json.load(f)
-            traffic = float(pm["k_hourly_batt"]["hbm_bytes_per_agent"]) * args.agents
-        except Exception:
-            traffic = None
-    n_launch = -(-12 // eng.hb_months) * eng.chunks
-    roof = {"bound": "hbm", "kernel": "k_hourly_batt", "achieved": achieved, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            # traffic and algorithmic bytes per launch (the year's bytes split evenly
-            # over the month launches); the per-step totals beside them
-            "traffic": (traffic / n_launch) if traffic else None,
-            "algorithmic_bytes_per_launch": bytes_launch / n_launch,
-            "traffic_per_step": traffic, "algorithmic_bytes_per_step": bytes_launch,
-            "kernel_ms": {"k_size": ms_size, "k_hourly_batt": ms_hourly, "k_batt_finance": ms_fin},
-            "dominant_kernel": dom, "event_samples": cnt,
-            # k_hourly_batt sweeps the year in month segments: kernel_ms is the
-            # per-step sum over these launches (rocprof reports per launch)
-            "hourly_launches_per_step": n_launch}
+    nbytes = algorithmic_bytes(pop.cols, not args.no_hourly, not args.no_batt)
+    traffic_pa, traffic_src = pmc_traffic(args.pmc_dir, args.config)
+    # launches per step: k_hourly_batt sweeps the year in month-segment launches
+    # per pipeline chunk; the year-lane kernels launch once per chunk
+    launches = {"k_size": eng.chunks, "k_hourly_batt": -(-12 // eng.hb_months) * eng.chunks,
+                "k_batt_finance": eng.chunks if not args.no_batt else 0}
+    kms = {"k_size": ms_size, "k_hourly_batt": ms_hourly, "k_batt_finance": ms_fin}
+    per_kernel = {}
+    for k, t in kms.items():
+        gbs = nbytes[k] / (t * 1e-3) / 1e9 if t > 0 else None
+        per_kernel[k] = {"ms_per_step": t, "launches_per_step": launches[k],
+                         "algorithmic_bytes_per_step": nbytes[k], "achieved_gbs": gbs,
+                         "hbm_frac": (gbs / HBM_PEAK_GBS) if gbs else None,
+                         "traffic_per_step": (traffic_pa[k] * args.agents) if k in traffic_pa else None}
+    dom = max(kms, key=lambda k: kms[k])
+    d = per_kernel[dom]
+    nl = max(launches[dom], 1)
+    roof = {"bound": "hbm", "kernel": dom, "achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": d["hbm_frac"],
+            # per launch, like rocprof's per-dispatch durations (bytes / launches)
+            "traffic": (d["traffic_per_step"] / nl) if d["traffic_per_step"] is not None else None,
+            "algorithmic_bytes_per_launch": nbytes[dom] / nl, "launches_per_step": nl,
+            "kernel_ms": kms, "per_kernel": per_kernel, "dominant_kernel": dom, "event_samples": cnt,
+            "traffic_source": traffic_src if dom in traffic_pa else None,
+            "note": ("k_hourly_batt streams its rows and planes: HBM is its roofline" if dom == "k_hourly_batt"
+                     else f"{dom} is fp64-VALU / latency bound (the year lanes re-bill per evaluation): "
+                          "its HBM fraction is reported for completeness, not as its bound")}
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
@@ -202,6 +255,7 @@ def main():
                        "global_agents": args.agents * ws,
                        "hourly_outputs": not args.no_hourly,
                        "demand_charges": not pop.skip_demand_charges,
+                       "battery_run": not args.no_batt,
                        "pipeline_chunks": eng.chunks, "hourly_months_per_launch": eng.hb_months,
                        "device_order": "caller" if args.caller_order else
                        ("profile (cf_row, load_row)" if args.order_major == "cf" else "profile (load_row, cf_row)"),

@@ -29,8 +29,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--agents", type=int, default=1_000_000, help="agents per GPU")
+    ap.add_argument("--config", default="national_mixed",
+                    help="national_mixed (C5) or de_res (C1: Delaware residential, one GPU)")
     ap.add_argument("--first-year", type=int, default=2026)
+    ap.add_argument("--step", type=int, default=1,
+                    help="years between model years (C1: 2; the Bass step is teq + 2 either way, "
+                         "diffusion_functions_elec.py:285)")
     ap.add_argument("--years", type=int, default=25, help="timed model years (2026-2050)")
+    ap.add_argument("--no-batt", action="store_true", help="PV-only variant (no PV+battery forward run)")
     ap.add_argument("--warmup", type=int, default=1, help="untimed model years, then reset")
     ap.add_argument("--hourly-chunk", type=int, default=None,
                     help="re-size chunks of this many agents for the state export")
@@ -46,12 +52,16 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from dgen_amd.engine import Engine
     from dgen_amd.synth import make_population
+    from dgen_amd.synth import STATES
     from dgen_amd.year_loop import LoopTables, YearLoop, loop_agents, rank_states
 
     t_setup = time.perf_counter()
-    pop = make_population("national_mixed", args.agents, seed=20260000 + 5 + 7919 * rank,
-                          state_pool=rank_states(rank, ws))
+    cnum = 1 if args.config == "de_res" else 5
+    pool = [STATES.index("DE")] if args.config == "de_res" else rank_states(rank, ws)
+    pop = make_population(args.config, args.agents, seed=20260000 + cnum + 7919 * rank, state_pool=pool)
     eng = Engine(local if ws > 1 else 0)
+    if args.no_batt:
+        eng.set_battery(False)
     eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     eng.set_tariffs(pop.tariffs)
     eng.set_switches(pop.switches)
@@ -61,10 +71,10 @@ def main():
     del pop
     setup_s = time.perf_counter() - t_setup
     for k in range(args.warmup):
-        loop.run_year(args.first_year + k)
+        loop.run_year(args.first_year + k * args.step)
     loop.reset()
     eng.kernel_times()
-    years = list(range(args.first_year, args.first_year + args.years))
+    years = list(range(args.first_year, args.first_year + args.years * args.step, args.step))
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -89,7 +99,9 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic national population (numpy PCG64; synthetic Bass / max-market-share "
                     "/ attachment tables; no DB offline)",
-            "config": {"workload": "national_loop", "agents_per_gpu": args.agents,
+            "config": {"workload": "national_loop" if args.config == "national_mixed" else f"{args.config}_loop",
+                       "population": args.config, "year_step": args.step, "battery_run": not args.no_batt,
+                       "agents_per_gpu": args.agents,
                        "global_agents": args.agents * ws, "years": [years[0], years[-1]],
                        "state_export": not args.no_export, "hourly_chunk": args.hourly_chunk,
                        "parallelism": f"dp{ws} (whole states per rank; one all-reduce per year)"},

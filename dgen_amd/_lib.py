@@ -99,7 +99,7 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
-ABI_VERSION = 3   # include/dgen_hip.h DGEN_ABI_VERSION
+ABI_VERSION = 4   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
 
@@ -107,8 +107,8 @@ EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
     "dgen_kernel_times", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
-    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
-    "dgen_finance_series",
+    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
+    "dgen_finance_series", "dgen_year_inputs", "dgen_initial_market_shares",
 ]
 
 
@@ -156,6 +156,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.dgen_finance_series.argtypes = [_vp, ctypes.POINTER(Outputs), _vp, _i64, _vp, _vp]
     L.dgen_set_hourly_segment.restype = _i32
     L.dgen_set_hourly_segment.argtypes = [_vp, _i32]
+    L.dgen_set_battery.restype = _i32
+    L.dgen_set_battery.argtypes = [_vp, _i32]
     L.dgen_segment_sums.restype = _i32
     L.dgen_segment_sums.argtypes = [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _vp, _i64, _vp, _vp]
     if L.dgen_abi_version() != ABI_VERSION:

@@ -607,7 +607,7 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 template <bool HOURLY>
 __global__ void __launch_bounds__(BLOCK, 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-              int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi) {
+              int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on) {
     // agents [i0, i1) of a batch of n (row stride of every plane stays n),
     // months [m_lo, m_hi) of the year: the year is swept in month segments,
     // one launch each, so that every resident wave works on the same weeks
@@ -633,8 +633,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
 
     // battery sizing at kW* (ff:140-147) and the storage rate switch (ff:167-175)
     double desired_kwh = kw_star / 0.8, desired_kw = desired_kwh / 2.0;
-    double bank, power;
-    batt_size(desired_kw, desired_kwh, is_res ? 240.0 : 500.0, cfg, &bank, &power);
+    double bank = 0.0, power = 0.0;
+    if (batt_on) batt_size(desired_kw, desired_kwh, is_res ? 240.0 : 500.0, cfg, &bank, &power);
     int tariff = O.tariff_final[i];
     int switched = O.switched[i];
     double otc = 0.0;
@@ -652,9 +652,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // the battery-case bill reads the hourly system output for net billing and
     // for demand charges (both need hourly imports, not bins)
     const bool need_sys = mo2 || tariff_demand(T, cfg, t) != nullptr;
-    const bool put_sys = need_sys && slot >= 0;
+    const bool put_sys = need_sys && slot >= 0 && batt_on;
     int status = O.status[i] | t.flags;
-    if (need_sys && slot < 0) status |= DGEN_ST_SCRATCH;
+    if (need_sys && slot < 0 && batt_on) status |= DGEN_ST_SCRATCH;
 
     const double inv_eta_in = 1.0 / cfg.batt_eta_in;
     const double in_per_bank = bank > 0.0 ? cfg.batt_eta_in / bank : 0.0;
@@ -814,6 +814,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     O.capacity_factor[i] = naep / 8760.0;
     O.batt_kw[i] = has_batt ? power : 0.0;
     O.batt_kwh[i] = bank;
+    if (!batt_on) O.npv_pv_batt[i] = NAN;   // k_batt_finance does not run
     // battery run on the PV run's tariff: k_batt_finance reuses its no-system
     // bill (same load, same tariff -> the same bill, as in the oracle)
     W.aux[i] = (tariff != O.tariff_final[i]) ? 1.0 : 0.0;
@@ -2572,6 +2573,117 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
 }
 
 // ---------------------------------------------------------------------------
+// Per-year agent attributes: the elec.apply_* left merges as
+// gathers from host-compiled per-year tables (include/dgen_hip.h
+// dgen_year_inputs); thread per agent.  apply_load_growth (elec.py:398-411):
+// residential agents scale their per-customer load, the others their
+// customer count; every agent its load in bin.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double yt_get(const double* tab, int64_t n_rows, int ncol, int32_t k, int c) {
+    return (k >= 0 && k < n_rows) ? tab[(int64_t)k * ncol + c] : NAN;
+}
+__device__ __forceinline__ int32_t yt_int(double v) {   // NaN (merge miss) -> -1
+    return (v == v) ? (int32_t)v : -1;
+}
+
+__global__ void k_year_inputs(dgen_year_keys K, dgen_year_tables T, dgen_year_out O, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t ks = K.k_sector[i], kc = K.k_sector_county[i], kt = K.k_state_sector[i];
+    auto S = [&](int c) { return yt_get(T.by_sector, T.n_sector, DGEN_YS_COLS, ks, c); };
+    auto C = [&](int c) { return yt_get(T.by_sector_county, T.n_sector_county, DGEN_YC_COLS, kc, c); };
+    const double mult = C(DGEN_YC_LOAD_MULT);
+    const bool res = K.is_res[i] != 0;
+    const double l0 = K.load_kwh_initial[i], c0 = K.customers_initial[i];
+    O.load_kwh[i] = res ? l0 * mult : l0;
+    O.customers_in_bin[i] = res ? c0 : c0 * mult;
+    O.load_kwh_in_bin[i] = K.load_in_bin_initial[i] * mult;
+    O.price_mult[i] = C(DGEN_YC_PRICE_MULT);
+    O.escalator[i] = C(DGEN_YC_ESCALATOR);
+    O.inflation[i] = T.inflation_rate;
+    O.capex[i] = S(DGEN_YS_CAPEX);
+    O.capex_combined[i] = S(DGEN_YS_CAPEX_COMBINED);
+    O.batt_capex_kwh[i] = S(DGEN_YS_BATT_CAPEX_KWH);
+    O.pv_deg[i] = S(DGEN_YS_PV_DEG);
+    O.itc_frac[i] = S(DGEN_YS_ITC);
+    O.econ_life[i] = yt_int(S(DGEN_YS_ECON_LIFE));
+    O.loan_term[i] = yt_int(S(DGEN_YS_LOAN_TERM));
+    O.down_payment[i] = S(DGEN_YS_DOWN_PAYMENT);
+    O.real_discount[i] = S(DGEN_YS_REAL_DISCOUNT);
+    O.tax_rate[i] = S(DGEN_YS_TAX_RATE);
+    O.vor[i] = yt_get(T.by_state_sector, T.n_state_sector, 1, kt, 0);
+    if (O.wholesale_row) {
+        const int32_t kk = K.k_county[i];
+        O.wholesale_row[i] = (T.wholesale_row && kk >= 0 && kk < T.n_county) ? T.wholesale_row[kk] : -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// First-year market seeding (elec.estimate_initial_market_shares,
+// elec.py:701-765).  Block per (state, sector, tech) group: lane 0 runs
+// pandas' group_sum over the group's rows in frame order (Kahan-compensated,
+// NaN skipped and not counted, a NaN compensation reset to 0 -- pandas
+// _libs/groupby.pyx group_sum), then the block writes every member's columns.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_initial_shares(dgen_init_in in, dgen_init_out out, const int64_t* __restrict__ idx,
+                 const int64_t* __restrict__ seg_off, const double* __restrict__ caps, int64_t n_seg) {
+    __shared__ double s_sum;
+    __shared__ int64_t s_cnt;
+    const int64_t g = blockIdx.x;
+    if (g >= n_seg) return;
+    const int64_t lo = seg_off[g], hi = seg_off[g + 1];
+    if (threadIdx.x == 0) {
+        double sum = 0.0, comp = 0.0;
+        int64_t cnt = 0;
+        for (int64_t r = lo; r < hi; r++) {
+            const double v = in.developable_agent_weight[idx[r]];
+            if (v != v) continue;
+            cnt++;
+            const double y = v - comp;
+            const double t = sum + y;
+            comp = (t - sum) - y;
+            if (comp != comp) comp = 0.0;
+            sum = t;
+        }
+        s_sum = sum;
+        s_cnt = cnt;
+        out.developable_customers_in_state[g] = sum;
+        out.agent_count[g] = cnt;
+    }
+    __syncthreads();
+    const double dev = s_sum;
+    const double cntd = (double)s_cnt;
+    const double* cp = caps + g * 5;
+    const double sys_mw = cp[0], batt_mw = cp[1], batt_mwh = cp[2], pv_n = cp[3], batt_n = cp[4];
+    auto z = [](double v) { return (v == v) ? v : 0.0; };    // fillna(0)
+    for (int64_t r = lo + threadIdx.x; r < hi; r += blockDim.x) {
+        const int64_t i = idx[r];
+        const double w = in.developable_agent_weight[i];
+        const double portion = (dev > 0.0) ? w / dev : 1.0 / cntd;
+        const double adopt = portion * pv_n;
+        const double skc = (portion * sys_mw) * 1000.;
+        const double bkw = (portion * batt_mw) * 1000.0;
+        const double bkwh = (portion * batt_mwh) * 1000.0;
+        const double ms = (w == 0.0) ? 0.0 : adopt / w;
+        const double mv = in.system_capex_per_kw[i] * skc;
+        out.adopters_cum_last_year[i] = z(adopt);
+        out.system_kw_cum_last_year[i] = z(skc);
+        out.batt_kw_cum_last_year[i] = z(bkw);
+        out.batt_kwh_cum_last_year[i] = z(bkwh);
+        out.market_share_last_year[i] = z(ms);
+        out.market_value_last_year[i] = z(mv);
+        out.initial_number_of_adopters[i] = z(adopt);
+        out.initial_pv_kw[i] = z(skc);
+        out.initial_batt_kw[i] = z(bkw);
+        out.initial_batt_kwh[i] = z(bkwh);
+        out.initial_market_share[i] = z(ms);
+        out.initial_market_value[i] = 0.0;
+        (void)batt_n;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Finance-series export: finance_series_export._norm25 over the
 // six 26-long yearly arrays of every agent, finance_series_export.py:9-20 --
 // first 25 entries, zero past the agent's list length (N + 1), non-finite -> 0.
@@ -2612,6 +2724,7 @@ struct dgen_ctx {
     hipStream_t s2;    // hourly + finance stream of the chunk pipeline
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
+    int battery;       // PV+battery forward run (dgen_set_battery)
     int head;          // next ring slot to record
     int pending;       // recorded, not yet folded
     double sum_ms[3];
@@ -2666,6 +2779,7 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     c->head = 0; c->pending = 0; c->count = 0;
     c->chunks = DGEN_DEFAULT_CHUNKS;
     c->hb_months = DGEN_DEFAULT_HOURLY_MONTHS;
+    c->battery = 1;
     c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
@@ -2855,13 +2969,15 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
             if (hourly)
                 hipLaunchKernelGGL(k_hourly_batt<true>, grid, block, lds, s2, *T, *A, *O, c->cfg, n,
-                                   ws, n_scratch, i0, i1, m0, m1);
+                                   ws, n_scratch, i0, i1, m0, m1, c->battery);
             else
                 hipLaunchKernelGGL(k_hourly_batt<false>, grid, block, lds, s2, *T, *A, *O, c->cfg, n,
-                                   ws, n_scratch, i0, i1, m0, m1);
+                                   ws, n_scratch, i0, i1, m0, m1, c->battery);
         }
         HIP_TRY(hipEventRecord(e[3], s2));
-        if (lpa == 32 && !dc)
+        if (!c->battery)
+            ;   // PV-only variant: no battery-case bill / cash flow
+        else if (lpa == 32 && !dc)
             hipLaunchKernelGGL((k_batt_finance_w<32, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
                                n, ws, n_scratch, i0, i1, nbws);
         else if (lpa == 32)
@@ -2887,6 +3003,15 @@ int32_t dgen_set_hourly_segment(dgen_ctx* c, int32_t months) {
         return DGEN_E_ARG;
     }
     c->hb_months = months;
+    return DGEN_OK;
+}
+
+int32_t dgen_set_battery(dgen_ctx* c, int32_t on) {
+    if (!c || (on != 0 && on != 1)) {
+        set_err("dgen_set_battery: on must be 0 or 1");
+        return DGEN_E_ARG;
+    }
+    c->battery = on;
     return DGEN_OK;
 }
 
@@ -3054,6 +3179,53 @@ int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
         hipLaunchKernelGGL(k_state_hourly<double>, grid, dim3(256), 0, (hipStream_t)stream,
                            (const double*)baseline, (const double*)pvonly, (const double*)with_batt,
                            w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_year_inputs(dgen_ctx* c, const dgen_year_keys* K, const dgen_year_tables* T,
+                         const dgen_year_out* O, int64_t n, void* stream) {
+    if (!c || !K || !T || !O || n < 0) { set_err("dgen_year_inputs: bad argument"); return DGEN_E_ARG; }
+    if (n == 0) return DGEN_OK;
+    const void* req[] = {K->k_sector, K->k_sector_county, K->k_state_sector, K->is_res, K->load_kwh_initial,
+                         K->customers_initial, K->load_in_bin_initial, O->load_kwh, O->price_mult,
+                         O->escalator, O->inflation, O->pv_deg, O->capex, O->capex_combined,
+                         O->batt_capex_kwh, O->itc_frac, O->down_payment, O->real_discount, O->tax_rate,
+                         O->vor, O->econ_life, O->loan_term, O->customers_in_bin, O->load_kwh_in_bin};
+    for (const void* p : req)
+        if (!p) { set_err("dgen_year_inputs: missing column"); return DGEN_E_ARG; }
+    if ((T->n_sector > 0 && !T->by_sector) || (T->n_sector_county > 0 && !T->by_sector_county) ||
+        (T->n_state_sector > 0 && !T->by_state_sector) || (O->wholesale_row && !K->k_county)) {
+        set_err("dgen_year_inputs: missing table");
+        return DGEN_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_year_inputs, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       *K, *T, *O, n);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_initial_market_shares(dgen_ctx* c, const dgen_init_in* in, const dgen_init_out* out,
+                                   const int64_t* idx, const int64_t* seg_off, const double* caps,
+                                   int64_t n_seg, void* stream) {
+    if (!c || !in || !out || !idx || !seg_off || !caps || n_seg < 0) {
+        set_err("dgen_initial_market_shares: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n_seg == 0) return DGEN_OK;
+    const void* req[] = {in->developable_agent_weight, in->system_capex_per_kw, out->adopters_cum_last_year,
+                         out->system_kw_cum_last_year, out->batt_kw_cum_last_year, out->batt_kwh_cum_last_year,
+                         out->market_share_last_year, out->market_value_last_year,
+                         out->initial_number_of_adopters, out->initial_pv_kw, out->initial_batt_kw,
+                         out->initial_batt_kwh, out->initial_market_share, out->initial_market_value,
+                         out->developable_customers_in_state, out->agent_count};
+    for (const void* p : req)
+        if (!p) { set_err("dgen_initial_market_shares: missing column"); return DGEN_E_ARG; }
+    if (n_seg > 0x7fffffff) { set_err("dgen_initial_market_shares: too many groups"); return DGEN_E_ARG; }
+    HIP_TRY(hipSetDevice(c->device));
+    hipLaunchKernelGGL(k_initial_shares, dim3((unsigned)n_seg), dim3(256), 0, (hipStream_t)stream, *in, *out,
+                       idx, seg_off, caps, n_seg);
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
 }

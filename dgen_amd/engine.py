@@ -74,6 +74,7 @@ class Engine:
         self.tables = _lib.Tables()
         self.chunks = _lib.DEFAULT_CHUNKS
         self.hb_months = _lib.DEFAULT_HOURLY_MONTHS
+        self.battery = True
         self._keep: Dict[str, object] = {}
 
     # ------------------------------------------------------------------ utils
@@ -272,6 +273,12 @@ class Engine:
         """Months per k_hourly_batt launch (dgen_set_hourly_segment)."""
         _lib.check(self.lib.dgen_set_hourly_segment(self.ctx, int(months)), "dgen_set_hourly_segment")
         self.hb_months = int(months)
+
+    def set_battery(self, on: bool):
+        """PV+battery forward run on (the reference, ff:479) or off (the PV-only
+        variant, dgen_set_battery)."""
+        _lib.check(self.lib.dgen_set_battery(self.ctx, int(bool(on))), "dgen_set_battery")
+        self.battery = bool(on)
 
     def kernel_times(self):
         """Average per-launch device time (ms) of the three sizing kernels over

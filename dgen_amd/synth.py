@@ -47,6 +47,7 @@ class Population:
     config: str
     state_ix: Optional[np.ndarray] = None   # int16 index into STATES per agent
     demand: Optional[np.ndarray] = None     # DEMAND_DTYPE (demand-charge configs)
+    county_ix: Optional[np.ndarray] = None  # int32 county per agent (wholesale row of non-CA agents)
 
     @property
     def skip_demand_charges(self) -> int:
@@ -271,4 +272,18 @@ def make_population(config: str, n_agents: int, seed: Optional[int] = None,
     return Population(shapes=shapes, cfs=cfs, wholesale=wholesale, tariffs=tariffs,
                       switches=switches, cols=cols, n_scratch=n_scratch, config=config,
                       state_ix=state_ix.astype(np.int16),
-                      demand=tt.demand_array() if metering == "nem_dc" else None)
+                      demand=tt.demand_array() if metering == "nem_dc" else None,
+                      county_ix=county)
+
+
+def subset(pop: Population, idx) -> Population:
+    """The agents `idx` of a population (same profile / tariff / switch
+    tables), scratch slots re-assigned: e.g. one rank's states of a national
+    population (year_loop.rank_states)."""
+    idx = np.asarray(idx, np.int64)
+    cols = {k: np.asarray(v)[idx].copy() for k, v in pop.cols.items()}
+    n_scratch = assign_scratch(cols, pop.tariffs, pop.switches)
+    pick = lambda a: None if a is None else np.asarray(a)[idx].copy()
+    return Population(shapes=pop.shapes, cfs=pop.cfs, wholesale=pop.wholesale, tariffs=pop.tariffs,
+                      switches=pop.switches, cols=cols, n_scratch=n_scratch, config=pop.config,
+                      state_ix=pick(pop.state_ix), demand=pop.demand, county_ix=pick(pop.county_ix))

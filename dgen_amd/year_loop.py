@@ -4,11 +4,16 @@ The reference's year loop (`dgen_model.py:245-462`) restricted to the hot path
 and the steps that consume it, kept resident on the GPU from one model year to
 the next:
 
-    per-year inputs      elec.apply_* merges (elec.py:29-409) -> synthetic
-                         trajectories applied to the resident SoA columns
-                         (capex / battery capex learning, load growth, price
-                         multiplier); the agent frame is reset to its base
-                         columns every year, dgen_model.py:245-247
+    per-year inputs      elec.apply_* merges (elec.py:29-409, dgen_model.py:252-292)
+                         -> dgen_year_inputs: per-year tables compiled on the
+                         host (dgen_amd.market.YearTables), gathered into the
+                         resident SoA columns (prices, financing, ITC,
+                         degradation, escalator, load growth, VOR); the frame
+                         is rebuilt from its base columns every year
+                         (dgen_model.py:245-247)
+    first-year market    elec.estimate_initial_market_shares (elec.py:701-765,
+                         dgen_model.py:390-393) -> dgen_initial_market_shares
+                         from the state starting capacities
     sizing               size_chunk -> dgen_size_agents (dgen_model.py:309-384)
     max market share     calc_max_market_share (ff:1264-1310) -> k_max_market_share
     diffusion            calc_diffusion_solar (diffusion_functions_elec.py:24-156)
@@ -34,10 +39,11 @@ year.  Nothing here runs on the CPU except index bookkeeping done once.
 
 Synthetic stand-ins (the DB tables are not available offline): Bass
 parameters per (state, sector), the max-market-share curves, storage
-attachment rates per state, customers per agent and the developable fraction
-(`LoopTables.synthetic`).  First model year: the reference seeds the market
-from observed state capacities (elec.py:701-765, DB); here the market starts
-empty (market share, adopters, value and capacities 0).
+attachment rates per state, customers per agent, the per-year input tables
+(built from the 2026 rows of the reference's input CSVs with learning /
+growth trajectories) and the state starting capacities
+(`LoopTables.synthetic`).  The developable weight is the agent's customers
+in bin, as calculate_developable_customers_and_load sets it (elec.py:414-423).
 """
 from __future__ import annotations
 
@@ -60,9 +66,7 @@ from .synth import STATES
 
 SECTORS = ("res", "com")
 TOTAL_COLS = ["system_kw_cum", "batt_kw_cum", "batt_kwh_cum", "number_of_adopters", "n_agents"]
-# per-year synthetic trajectories relative to the first model year
-TRAJ = {"capex": -0.020, "capex_combined": -0.020, "batt_capex_kwh": -0.030,
-        "load_kwh": 0.010, "price_mult": 0.005}
+LOOP_YEARS = (2022, 2050)       # the years the synthetic input tables cover
 
 
 def rank_states(rank: int, world: int, n_states: int = len(STATES)) -> np.ndarray:
@@ -94,9 +98,77 @@ class LoopTables:
     bass: pd.DataFrame
     mms_df: pd.DataFrame
     attach_rate: np.ndarray                  # [n_states]
+    inputs: Dict[str, pd.DataFrame] = field(default_factory=dict)   # market.YearTables roles
+    inflation_rate: float = 0.025
+    caps: Optional[pd.DataFrame] = None      # state starting capacities (elec.py:621-652)
 
     @staticmethod
-    def synthetic(seed: int = 20260105) -> "LoopTables":
+    def synthetic_inputs(rng, n_counties: int = 3100):
+        """Per-year input tables in the reference's formats (market.YearTables
+        roles), from the 2026 rows of its CSVs (capex
+        pv_price_atb23_mid.csv:14, battery pv_plus_batt_prices_FY23_mid.csv:14,
+        financing_atb_FY23.csv:14, degradation pv_tech_performance_defaultFY19
+        .csv:14) with learning / growth trajectories; ITC steps down after
+        2032 as the federal schedule does."""
+        years = np.arange(LOOP_YEARS[0], LOOP_YEARS[1] + 1)
+        k = (years - 2026).astype(np.float64)
+        sec = list(SECTORS)
+        capex = {"res": 4637.5, "com": 1672.9}
+        comb = {"res": 4500.0, "com": 1600.0}
+        batt = {"res": 431.0, "com": 197.3}
+        pv_price = pd.DataFrame([{"year": int(y), "sector_abbr": s, "system_capex_per_kw": capex[s] * 0.98 ** kk}
+                                 for y, kk in zip(years, k) for s in sec])
+        pvb = pd.DataFrame([{"year": int(y), "sector_abbr": s, "system_capex_per_kw": comb[s] * 0.98 ** kk,
+                             "batt_capex_per_kwh": batt[s] * 0.97 ** kk} for y, kk in zip(years, k) for s in sec])
+        pv_tech = pd.DataFrame([{"year": int(y), "sector_abbr": s, "pv_degradation_factor": 0.005}
+                                for y in years for s in sec])
+        itc = pd.DataFrame([{"year": int(y), "tech": "solar", "sector_abbr": s,
+                             "itc_fraction_of_capex": 0.3 if y <= 2032 else (0.26 if y == 2033 else
+                                                                            (0.22 if y == 2034 else 0.0))}
+                            for y in years for s in sec])
+        fin = pd.DataFrame([{"year": int(y), "sector_abbr": s, "economic_lifetime_yrs": 25,
+                             "loan_term_yrs": 20 if s == "res" else 30,
+                             "down_payment_fraction": 0.3 if s == "res" else 1.0,
+                             "real_discount_rate": 0.05 if s == "res" else 0.0378, "tax_rate": 0.2574}
+                            for y in years for s in sec])
+        cty = np.arange(n_counties)
+        rows_lg, rows_ep = [], []
+        for s in sec:
+            g = rng.uniform(0.5, 1.5, n_counties)
+            base = rng.uniform(0.9, 1.1, n_counties)
+            drift = rng.uniform(-0.01, 0.015, n_counties)
+            for y, kk in zip(years, k):
+                rows_lg.append(pd.DataFrame({"year": int(y), "sector_abbr": s, "county_id": cty,
+                                             "load_multiplier": 1.0 + 0.01 * kk * g}))
+                rows_ep.append(pd.DataFrame({"year": int(y), "sector_abbr": s, "county_id": cty,
+                                             "elec_price_multiplier": base * (1.0 + drift) ** kk}))
+        vor = pd.DataFrame([{"state_abbr": st, "sector_abbr": s,
+                             "value_of_resiliency_usd": float(rng.uniform(0, 300)) if rng.random() < 0.2 else 0.0}
+                            for st in STATES for s in sec])
+        return {"load_growth": pd.concat(rows_lg, ignore_index=True),
+                "elec_price": pd.concat(rows_ep, ignore_index=True), "pv_tech": pv_tech,
+                "pv_price": pv_price, "pv_plus_batt_price": pvb, "vor": vor, "financing": fin, "itc": itc}
+
+    @staticmethod
+    def synthetic_caps(rng):
+        """State starting capacities (the state_starting_capacities_to_model
+        table's shape, elec.py:621-652): PV and storage MW / MWh / system
+        counts per (state, sector); a few states without a row."""
+        rows = []
+        for i, st in enumerate(STATES):
+            for s in SECTORS:
+                if i % 17 == 5:
+                    continue
+                mw = float(rng.uniform(5, 2500 if s == "res" else 1500))
+                rows.append({"state_abbr": st, "sector_abbr": s, "system_mw": mw,
+                             "batt_mw": mw * float(rng.uniform(0.0, 0.08)),
+                             "batt_mwh": mw * float(rng.uniform(0.0, 0.3)),
+                             "pv_systems_count": mw * 1000.0 / (7.0 if s == "res" else 120.0),
+                             "batt_systems_count": mw * float(rng.uniform(0, 30))})
+        return pd.DataFrame(rows)
+
+    @staticmethod
+    def synthetic(seed: int = 20260105, n_counties: int = 3100) -> "LoopTables":
         rng = np.random.default_rng(seed)
         rows = []
         for s in STATES:
@@ -116,24 +188,28 @@ class LoopTables:
                 recs.append({"payback_period": float(p), "sector_abbr": sec,
                              "max_market_share": float(v), "metric": "payback_period",
                              "source": "synthetic", "business_model": "host_owned"})
-        return LoopTables(bass=bass, mms_df=pd.DataFrame(recs),
-                          attach_rate=rng.uniform(0.05, 0.35, len(STATES)))
+        attach = rng.uniform(0.05, 0.35, len(STATES))
+        irng = np.random.default_rng(seed + 1)
+        return LoopTables(bass=bass, mms_df=pd.DataFrame(recs), attach_rate=attach,
+                          inputs=LoopTables.synthetic_inputs(irng, n_counties),
+                          caps=LoopTables.synthetic_caps(irng))
 
 
 def loop_agents(pop, agent_id0: int = 0, seed: int = 20260205) -> Dict[str, np.ndarray]:
     """Per-agent columns of the diffusion / attachment steps for a synthetic
-    population (caller order): agent_id, state, sector, customers_in_bin,
-    developable_agent_weight (= customers x developable fraction,
-    elec.calculate_developable_customers_and_load)."""
+    population (caller order): agent_id, state, sector, county,
+    customers_in_bin (the initial customers; apply_load_growth scales the
+    non-residential ones per year)."""
     n = len(pop.cols["load_kwh"])
     rng = np.random.default_rng(seed + int(agent_id0))
     is_res = (np.asarray(pop.cols["flags"]) & 1).astype(bool)
     cust = np.where(is_res, rng.lognormal(np.log(400.0), 0.5, n), rng.lognormal(np.log(40.0), 0.5, n))
-    frac = rng.uniform(0.5, 0.9, n)
+    county = (np.asarray(pop.county_ix, np.int64) if pop.county_ix is not None
+              else np.zeros(n, np.int64))
     return {"agent_id": np.arange(agent_id0, agent_id0 + n, dtype=np.int64),
             "state": np.asarray(pop.state_ix, dtype=np.int64),
             "sector": np.where(is_res, 0, 1).astype(np.int64),
-            "customers_in_bin": cust, "developable_agent_weight": cust * frac}
+            "county": county, "customers_in_bin": cust}
 
 
 @dataclass
@@ -172,7 +248,20 @@ class YearLoop:
         self.batch = engine.upload_agents(pop.cols, n_scratch=pop.n_scratch, order=perm)
         dev = engine.dev
         f64 = lambda a: torch.as_tensor(np.asarray(a, np.float64)[perm], device=dev)
-        self.base = {k: self.batch.cols[k].clone() for k in TRAJ}
+        # per-year inputs: key codes in device order, initial load / customers
+        from .market import YearInputs, YearTables
+        frame = pd.DataFrame({"state_abbr": [STATES[s] for s in agents["state"][perm]],
+                              "sector_abbr": [SECTORS[c] for c in agents["sector"][perm]],
+                              "county_id": np.asarray(agents["county"], np.int64)[perm]})
+        self.inv = inv
+        self.caller_frame = (list(frame["state_abbr"].to_numpy()[inv]), list(frame["sector_abbr"].to_numpy()[inv]))
+        self.year_tables = YearTables(frame, tables.inputs, tables.inflation_rate)
+        load0 = np.asarray(pop.cols["load_kwh"], np.float64)[perm]
+        cust0 = np.asarray(agents["customers_in_bin"], np.float64)[perm]
+        self.year_inputs = YearInputs(engine, self.year_tables, load0, cust0, load0 * cust0)
+        self.loop_cols = {k: torch.empty(n, dtype=torch.float64, device=engine.dev)
+                          for k in ("customers_in_bin", "load_kwh_in_bin")}
+        self.frame = frame
         st, sec = agents["state"], agents["sector"]
         self.state_caller = st
         # per-agent Bass parameters (the reference's merge on (state, sector), :41-44)
@@ -183,8 +272,10 @@ class YearLoop:
         tab = b.reindex(list(uk.keys()))
         self.bass = {c: f64(tab[src].to_numpy(np.float64)[kix]) for c, src in
                      (("bass_p", "bass_param_p"), ("bass_q", "bass_param_q"), ("teq_yr1", "teq_yr1"))}
-        self.cust = f64(agents["customers_in_bin"])
-        self.dev_w = f64(agents["developable_agent_weight"])
+        # customers_in_bin / developable weight: the year's loop column
+        # (calculate_developable_customers_and_load, elec.py:414-423)
+        self.cust = self.loop_cols["customers_in_bin"]
+        self.dev_w = self.cust
         # max market share table, curve row per agent (sector)
         mt, rows, fmin, min_pb, max_pb = mms_table(tables.mms_df)
         self.mms_tab = torch.as_tensor(mt, device=dev)
@@ -236,10 +327,25 @@ class YearLoop:
 
     # --------------------------------------------------------------- steps
     def apply_year_inputs(self, year: int):
-        """Base columns x synthetic trajectory (reset each year, dm:245-247)."""
-        k = year - self.first_year
-        for c, r in TRAJ.items():
-            self.batch.cols[c].copy_(self.base[c] * float((1.0 + r) ** k))
+        """This year's elec.apply_* merges as device gathers (dgen_year_inputs)
+        into the resident SoA columns and the loop's customers / load in bin."""
+        self.year_inputs.apply(year, self.batch.cols, self.loop_cols)
+
+    def initial_market(self):
+        """First model year: elec.estimate_initial_market_shares (elec.py:701-765)
+        on device from the state starting capacities, into the carry."""
+        from .market import initial_market_shares
+        caps = self.tables.caps if self.tables.caps is not None else pd.DataFrame(
+            columns=["state_abbr", "sector_abbr", "system_mw", "batt_mw", "batt_mwh", "pv_systems_count",
+                     "batt_systems_count"])
+        st, sec = self.caller_frame          # pandas' group sums visit the frame (caller) order
+        ini = initial_market_shares(self.eng, st, sec, ["solar"] * self.n, self.dev_w,
+                                    self.batch.cols["capex"], caps, dev_index=self.inv)
+        c = self.carry
+        for k in ("market_share_last_year", "adopters_cum_last_year", "market_value_last_year",
+                  "system_kw_cum_last_year", "batt_kw_cum_last_year", "batt_kwh_cum_last_year"):
+            c[k].copy_(ini[k])
+        return ini
 
     def _max_market_share(self):
         import torch
@@ -342,6 +448,8 @@ class YearLoop:
         self.apply_year_inputs(year)
         eng.size(self.batch, self.out, self.c_out)
         mms = self._max_market_share()
+        if first:
+            self.initial_market()
         d = self._diffusion(mms, first)
         att = self._attach(d["new_adopters"])
         hourly_local = None

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 3
+#define DGEN_ABI_VERSION 4
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_NH    8760   /* hours per year                                    */
@@ -377,6 +377,93 @@ int32_t dgen_state_hourly(dgen_ctx* ctx, const void* baseline, const void* pvonl
                           void* stream);
 
 /* ------------------------------------------------------------------------
+ * Per-year agent attributes: the elec.apply_* merges that
+ * dgen_model.py:252-292 runs on the agent frame every model year, as device
+ * gathers over per-year tables compiled on the host (dgen_amd/market.py,
+ * the reference's own expressions per table row):
+ *   apply_load_growth                         elec.py:398-411
+ *   apply_elec_price_multiplier_and_escalator elec.py:29-82
+ *   apply_pv_tech_performance / apply_pv_prices / apply_pv_plus_batt_prices
+ *   apply_financial_params (financing + ITC)  elec.py:135-394
+ *   apply_value_of_resiliency                 elec.py:284-314
+ *   apply_wholesale_elec_prices               elec.py:608-616
+ *   calculate_developable_customers_and_load  elec.py:414-423
+ * A left merge that finds no row gives NaN (reals) or -1 (ints); -1 keys do
+ * the same.  by_sector rows carry DGEN_YS_COLS columns in this order:       */
+enum {
+    DGEN_YS_CAPEX = 0,          /* system_capex_per_kw                        */
+    DGEN_YS_CAPEX_COMBINED,     /* system_capex_per_kw_combined               */
+    DGEN_YS_BATT_CAPEX_KWH,     /* batt_capex_per_kwh_combined                */
+    DGEN_YS_PV_DEG,             /* pv_degradation_factor                      */
+    DGEN_YS_ITC,                /* itc_fraction_of_capex (tech 'solar')       */
+    DGEN_YS_ECON_LIFE,          /* economic_lifetime_yrs                      */
+    DGEN_YS_LOAN_TERM,          /* loan_term_yrs                              */
+    DGEN_YS_DOWN_PAYMENT,       /* down_payment_fraction                      */
+    DGEN_YS_REAL_DISCOUNT,      /* real_discount_rate                         */
+    DGEN_YS_TAX_RATE,           /* tax_rate                                   */
+    DGEN_YS_COLS
+};
+/* by_sector_county rows: load_multiplier, elec_price_multiplier,
+ * elec_price_escalator (DGEN_YC_COLS); by_state_sector: value_of_resiliency_usd. */
+enum { DGEN_YC_LOAD_MULT = 0, DGEN_YC_PRICE_MULT, DGEN_YC_ESCALATOR, DGEN_YC_COLS };
+
+typedef struct {
+    const int32_t* k_sector;          /* row of by_sector (-1: none)            */
+    const int32_t* k_sector_county;   /* row of by_sector_county                 */
+    const int32_t* k_state_sector;    /* row of by_state_sector                  */
+    const int32_t* k_county;          /* row of wholesale_row                    */
+    const uint8_t* is_res;            /* sector_abbr == 'res' (load growth rule) */
+    const double* load_kwh_initial;   /* load_kwh_per_customer_in_bin_initial    */
+    const double* customers_initial;  /* customers_in_bin_initial                */
+    const double* load_in_bin_initial;/* load_kwh_in_bin_initial                 */
+} dgen_year_keys;
+
+typedef struct {
+    const double* by_sector;          /* [n_sector][DGEN_YS_COLS]                */
+    const double* by_sector_county;   /* [n_sector_county][DGEN_YC_COLS]         */
+    const double* by_state_sector;    /* [n_state_sector]                        */
+    const int32_t* wholesale_row;     /* [n_county]: this year's wholesale row   */
+    int64_t n_sector, n_sector_county, n_state_sector, n_county;
+    double inflation_rate;            /* apply_financial_params' scalar          */
+} dgen_year_tables;
+
+typedef struct {                      /* the dgen_agents columns it rewrites +   */
+    double *load_kwh, *price_mult, *escalator, *inflation, *pv_deg, *capex, *capex_combined;
+    double *batt_capex_kwh, *itc_frac, *down_payment, *real_discount, *tax_rate, *vor;
+    int32_t *econ_life, *loan_term, *wholesale_row;
+    double *customers_in_bin, *load_kwh_in_bin;   /* the loop's developable weight / load */
+} dgen_year_out;
+
+int32_t dgen_year_inputs(dgen_ctx* ctx, const dgen_year_keys* keys, const dgen_year_tables* tables,
+                         const dgen_year_out* out, int64_t n, void* stream);
+
+/* First-model-year market seeding, elec.estimate_initial_market_shares
+ * (elec.py:701-765): per (state, sector, tech) group the developable
+ * customers (pandas' Kahan-compensated group sum, rows in frame order) and the
+ * agent count, then each agent's portion of the state's starting capacities
+ * (caps[g * 5 + {system_mw, batt_mw, batt_mwh, pv_systems_count,
+ * batt_systems_count}], NaN when the state has no row) and the
+ * *_last_year / initial_* columns, NaN -> 0 (fillna).  Group g's members are
+ * rows idx[seg_off[g] .. seg_off[g+1]) in frame order.                      */
+typedef struct {
+    const double* developable_agent_weight;
+    const double* system_capex_per_kw;
+} dgen_init_in;
+
+typedef struct {
+    double *adopters_cum_last_year, *system_kw_cum_last_year, *batt_kw_cum_last_year;
+    double *batt_kwh_cum_last_year, *market_share_last_year, *market_value_last_year;
+    double *initial_number_of_adopters, *initial_pv_kw, *initial_batt_kw, *initial_batt_kwh;
+    double *initial_market_share, *initial_market_value;
+    double *developable_customers_in_state;   /* per group, [n_seg]          */
+    int64_t *agent_count;                     /* per group, [n_seg]          */
+} dgen_init_out;
+
+int32_t dgen_initial_market_shares(dgen_ctx* ctx, const dgen_init_in* in, const dgen_init_out* out,
+                                   const int64_t* idx, const int64_t* seg_off, const double* caps,
+                                   int64_t n_seg, void* stream);
+
+/* ------------------------------------------------------------------------
  * Finance-series export, finance_series_export.py:9-81:
  * _norm25 of the six yearly arrays the export writes per agent, in the
  * reference's column order -- cf_energy_value / utility_bill_w_sys /
@@ -410,6 +497,14 @@ int32_t dgen_set_pipeline(dgen_ctx* ctx, int32_t chunks);
  * slices stay cache-resident.  Results do not depend on it.  Range [1, 12];
  * default DGEN_DEFAULT_HOURLY_MONTHS.  Replaces nothing in the reference.   */
 int32_t dgen_set_hourly_segment(dgen_ctx* ctx, int32_t months);
+
+/* PV+battery forward run on (1, default: the reference, which always runs it
+ * at ff:479) or off (0: the PV-only variant of SURVEY 8(d)).  Off: no battery
+ * sizing, storage rate switch or dispatch (batt_kw = batt_kwh = 0, the
+ * with-battery plane is the PV-only net load at kW*), k_batt_finance is not
+ * launched: npv_pv_batt is NaN and the three battery-case yearly arrays are
+ * left untouched.                                                          */
+int32_t dgen_set_battery(dgen_ctx* ctx, int32_t on);
 
 #ifdef __cplusplus
 }

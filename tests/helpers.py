@@ -196,3 +196,34 @@ def golden_tariffs_dc():
     flipped (tests/golden/make_golden_demand.py)."""
     with open(os.path.join(GOLDEN, "tariffs_dc.json")) as f:
         return json.load(f)
+
+
+# tests/golden/market.json column -> device SoA / loop column (dgen_amd.market)
+MARKET_COLS = {"load_kwh_per_customer_in_bin": "load_kwh", "customers_in_bin": "customers_in_bin",
+               "load_kwh_in_bin": "load_kwh_in_bin", "elec_price_multiplier": "price_mult",
+               "elec_price_escalator": "escalator", "pv_degradation_factor": "pv_deg",
+               "system_capex_per_kw": "capex", "system_capex_per_kw_combined": "capex_combined",
+               "batt_capex_per_kwh_combined": "batt_capex_kwh", "value_of_resiliency_usd": "vor",
+               "itc_fraction_of_capex": "itc_frac", "inflation_rate": "inflation",
+               "economic_lifetime_yrs": "econ_life", "loan_term_yrs": "loan_term",
+               "down_payment_fraction": "down_payment", "real_discount_rate": "real_discount",
+               "tax_rate": "tax_rate"}
+
+
+@lru_cache(maxsize=None)
+def golden_market():
+    """market.json (tests/golden/make_golden_market.py): agents, the reference's
+    input tables as DataFrames, and per year the merged columns (None -> NaN)."""
+    with open(os.path.join(GOLDEN, "market.json")) as f:
+        meta = json.load(f)
+    nan = lambda v: np.array([np.nan if x is None else x for x in v], dtype=np.float64)
+    meta["agents"] = pd.DataFrame(meta["agents"])
+    T = {k: pd.DataFrame(v) for k, v in meta["tables"].items()}
+    meta["tables"] = {"load_growth": T["load_growth"], "elec_price": T["elec"], "pv_tech": T["pv_tech"],
+                      "pv_price": T["pv_price"], "pv_plus_batt_price": T["pvb_price"], "vor": T["vor"],
+                      "financing": T["fin"], "itc": T["itc"]}
+    for y in meta["years"]:
+        y["columns"] = {k: nan(v) for k, v in y["columns"].items()}
+        if "initial" in y:
+            y["initial"]["columns"] = {k: nan(v) for k, v in y["initial"]["columns"].items()}
+    return meta

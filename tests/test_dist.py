@@ -117,7 +117,8 @@ def test_state_pool_population():
     assert np.array_equal(is_ca.astype(bool), pop.state_ix == STATES.index("CA"))
     ag = loop_agents(pop, agent_id0=500)
     assert ag["agent_id"][0] == 500 and len(np.unique(ag["agent_id"])) == 500
-    assert (ag["developable_agent_weight"] <= ag["customers_in_bin"]).all()
+    assert (ag["customers_in_bin"] > 0).all()
+    assert np.array_equal(ag["county"], pop.county_ix)
     # the default (all states) stream is unchanged by the pool option
     a = make_population("national_mixed", 300, seed=9, n_res_shapes=8, n_com_shapes=4, n_cf=4,
                         n_counties=4, n_tariffs=8)
@@ -161,3 +162,37 @@ def test_merge_state_rows_single_process():
     from dgen_amd.year_loop import merge_state_rows
     t = merge_state_rows(torch.ones((2, 3), dtype=torch.float64), [4, 7], 10)
     assert t.shape == (10, 3) and t[4].tolist() == [1.0] * 3 and t.sum().item() == 6.0
+
+
+def _timed_worker(rank, world, port, q):
+    """bench.timed_region under gloo: rank r's steps sleep (r + 1) x 40 ms; every
+    rank must report the slowest rank's time (the contract's max over ranks)."""
+    import sys
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+    el = bench.timed_region(lambda: (calls.append(1), time.sleep(0.04 * (rank + 1))), 3,
+                            lambda: None, dist, torch.device("cpu"))
+    q.put((rank, el, len(calls)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_timed_region_max_over_ranks_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timed_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    (r0, el0, c0), (r1, el1, c1) = res
+    assert c0 == c1 == 3                      # exactly `steps` timed calls per rank
+    assert el0 == el1                         # every rank reports the same (max) time
+    assert el0 >= 3 * 0.08 * 0.95             # ... the slower rank's (3 x 80 ms)

@@ -74,6 +74,7 @@ def _check(o, ref, life, pop):
                          ("bill_w_batt", "bill_w_pv_batt"), ("bill_wo_batt", "bill_wo_pv_batt"),
                          ("cash_flow", "cash_flow")):
             assert np.allclose(o[k_o][i, :N1], r[k_r], rtol=1e-6, atol=1e-5), (i, k_o)
+    print(f"demand-charge Brent path flips: {flipped} of {len(ref)}", flush=True)
     assert flipped <= max(1, len(ref) // 50), flipped
 
 

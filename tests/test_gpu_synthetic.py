@@ -16,7 +16,8 @@ from tests import helpers
 
 pytestmark = pytest.mark.gpu
 
-CASES = [("res_1m_nem_tou", 600), ("ca_res_storage", 300), ("com_8m", 200), ("national_mixed", 400)]
+CASES = [("de_res", 300), ("res_1m_nem_tou", 600), ("ca_res_storage", 300), ("com_8m", 200),
+         ("national_mixed", 400)]
 
 
 def _small_pop(cfg, n):
@@ -149,3 +150,38 @@ def test_hourly_segment_is_invisible(engine):
         for k in r:
             if r[k] is not None:
                 assert np.array_equal(res[0][k], r[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("cfg", ["de_res", "ca_res_storage"])
+def test_pv_only_variant(engine, cfg):
+    """dgen_set_battery(0) (SURVEY 8(d) PV-only variant): the search and every
+    PV-only output are bit-identical to the reference run's, no battery is
+    sized, the with-battery plane is the PV-only net load at kW*, and
+    k_batt_finance does not run (npv_pv_batt NaN)."""
+    pop = _small_pop(cfg, 300)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    res = []
+    try:
+        for on in (True, False):
+            engine.set_battery(on)
+            out = engine.alloc_outputs(batch.n, hourly=True)
+            engine.size(batch, out)
+            torch.cuda.synchronize()
+            res.append(outputs_to_host(out))
+    finally:
+        engine.set_battery(True)
+    a, b = res
+    for k in ("system_kw", "x_last", "nfev", "npv", "payback_period", "first_with", "first_without",
+              "annual_kwh", "naep", "baseline", "net_pvonly", "cash_flow", "bill_w_pv", "bill_wo_pv"):
+        assert np.array_equal(a[k], b[k], equal_nan=True), k
+    assert (b["batt_kw"] == 0).all() and (b["batt_kwh"] == 0).all() and np.isnan(b["npv_pv_batt"]).all()
+    # no battery: with-battery plane = max(load - pv(kW*), 0)
+    kw = b["system_kw"]
+    shp, cf = pop.shapes[pop.cols["load_row"]].astype(np.float64), pop.cfs[pop.cols["cf_row"]] / 1e6
+    load = shp * (pop.cols["load_kwh"] / shp.sum(axis=1))[:, None]
+    pv = cf * (((kw * 1000.0) * 0.96) / 1000.0)[:, None]
+    ref = np.maximum(load - pv, 0.0).astype(np.float32)
+    assert np.allclose(b["net_with_batt"], ref, rtol=1e-5, atol=1e-4)

@@ -13,8 +13,10 @@ import torch
 from dgen_amd.engine import hourly_agent_major
 from dgen_amd.synth import STATES, make_population
 from dgen_amd.year_loop import SECTORS, LoopTables, YearLoop, loop_agents
+from dgen_amd.market import YearTables
 from oracle import attach as oa
 from oracle import diffusion as od
+from oracle import market as om
 
 pytestmark = pytest.mark.gpu
 
@@ -22,20 +24,25 @@ N = 2500
 YEARS = [2026, 2027, 2028]
 
 
-def _setup(engine, hourly_chunk=None, seed=20269001):
-    pop = make_population("national_mixed", N, seed=seed, n_res_shapes=64, n_com_shapes=32,
-                          n_cf=32, n_counties=16, n_tariffs=48)
+def _setup(engine, hourly_chunk=None, seed=20269001, config="national_mixed", first_year=YEARS[0]):
+    pool = [STATES.index("DE")] if config == "de_res" else None
+    pop = make_population(config, N, seed=seed, n_res_shapes=64, n_com_shapes=32,
+                          n_cf=32, n_counties=16, n_tariffs=48, state_pool=pool)
     engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     engine.set_tariffs(pop.tariffs)
     engine.set_switches(pop.switches)
     ag = loop_agents(pop, agent_id0=1000)
     tabs = LoopTables.synthetic()
-    return pop, ag, tabs, YearLoop(engine, pop, ag, tabs, first_year=YEARS[0],
+    return pop, ag, tabs, YearLoop(engine, pop, ag, tabs, first_year=first_year,
                                    hourly_export=True, hourly_chunk=hourly_chunk)
 
 
-def test_year_loop_matches_oracle_chain(engine):
-    pop, ag, tabs, loop = _setup(engine)
+@pytest.mark.parametrize("config,years", [("national_mixed", YEARS),
+                                          # C1: Delaware residential, 2-year steps from 2022
+                                          ("de_res", [2022, 2024, 2026])])
+def test_year_loop_matches_oracle_chain(engine, config, years):
+    YEARS = years
+    pop, ag, tabs, loop = _setup(engine, config=config, first_year=years[0])
     perm = loop.perm
     inv = np.empty(N, np.int64)
     inv[perm] = np.arange(N)
@@ -47,18 +54,36 @@ def test_year_loop_matches_oracle_chain(engine):
     q = np.array([bass.loc[(STATES[s], SECTORS[c]), "bass_param_q"] for s, c in zip(st, sec)])
     t1 = np.array([bass.loc[(STATES[s], SECTORS[c]), "teq_yr1"] for s, c in zip(st, sec)])
     m = tabs.mms_df
+    # the per-year inputs restated on the host (caller order): elec.apply_*
+    # merges, pinned to the reference by tests/test_market.py
+    import pandas as pd
+    frame = pd.DataFrame({"state_abbr": [STATES[s] for s in st], "sector_abbr": sec_s,
+                          "county_id": ag["county"]})
+    yt = YearTables(frame, tabs.inputs, tabs.inflation_rate)
+    load0, cust0 = pop.cols["load_kwh"], ag["customers_in_bin"]
     carry = {k: np.zeros(N) for k in ("ms", "adopt", "mv", "skc", "bkw", "bkwh")}
     for y in YEARS:
         r = loop.run_year(y, keep_per_agent=True)
         o = {k: h(loop.out[k]) for k in ("payback_period", "system_kw", "batt_kw", "batt_kwh")}
         assert (h(loop.out["status"]) == 0).all()
-        capex = pop.cols["capex"] * (1.0 - 0.02) ** (y - YEARS[0])
+        yin = yt.gather_host(y, load0, cust0, load0 * cust0)
+        for k in ("load_kwh", "capex", "escalator", "price_mult", "pv_deg", "itc_frac"):
+            assert np.array_equal(h(loop.batch.cols[k]), yin[k]), (y, k)
+        capex, cust = yin["capex"], yin["customers_in_bin"]
+        if y == YEARS[0]:      # elec.estimate_initial_market_shares from the state starting capacities
+            ini = om.initial_market_shares([STATES[s] for s in st], sec_s, ["solar"] * N, cust, capex,
+                                           tabs.caps.to_dict(orient="list"))
+            for k_c, k_i in (("ms", "market_share_last_year"), ("adopt", "adopters_cum_last_year"),
+                             ("mv", "market_value_last_year"), ("skc", "system_kw_cum_last_year"),
+                             ("bkw", "batt_kw_cum_last_year"), ("bkwh", "batt_kwh_cum_last_year")):
+                carry[k_c] = ini[k_i]
+                assert np.array_equal(h(r.per_agent[k_i + "_in"]), ini[k_i]), k_i
         _, _, mms = od.max_market_share(o["payback_period"], sec_s, m["sector_abbr"].tolist(),
                                         m["payback_period"].to_numpy(), m["max_market_share"].to_numpy(),
                                         m["payback_period"].to_numpy())
         got_mms = h(r.per_agent["max_market_share"])
         assert np.array_equal(got_mms, mms, equal_nan=True), y
-        d = od.diffusion(mms, carry["ms"], p, q, t1, ag["developable_agent_weight"], o["system_kw"],
+        d = od.diffusion(mms, carry["ms"], p, q, t1, cust, o["system_kw"],
                          capex, carry["adopt"], carry["mv"], carry["skc"], y == YEARS[0])
         for k in ("market_share", "new_adopters", "number_of_adopters", "market_value", "system_kw_cum"):
             assert np.allclose(h(r.per_agent[k]), d[k], rtol=1e-12, atol=1e-12), (y, k)
@@ -67,7 +92,7 @@ def test_year_loop_matches_oracle_chain(engine):
         assert np.array_equal(h(r.per_agent["added"]), att["batt_adopters_added_this_year"]), y
         assert np.allclose(h(r.per_agent["batt_kw_cum"]), att["batt_kw_cum"], rtol=1e-12, atol=1e-12)
         # per-state hourly export from the loop's own planes (caller order)
-        w = oa.weights(ag["customers_in_bin"], h(r.per_agent["number_of_adopters"]), carry["bkw"],
+        w = oa.weights(cust, h(r.per_agent["number_of_adopters"]), carry["bkw"],
                        o["batt_kw"], att["batt_adopters_added_this_year"])
         planes = [hourly_agent_major(loop.out[k]).cpu().numpy()[inv].astype(np.float64)
                   for k in ("baseline", "net_pvonly", "net_with_batt")]
@@ -98,3 +123,40 @@ def test_chunked_hourly_export_matches_in_place(engine):
         a, b = whole.run_year(y), chunked.run_year(y)
         assert torch.equal(a.totals, b.totals), y
         assert torch.allclose(a.hourly, b.hourly, rtol=1e-12, atol=1e-9), y
+
+
+def test_two_state_shards_reproduce_one_pool(engine):
+    """Multi-GPU by construction: the two ranks' state shards (rank_states(r, 2))
+    run one after the other on this GPU reproduce the single-pool loop --
+    per-agent results bit for bit, per-state totals and hourly rows as the
+    all-reduce would merge them (states are disjoint across ranks)."""
+    from dgen_amd.synth import subset
+    from dgen_amd.year_loop import rank_states
+    pop, ag, tabs, whole = _setup(engine)
+    years = [2026, 2027]
+    full = [whole.run_year(y, keep_per_agent=True) for y in years]
+    full_out = {k: whole.out[k].cpu().numpy()[np.argsort(whole.perm)] for k in ("system_kw", "npv", "batt_kw")}
+    tot = [np.zeros_like(r.totals.cpu().numpy()) for r in full]
+    hrs = [np.zeros_like(r.hourly.cpu().numpy()) for r in full]
+    seen = np.zeros(N, bool)
+    for rank in range(2):
+        mine = np.isin(ag["state"], rank_states(rank, 2))
+        idx = np.nonzero(mine)[0]
+        seen |= mine
+        sp = subset(pop, idx)
+        sa = {k: np.asarray(v)[idx] for k, v in ag.items()}
+        loop = YearLoop(engine, sp, sa, tabs, first_year=years[0], hourly_export=True)
+        for j, y in enumerate(years):
+            r = loop.run_year(y, keep_per_agent=True)
+            tot[j] += r.totals.cpu().numpy()
+            hrs[j] += r.hourly.cpu().numpy()
+            inv = np.argsort(loop.perm)
+            fk = lambda t: t.cpu().numpy()[np.argsort(whole.perm)][idx]
+            for k in ("market_share", "number_of_adopters", "system_kw_cum"):
+                assert np.array_equal(r.per_agent[k].cpu().numpy()[inv], fk(full[j].per_agent[k])), (rank, y, k)
+        for k, v in full_out.items():
+            assert np.array_equal(loop.out[k].cpu().numpy()[np.argsort(loop.perm)], v[idx]), (rank, k)
+    assert seen.all()
+    for j in range(len(years)):
+        assert np.array_equal(tot[j], full[j].totals.cpu().numpy()), years[j]
+        assert np.allclose(hrs[j], full[j].hourly.cpu().numpy(), rtol=0, atol=0), years[j]
