@@ -37,30 +37,39 @@ NB_BYTES = 9280                 # net-billing split record per scratch slot (DGE
 
 
 def algorithmic_bytes(cols, hourly: bool, battery: bool):
-    """ALGORITHMIC bytes per step of each sizing kernel for this population
-    (DESIGN.md section 5): what the algorithm must read and write once,
-    whatever the caches serve.
-      k_size          576 (month, daytype, hour) slot sums of both profile rows
-                      (f64) + ~24 scalars + 4 yearly output arrays of N+1 f64;
-                      agents that bill hourly imports (net billing / demand
-                      charges, the scratch-slot agents) also read both profile
-                      rows once (the split / envelope build) and write the
+    """ALGORITHMIC HBM bytes per step of each sizing kernel for this population
+    (DESIGN.md section 5): the bytes the step cannot avoid moving.  Profile
+    rows are shared: every distinct load-shape / cf row the batch uses must be
+    read once (not once per agent -- per-agent row reads that hit in L2 / MALL
+    are not HBM traffic); per-agent inputs and outputs are moved once each.
+      k_size          the distinct rows' 576 (month, daytype, hour) slot sums
+                      (f64, both tables), ~24 scalars and 4 yearly output
+                      arrays of N+1 f64 per agent; agents that bill hourly
+                      imports (net billing / demand charges: the scratch-slot
+                      agents) also need their distinct rows and write the
                       split record
-      k_hourly_batt   both profile rows + the (month, period) bins + scalars,
-                      the three f32 hourly planes when requested, and the f64
-                      system-output plane of the scratch-slot agents
-      k_batt_finance  the bins + scalars + 3 yearly arrays; scratch-slot agents
-                      read the system-output plane and the load-shape row"""
+      k_hourly_batt   the distinct rows, the (month, period) bins + scalars per
+                      agent, the three f32 hourly planes when requested, and
+                      the f64 system-output plane of the scratch-slot agents
+      k_batt_finance  bins + scalars + 3 yearly arrays per agent; the
+                      scratch-slot agents read their system-output plane and
+                      their distinct load rows"""
     n = len(cols["load_kwh"])
+    lr, cr = np.asarray(cols["load_row"]), np.asarray(cols["cf_row"])
     yearly = 8.0 * (np.asarray(cols["econ_life"], np.int64) + 1).sum()
-    nh = int((np.asarray(cols["scratch_slot"]) >= 0).sum())
-    k_size = n * (2 * 576 * 8 + 24 * 8) + 4 * yearly + nh * (2 * ROW_BYTES + NB_BYTES)
-    k_hourly = n * (2 * ROW_BYTES + 2 * 144 * 8 + 16 * 8)
+    sl = np.asarray(cols["scratch_slot"]) >= 0
+    nh = int(sl.sum())
+    rows = (np.unique(lr).size + np.unique(cr).size) * ROW_BYTES
+    rows_h = (np.unique(lr[sl]).size + np.unique(cr[sl]).size) * ROW_BYTES if nh else 0
+    slots = (np.unique(lr).size + np.unique(cr).size) * 576 * 8
+    k_size = slots + n * 24 * 8 + 4 * yearly + rows_h + nh * NB_BYTES
+    k_hourly = rows + n * (2 * 144 * 8 + 16 * 8)
     if hourly:
         k_hourly += n * 3 * PLANE_BYTES
     if battery:
         k_hourly += nh * SYS_BYTES
-    k_fin = (n * (2 * 144 * 8 + 24 * 8) + 3 * yearly + nh * (SYS_BYTES + ROW_BYTES)) if battery else 0.0
+    k_fin = (n * (2 * 144 * 8 + 24 * 8) + 3 * yearly + nh * SYS_BYTES +
+             (np.unique(lr[sl]).size * ROW_BYTES if nh else 0)) if battery else 0.0
     return {"k_size": float(k_size), "k_hourly_batt": float(k_hourly), "k_batt_finance": float(k_fin)}
 
 

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Benchmark of the drop-in host path: financial_functions.size_chunk on an
+agent DataFrame in the reference's schema (dgen_amd.synth.reference_frame:
+shared tariff dicts and per-county wholesale arrays, ProfileStore keys, a
+rate_switch_table), end to end -- columnise, upload, size on the GPU,
+download, build the output frame -- with each phase timed.
+
+Beside it, the round-1 row-by-row path (iterrows + per-row columnariser +
+per-row output Series, what size_chunk did before) on a smaller frame, so the
+host-path speed-up is measured, not assumed.  Prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+
+def rowwise(df, store, table):
+    """The round-1 size_chunk body: per-row copies, PopulationBuilder.add per
+    row, per-row output Series (dgen_amd.financial_functions.size_rows)."""
+    import pandas as pd
+    from dgen_amd import financial_functions as ff
+    t0 = time.perf_counter()
+    rows = []
+    for aid, row in df.iterrows():
+        r = row.copy()
+        r.name = aid
+        rows.append(r)
+    sized, _ = ff.size_rows(rows, store, table, hourly="list")
+    out = pd.DataFrame(sized)
+    return time.perf_counter() - t0, len(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--agents", type=int, default=100_000)
+    ap.add_argument("--hourly", default="array", choices=["list", "array", "none"])
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--rowwise-agents", type=int, default=5_000,
+                    help="frame size for the row-by-row comparison (0: skip)")
+    args = ap.parse_args()
+    from dgen_amd import financial_functions as ff
+    from dgen_amd.synth import reference_frame
+
+    df, store, table = reference_frame(args.agents)
+    ff._worker_conn = store
+    ff.size_chunk(df.iloc[:2000], None, table, hourly=args.hourly)        # engine + tables warm
+    runs = []
+    for _ in range(args.reps):
+        tm = {}
+        t0 = time.perf_counter()
+        out, agg = ff.size_chunk(df, None, table, hourly=args.hourly, timing=tm)
+        tm["total_s"] = time.perf_counter() - t0
+        tm["net_sum_s"] = tm["total_s"] - tm["columnize_s"] - tm["device_call_s"] - tm["output_frame_s"]
+        runs.append(tm)
+    best = min(runs, key=lambda r: r["total_s"])
+    res = {"metric": "drop-in size_chunk agents/s (reference-schema frame -> sized frame, end to end)",
+           "value": args.agents / best["total_s"], "unit": "agents/s", "higher_is_better": True,
+           "config": {"agents": args.agents, "hourly": args.hourly, "reps": args.reps,
+                      "frame": "dgen_amd.synth.reference_frame (synthetic, reference schema)"},
+           "phases_s": {k: round(v, 4) for k, v in best.items()},
+           "device_share": best["device_s"] / best["total_s"]}
+    if args.rowwise_agents:
+        n = min(args.rowwise_agents, args.agents)
+        sub = df.iloc[:n]
+        tm = {}
+        t0 = time.perf_counter()
+        ff.size_chunk(sub, None, table, hourly="list", timing=tm)
+        t_new = time.perf_counter() - t0
+        t_old, _ = rowwise(sub, store, table)
+        res["rowwise_comparison"] = {"agents": n, "hourly": "list", "rowwise_agents_per_s": n / t_old,
+                                     "frame_agents_per_s": n / t_new, "speedup": t_old / t_new}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

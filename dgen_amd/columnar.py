@@ -12,6 +12,7 @@ import hashlib
 from typing import Any, Dict, Hashable, List, Optional, Sequence, Tuple
 
 import numpy as np
+import pandas as pd
 
 from . import _lib
 from .engine import SWITCH_DTYPE
@@ -101,6 +102,39 @@ class WholesaleIndex:
             self.rows.append(a)
         return k
 
+    def add_cached(self, arr, mult: float, cache: Dict[int, Tuple]) -> int:
+        """add() with the conversion, finiteness scan and content hash done
+        once per distinct array object (cache: id -> (key, array, all finite,
+        max |x|)); a row enters the table at its first valid use, as in add().
+        The f32-finiteness of arr * mult (series_8760) follows from the largest
+        |x|: |x * mult| is monotone in |x|."""
+        if arr is None:
+            return -1
+        ent = cache.get(id(arr))
+        if ent is None:
+            try:
+                a = np.asarray(arr, dtype=np.float64).ravel()
+            except Exception:
+                a = None
+            if a is None or a.size != 8760:
+                ent = (None, None, False, 0.0)
+            else:
+                ent = (hashlib.blake2b(a.tobytes(), digest_size=16).digest(), a,
+                       bool(np.isfinite(a).all()), float(np.abs(a).max()))
+            cache[id(arr)] = ent
+        key, a, fin, mx = ent
+        if key is None or not fin or not np.isfinite(mult):
+            return -1
+        with np.errstate(over="ignore"):
+            if not np.isfinite(np.float32(mx * abs(mult))):
+                return -1
+        k = self._index.get(key)
+        if k is None:
+            k = len(self.rows)
+            self._index[key] = k
+            self.rows.append(a)
+        return k
+
     def array(self) -> Optional[np.ndarray]:
         return np.stack(self.rows) if self.rows else None
 
@@ -157,7 +191,8 @@ def assign_scratch(cols: Dict[str, np.ndarray], tariffs: np.ndarray, switches: n
     be net billing (mo 2) or carry demand charges (both bill hourly imports):
     its initial tariff or any rate-switch candidate."""
     n = len(cols["load_kwh"])
-    mo2 = (tariffs["mo"] == 2) | (tariffs["dc"] > 0) if tariffs.size else np.zeros(0, bool)
+    # net billing (metering options 2 and 3) bills hourly imports
+    mo2 = ((tariffs["mo"] == 2) | (tariffs["mo"] == 3) | (tariffs["dc"] > 0)) if tariffs.size else np.zeros(0, bool)
     need = mo2[cols["tariff0"]] if n else np.zeros(0, bool)
     if switches.size:
         sw_mo2 = mo2[switches["tariff"]]
@@ -170,3 +205,77 @@ def assign_scratch(cols: Dict[str, np.ndarray], tariffs: np.ndarray, switches: n
     slots[need] = np.arange(int(need.sum()), dtype=np.int32)
     cols["scratch_slot"] = slots
     return int(need.sum())
+
+
+def _num(series) -> np.ndarray:
+    """float(x) per cell, NaN where that raises (financial_functions._finite_float)."""
+    out = pd.to_numeric(series, errors="coerce")
+    return np.asarray(out, dtype=np.float64)
+
+
+def columnize_frame(df, src, rate_switch_table=None, skip_demand_charges=None) -> "PopulationBuilder":
+    """Vectorised PopulationBuilder over an agent DataFrame in the reference's
+    schema (the columns calc_system_size_and_performance reads, ff:330-421):
+    numeric columns converted whole, profile keys / tariffs / rate-switch
+    candidates / wholesale series resolved once per distinct object (tariff
+    dicts and wholesale arrays that rows share, as pandas merges leave them,
+    are compiled / validated / hashed once).  Produces exactly the columns and
+    tables add() row by row would (tests/test_boundary.py)."""
+    b = PopulationBuilder(rate_switch_table, skip_demand_charges)
+    n = len(df)
+    cols = empty_columns(n)
+    sector = df["sector_abbr"].tolist()
+    state = df["state_abbr"].tolist() if "state_abbr" in df else [""] * n
+    is_ca = np.array([_is_ca(s) for s in state], bool)
+    is_res = np.array([s == "res" for s in sector], bool)
+    # profile rows: one lookup per distinct key
+    lk, sk = {}, {}
+    bldg, gid = df["bldg_id"].tolist(), df["solar_re_9809_gid"].tolist()
+    tilt, az = df["tilt"].tolist(), df["azimuth"].tolist()
+    for i in range(n):
+        k1 = (bldg[i], sector[i], state[i])
+        r = lk.get(k1)
+        if r is None:
+            r = lk[k1] = src.load_row({"bldg_id": bldg[i], "sector_abbr": sector[i], "state_abbr": state[i]})
+        cols["load_row"][i] = r
+        k2 = (gid[i], tilt[i], az[i])
+        r = sk.get(k2)
+        if r is None:
+            r = sk[k2] = src.solar_row({"solar_re_9809_gid": gid[i], "tilt": tilt[i], "azimuth": az[i]})
+        cols["cf_row"][i] = r
+    # tariffs: content key once per distinct dict / string object
+    from .tariff import tariff_key
+    tdict = df["tariff_dict"].tolist()
+    tkey: Dict[int, str] = {}
+    eia = df["eia_id"].tolist()
+    mult = _num(df["elec_price_multiplier"])
+    whl = df["wholesale_prices"].tolist() if "wholesale_prices" in df else [None] * n
+    wcache: Dict[int, Tuple] = {}
+    W = b.wholesale
+    for i in range(n):
+        raw = tdict[i]
+        key = tkey.get(id(raw))
+        if key is None:
+            key = tkey[id(raw)] = tariff_key(raw)
+        cols["tariff0"][i] = b.tariffs.add(raw, bool(is_ca[i]), key=key)
+        cols["sw_solar_off"][i], cols["sw_solar_cnt"][i] = b.switches.candidates("solar", eia[i], sector[i],
+                                                                                  bool(is_ca[i]))
+        cols["sw_storage_off"][i], cols["sw_storage_cnt"][i] = b.switches.candidates("storage", eia[i],
+                                                                                      sector[i], bool(is_ca[i]))
+        cols["wholesale_row"][i] = -1 if is_ca[i] else W.add_cached(whl[i], float(mult[i]), wcache)
+    cols["flags"] = (is_res.astype(np.uint8) | (is_ca.astype(np.uint8) << 1)).astype(np.uint8)
+    cols["econ_life"] = df["economic_lifetime_yrs"].astype(np.int64).to_numpy().astype(np.int32)
+    cols["loan_term"] = df["loan_term_yrs"].astype(np.int64).to_numpy().astype(np.int32)
+    for name, ref in (("load_kwh", "load_kwh_per_customer_in_bin"), ("inflation", "inflation_rate"),
+                      ("pv_deg", "pv_degradation_factor"), ("escalator", "elec_price_escalator"),
+                      ("down_payment", "down_payment_fraction"), ("tax_rate", "tax_rate"),
+                      ("real_discount", "real_discount_rate"), ("itc_frac", "itc_fraction_of_capex"),
+                      ("capex", "system_capex_per_kw"), ("capex_combined", "system_capex_per_kw_combined"),
+                      ("batt_capex_kwh", "batt_capex_per_kwh_combined"), ("ccm", "cap_cost_multiplier"),
+                      ("vor", "value_of_resiliency_usd")):
+        cols[name] = _num(df[ref])
+    cols["price_mult"] = mult
+    cols["scratch_slot"] = np.full(n, -1, np.int32)
+    assign_scratch(cols, b.tariffs.array(), b.switches.array())
+    b.frame_columns = cols
+    return b

@@ -52,6 +52,12 @@ typedef __attribute__((address_space(3))) char* lds_ptr_t;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+// Metering options billed from hourly imports / exports (net billing: 2, and
+// 3 = with $ carryover); 0 (NEM kWh), 1 (NEM $) and 4 (buy all / sell all)
+// bill from the monthly (month, period) bins.  SAM's enumeration; the
+// reference passes the tariff's value through (ff:586-588, 970-971).
+__host__ __device__ __forceinline__ bool net_hourly(const dgen_tariff& t) { return t.mo == 2 || t.mo == 3; }
+
 __constant__ int c_month_start_day[13] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334, 365};
 __constant__ int c_days_in_month[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
 
@@ -647,7 +653,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     }
     const dgen_tariff& t = T.tariffs[tariff];
     const int P = t.P;
-    const bool mo2 = (t.mo == 2);
+    const bool mo2 = net_hourly(t);     // hourly imports (net billing 2 / 3), else bins
     const int slot = A.scratch_slot[i];
     // the battery-case bill reads the hourly system output for net billing and
     // for demand charges (both need hourly imports, not bins)
@@ -975,6 +981,52 @@ __device__ __forceinline__ double yl_month_charge(const dgen_tariff& t, int m, c
     return charge;
 }
 
+// A net-billing month's bill: fixed + energy charge - export credit; option 3
+// floors the energy part at 0 and carries the excess credit to the next month
+// (lost at year end).  oracle/orc.c year_bill, same order.
+__device__ __forceinline__ double nb_month(const dgen_tariff& t, double charge, double cr, double& carry) {
+    if (t.mo == 3) {
+        const double e = charge - cr - carry;
+        carry = e < 0.0 ? -e : 0.0;
+        return t.fixed + (e < 0.0 ? 0.0 : e);
+    }
+    return t.fixed + charge - cr;
+}
+
+// Bill of metering options 1 (NEM with $ credits: per-period monthly net,
+// imports billed, surplus kWh credited at the period's tier-1 sell rate, the
+// energy part floored at 0 with the excess carried) and 4 (buy all / sell
+// all: the whole load billed, all generation credited at the tier-1 sell
+// rate) from the lane's bins; oracle/orc.c year_bill, same order.  Parity
+// unpinned (SSC restatement).
+__device__ double yl_bill_bins_ext(const dgen_tariff& t, const YLds& S, double gscale) {
+    const int P = t.P, half = S.half;
+    double total = 0.0, carry = 0.0;
+    for (int m = 0; m < 12; m++) {
+        double cr = 0.0;
+        for (int p = 0; p < P; p++) {
+            const double L = S.L[m * half + p], G = S.G[m * half + p];
+            if (t.mo == 1) {
+                const double nn = L - gscale * G;
+                S.at(p) = nn > 0.0 ? nn : 0.0;
+                cr += (nn < 0.0 ? -nn : 0.0) * t.sell[p][0];
+            } else {
+                S.at(p) = L;
+                cr += (gscale * G) * t.sell[p][0];
+            }
+        }
+        const double charge = yl_month_charge(t, m, S, 0);
+        if (t.mo == 1) {
+            const double e = charge - cr - carry;
+            carry = e < 0.0 ? -e : 0.0;
+            total += t.fixed + (e < 0.0 ? 0.0 : e);
+        } else {
+            total += t.fixed + (charge - cr);
+        }
+    }
+    return total;
+}
+
 // NEM (mo 0) bill of the lane's year: net = L - gscale * G per (month, period)
 // from the LDS bins; per-period kWh credits; December true-up.
 __device__ __forceinline__ double yl_bill_mo0(const dgen_tariff& t, const YLds& S, double gscale,
@@ -1086,6 +1138,7 @@ __device__ __forceinline__ double yl_bill_mo0_reg(const dgen_tariff& t, const YL
 
 __device__ __forceinline__ double yl_bill_nem(const dgen_tariff& t, const YLds& S, double gscale,
                                               double yearend) {
+    if (t.mo != 0) return yl_bill_bins_ext(t, S, gscale);                 // options 1 and 4
     return (t.P <= PREG) ? yl_bill_mo0_reg(t, S, gscale, yearend) : yl_bill_mo0(t, S, gscale, yearend);
 }
 
@@ -1152,7 +1205,7 @@ constexpr int MO2_CH = 8;
 __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YSrc& src, double s,
                                                   bool with_gen) {
     const int P = t.P;
-    double total = 0.0;
+    double total = 0.0, carry = 0.0;
     int h = 0;
     for (int m = 0; m < 12; m++) {
         double imp[PREG], exv[PREG];
@@ -1213,7 +1266,7 @@ __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YS
 #pragma unroll
         for (int p = 0; p < PREG; p++)
             if (p < P) cr += src.ts ? exv[p] : exv[p] * t.sell[p][0];
-        total += t.fixed + reg_month_charge(t, m, imp) - cr;
+        total += nb_month(t, reg_month_charge(t, m, imp), cr, carry);
     }
     return total;
 }
@@ -1222,7 +1275,7 @@ __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YS
 __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& src, double s,
                                               bool with_gen, const YLds& S) {
     const int P = t.P, half = S.half;
-    double total = 0.0;
+    double total = 0.0, carry = 0.0;
     int h = 0;
     for (int m = 0; m < 12; m++) {
         for (int p = 0; p < P; p++) { S.at(p) = 0.0; S.at(half + p) = 0.0; }
@@ -1306,7 +1359,7 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
             double e = S.at(half + p);
             cr += src.ts ? e : e * t.sell[p][0];
         }
-        total += t.fixed + yl_month_charge(t, m, S, 0) - cr;
+        total += nb_month(t, yl_month_charge(t, m, S, 0), cr, carry);
     }
     return total;
 }
@@ -1663,7 +1716,7 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
     const NbRec R = nb_rec(nbp);
     const int P = t.P, half = S.half;
     const double kws = src.gen_scale;
-    double total = 0.0;
+    double total = 0.0, carry = 0.0;
     for (int m = 0; m < 12; m++) {
         for (int p = 0; p < P; p++) {
             const double* q = R.sums + (m * MAXP + p) * 4;
@@ -1722,7 +1775,7 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
             const double e = S.at(half + p);
             cr += src.ts ? e : e * t.sell[p][0];
         }
-        total += t.fixed + yl_month_charge(t, m, S, 0) - cr;
+        total += nb_month(t, yl_month_charge(t, m, S, 0), cr, carry);
     }
     return total;
 }
@@ -1891,6 +1944,7 @@ struct YCtx {
     double wo1;           // year-1 no-system bill, current tariff
     const double* lslots;
     const double* gslots;
+    const double* ts_row;     // the agent's 8760 wholesale row (non-CA), or nullptr
     YSrc src;
     YLds S;
     YLoan loan;
@@ -1907,7 +1961,9 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
     const dgen_tariff& t = *c.tp;
     c.tariff = tix;
     c.status |= t.flags;
-    if (t.mo == 0) {
+    // the 8760 TS sell rate applies under net billing option 2 only (ff:626-641)
+    c.src.ts = (t.mo == 2) ? c.ts_row : nullptr;
+    if (!net_hourly(t)) {
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);
@@ -1943,7 +1999,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double kws = ((kw * 1000.0) * 0.96) / 1000.0;                  // ff:118-120
     double total = ((c.capex * kw + 0.0) * c.ccm) + 0.0 + otc;     // ff:263,280-282
     double wb;
-    if (t.mo == 0) {
+    if (!net_hourly(t)) {
         wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
     } else {
         c.src.gen_scale = kws;
@@ -2042,7 +2098,8 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.src.load_scale = c.load_scale;
     c.src.gen_scale = 0.0;
     const int wr = A.wholesale_row[i];
-    c.src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+    c.ts_row = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+    c.src.ts = nullptr;                       // set per tariff (yl_set_tariff)
     c.src.ts_mult = A.price_mult[i];
 
     bool bad = false;
@@ -2145,7 +2202,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     double batt_costs = A.batt_capex_kwh[i] * bank * 0.7;                           // ff:219
     double total = ((system_costs + batt_costs) * A.ccm[i]) + 0.0 + otc;
     const double vor = A.vor[i];
-    const bool mo2 = t.mo == 2;
+    const bool mo2 = net_hourly(t);
     const dgen_demand* dem = DC ? tariff_demand(T, cfg, t) : nullptr;
     YSrc src;
     {
@@ -2158,7 +2215,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         const int slot = A.scratch_slot[i];
         src.sysgen = (slot >= 0) ? W.scratch + (int64_t)slot * 4 : nullptr;
         const int wr = A.wholesale_row[i];
-        src.ts = (!is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+        src.ts = (t.mo == 2 && !is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
         src.ts_mult = A.price_mult[i];
     }
     double wo1, wb;
@@ -2513,9 +2570,12 @@ __global__ void k_export_weights(const double* __restrict__ customers, const dou
 // hours); f64 planes are plain [h][n].  Members of state s are
 // idx[seg_off[s] .. seg_off[s+1]) (idx null: the plane columns themselves,
 // states contiguous).  Block per (state, tile of SH_TILE hours): the three
-// weights of an agent are read once per tile instead of once per hour.  Fixed
-// reduction order.
-constexpr int SH_TILE = 16;
+// weights and the column index of an agent are read once per tile (32 B per
+// 32 hours against 384 B of planes).  The plane reads are coalesced only when
+// a state's columns are a contiguous ascending range (the year loop's
+// state-major device order); a scattered idx fetches a 128-B line per 16-B
+// quad.  Fixed reduction order.
+constexpr int SH_TILE = 32;
 template <typename V>
 __global__ void __launch_bounds__(256)
 k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
@@ -2523,7 +2583,7 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
                const double* __restrict__ w_batt, const double* __restrict__ w_non,
                const int64_t* __restrict__ idx, int64_t n, int nh,
                const int64_t* __restrict__ seg_off, int64_t n_seg, double* __restrict__ out) {
-    __shared__ double red[256];
+    __shared__ double red[4][SH_TILE];
     const int64_t s = blockIdx.x;
     const int h0 = blockIdx.y * SH_TILE;
     if (s >= n_seg || h0 >= nh) return;
@@ -2560,16 +2620,20 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
             }
         }
     }
-    for (int t = 0; t < nt; t++) {
-        red[threadIdx.x] = acc[t];
-        __syncthreads();
-        for (int w = 128; w > 0; w >>= 1) {
-            if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-            __syncthreads();
-        }
-        if (threadIdx.x == 0) out[s * nh + h0 + t] = red[0] / 1000.0;
-        __syncthreads();
+    // butterfly within each wave (static acc indices: no scratch), then the
+    // four wave partials in wave order
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int t = 0; t < SH_TILE; t++) {
+        double v = acc[t];
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+        if (lane == 0) red[wv][t] = v;
     }
+    __syncthreads();
+    if (threadIdx.x < nt)
+        out[s * nh + h0 + threadIdx.x] =
+            (((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x]) / 1000.0;
 }
 
 // ---------------------------------------------------------------------------

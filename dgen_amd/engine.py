@@ -39,7 +39,8 @@ class AgentBatch:
     perm: Optional[np.ndarray] = None
 
 
-def profile_order(cols: Dict[str, np.ndarray], major: str = "load") -> np.ndarray:
+def profile_order(cols: Dict[str, np.ndarray], major: str = "load",
+                  group: Optional[np.ndarray] = None) -> np.ndarray:
     """Device order for a batch: agents grouped by (load_row, cf_row)
     (major="cf": by (cf_row, load_row)).
 
@@ -51,9 +52,14 @@ def profile_order(cols: Dict[str, np.ndarray], major: str = "load") -> np.ndarra
     38.0 ms cf-major, 45.3 ms caller order).  The
     reference's agent order carries no meaning (size_chunk returns rows keyed
     by agent_id, ff:1149-1218), so the host columnarizer is free to choose it.
-    Stable, so ties keep caller order."""
+    group (optional) is an outer key: the model-year loop passes the state so
+    each state's members are one contiguous column range of the hourly planes
+    and k_state_hourly streams them coalesced.  Stable, so ties keep caller
+    order."""
     lr, cr = np.asarray(cols["load_row"]), np.asarray(cols["cf_row"])
     keys = (lr, cr) if major == "cf" else (cr, lr)
+    if group is not None:
+        keys = keys + (np.asarray(group),)
     return np.lexsort(keys).astype(np.int64)
 
 

@@ -24,7 +24,7 @@ import numpy as np
 import pandas as pd
 
 from . import _lib
-from .columnar import PopulationBuilder
+from .columnar import PopulationBuilder, columnize_frame
 from .profiles import ProfileStore, SqlProfileSource, as_source
 from .tariff import (FORCE_NET_BILLING, SKIP_DEMAND_CHARGES, normalize_tariff,  # noqa: F401
                      process_tariff)
@@ -131,6 +131,43 @@ def _raise_for_status(status: np.ndarray, agent_ids) -> None:
     raise _lib.DgenError(f"agent {who}: sizing failed with status 0x{s:x}")
 
 
+_loaded = {}
+
+
+def _device_tables(eng, src: ProfileStore, b: PopulationBuilder):
+    """Upload the profile tables (and their row / slot sums) only when the
+    store has grown or the wholesale table changed since the last call: a
+    chunk loop re-sizes against the same tables."""
+    wh = b.wholesale.array()
+    wkey = None if wh is None else (wh.shape, hash(wh.tobytes()))
+    key = (id(eng), id(src), src.n_load, src.n_solar, wkey)
+    if _loaded.get("key") != key:
+        eng.load_profiles(src.shapes, src.cfs, wh)
+        _loaded["key"] = key
+    eng.set_tariffs(b.tariffs.array())
+    eng.set_switches(b.switches.array())
+
+
+def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[dict] = None):
+    import time
+    import torch
+    from .engine import outputs_to_host, profile_order
+    eng = get_engine()
+    t0 = time.perf_counter()
+    _device_tables(eng, src, b)
+    batch = eng.upload_agents(cols, order=profile_order(cols))
+    out = eng.alloc_outputs(batch.n, hourly=True)
+    torch.cuda.synchronize(eng.dev)
+    t1 = time.perf_counter()
+    eng.size(batch, out)
+    torch.cuda.synchronize(eng.dev)
+    t2 = time.perf_counter()
+    o = outputs_to_host(out, batch.perm)
+    if timing is not None:
+        timing.update(upload_s=t1 - t0, device_s=t2 - t1, download_s=time.perf_counter() - t2)
+    return o
+
+
 def size_rows(rows, con, rate_switch_table, hourly: str = "list"):
     """Size a list of agent rows (pd.Series) in one batched device call.
     Returns (list of output Series, host outputs dict)."""
@@ -141,17 +178,7 @@ def size_rows(rows, con, rate_switch_table, hourly: str = "list"):
     src.ensure(rows)
     b = _columnarize(rows, src, rate_switch_table)
     cols = b.columns()
-    eng = get_engine()
-    from .engine import outputs_to_host, profile_order
-    import torch
-    eng.load_profiles(src.shapes, src.cfs, b.wholesale.array())
-    eng.set_tariffs(b.tariffs.array())
-    eng.set_switches(b.switches.array())
-    batch = eng.upload_agents(cols, order=profile_order(cols))
-    out = eng.alloc_outputs(batch.n, hourly=True)
-    eng.size(batch, out)
-    torch.cuda.synchronize(eng.dev)
-    o = outputs_to_host(out, batch.perm)
+    o = _run_device(b, cols, src)
     ids = [r.get("agent_id", r.name) for r in rows]
     _raise_for_status(o["status"], ids)
     cfs = src.cfs
@@ -226,32 +253,103 @@ _DROP = ("adopter_load_hourly", "adopter_pv_hourly", "adopter_batt_to_load_hourl
          "generation_hourly", "batt_dispatch_profile", "net_hourly")
 
 
-def size_chunk(static_agents_df: pd.DataFrame, sectors, rate_switch_table, mode="simple"):
+def _yearly_lists(a: np.ndarray, n1: np.ndarray):
+    return [a[i, :n1[i]].tolist() for i in range(a.shape[0])]
+
+
+def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
+               timing: Optional[dict] = None):
+    """The batched form of calc_system_size_and_performance over a whole agent
+    frame (what size_chunk needs), built by column: the frame is columnised
+    at once (columnar.columnize_frame), sized in one device call, and the
+    output columns are assigned whole.  Same values and columns as mapping
+    calc_system_size_and_performance over the rows (ff:449-565 write order);
+    hourly: "list" (the reference's fp64 lists), "array" (each cell a row
+    view of one [n, 8760] float32 array, no per-agent copy) or "none".
+    timing: filled with the host / device phases (seconds)."""
+    import time
+    if rate_switch_table is None:
+        raise AttributeError("'NoneType' object has no attribute 'loc' (rate_switch_table is required)")
+    t0 = time.perf_counter()
+    src = _source(con)
+    src.ensure_frame(df)
+    b = columnize_frame(df, src, rate_switch_table)
+    cols = b.frame_columns
+    t1 = time.perf_counter()
+    dev_t: dict = {}
+    o = _run_device(b, cols, src, dev_t)
+    t2 = time.perf_counter()
+    ids = df["agent_id"].tolist() if "agent_id" in df else list(df.index)
+    _raise_for_status(o["status"], ids)
+    out = df.copy(deep=False)
+    if "agent_id" not in out.columns:
+        out.insert(len(out.columns), "agent_id", list(df.index))
+    n1 = df["economic_lifetime_yrs"].astype(np.int64).to_numpy() + 1
+    out["naep"] = o["naep"]
+    out["cf_energy_value_pv_only"] = _yearly_lists(o["cfev_pv"], n1)
+    out["utility_bill_w_sys_pv_only"] = _yearly_lists(o["bill_w_pv"], n1)
+    out["utility_bill_wo_sys_pv_only"] = _yearly_lists(o["bill_wo_pv"], n1)
+    sw = np.nonzero(o["switched"] != 0)[0]
+    if sw.size:
+        # elec.py:852-855: the sticky switch rewrites the agent in place
+        lim = (np.asarray(out["nem_system_kw_limit"].tolist(), dtype=object) if "nem_system_kw_limit" in out
+               else np.full(len(out), np.nan, dtype=object))
+        tid = np.asarray(out["tariff_id"].tolist(), dtype=object) if "tariff_id" in out else None
+        tdi = np.empty(len(out), dtype=object)
+        tdi[:] = out["tariff_dict"].tolist()
+        for i in sw:
+            lim[i] = 1e6
+            r = b.switches.row_of_tariff.get(int(o["tariff_final"][i]))
+            if r is not None:
+                if tid is not None:
+                    tid[i] = r["rate_id_alias"]
+                tdi[i] = r["json"]
+        out["nem_system_kw_limit"] = pd.Series(lim, index=out.index).infer_objects()
+        if tid is not None:
+            out["tariff_id"] = pd.Series(tid, index=out.index).infer_objects()
+        out["tariff_dict"] = pd.Series(tdi, index=out.index)
+    out["cf_energy_value_pv_batt"] = _yearly_lists(o["cfev_batt"], n1)
+    out["utility_bill_w_sys_pv_batt"] = _yearly_lists(o["bill_w_batt"], n1)
+    out["utility_bill_wo_sys_pv_batt"] = _yearly_lists(o["bill_wo_batt"], n1)
+    if hourly != "none":
+        conv = ((lambda a: [r.astype(np.float64).tolist() for r in a]) if hourly == "list"
+                else (lambda a: list(a)))
+        out["baseline_net_hourly"] = conv(o["baseline"])
+        out["adopter_net_hourly_pvonly"] = conv(o["net_pvonly"])
+        out["adopter_net_hourly_with_batt"] = conv(o["net_with_batt"])
+        out["adopter_net_hourly"] = out["adopter_net_hourly_pvonly"]
+    out["system_kw"] = o["system_kw"]
+    out["annual_energy_production_kwh"] = o["annual_kwh"]
+    out["capacity_factor"] = o["capacity_factor"]
+    out["price_per_kwh"] = o["price_per_kwh"]
+    out["npv"] = o["npv"]
+    out["payback_period"] = o["payback_period"]
+    out["cash_flow"] = _yearly_lists(o["cash_flow"], n1)
+    out["batt_kw"] = o["batt_kw"]
+    out["batt_kwh"] = o["batt_kwh"]
+    t3 = time.perf_counter()
+    if timing is not None:
+        timing.update(columnize_s=t1 - t0, device_call_s=t2 - t1, output_frame_s=t3 - t2, **dev_t)
+    return out, o
+
+
+def size_chunk(static_agents_df: pd.DataFrame, sectors, rate_switch_table, mode="simple",
+               hourly: str = "list", timing: Optional[dict] = None):
     """ff:1136 -- size a chunk; returns (df_out, agg) with
     agg["net_sum_kw"][h] = sum_agents adopter[h] * n_adopt + baseline[h] * (n_cust - n_adopt)."""
     global _worker_conn
-    rows = []
-    for aid, row in static_agents_df.iterrows():
-        r = row.copy()
-        r.name = aid
-        rows.append(r)
-    if not rows:
+    if len(static_agents_df) == 0:
         return pd.DataFrame([]), {"mode": "simple", "n_hours": 0, "net_sum_kw": []}
-    sized, o = size_rows(rows, _worker_conn, rate_switch_table)
-    n_cust = np.array([_finite_float(s.get("customers_in_bin", 0.0), 0.0) for s in sized])
-    n_adopt = np.array([_finite_float(s.get("number_of_adopters", 0.0), 0.0) for s in sized])
+    df_out, o = size_frame(static_agents_df, _worker_conn, rate_switch_table, hourly=hourly, timing=timing)
+    num = lambda c: (np.array([_finite_float(v, 0.0) for v in df_out[c].tolist()], np.float64)
+                     if c in df_out else np.zeros(len(df_out)))
+    n_cust, n_adopt = num("customers_in_bin"), num("number_of_adopters")
     n_non = np.maximum(n_cust - n_adopt, 0.0)
-    adop = o["net_pvonly"].astype(np.float64)
-    base = o["baseline"].astype(np.float64)
     net_sum = np.zeros(NH)
-    for k in range(len(sized)):        # agent order, like the reference's running sum
-        net_sum += adop[k] * n_adopt[k] + base[k] * n_non[k]
-    out_rows = []
-    for s in sized:
-        for c in _DROP:
-            if c in s.index:
-                s = s.drop(labels=[c])
-        out_rows.append(s)
-    df_out = pd.DataFrame(out_rows)
+    adop, base = o["net_pvonly"], o["baseline"]
+    for k in range(len(df_out)):       # agent order, like the reference's running sum
+        if n_adopt[k] != 0.0 or n_non[k] != 0.0:
+            net_sum += adop[k].astype(np.float64) * n_adopt[k] + base[k].astype(np.float64) * n_non[k]
+    df_out = df_out.drop(columns=[c for c in _DROP if c in df_out.columns])
     agg = {"mode": "simple", "n_hours": NH, "net_sum_kw": net_sum.tolist()}
     return df_out, agg

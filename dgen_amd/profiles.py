@@ -56,6 +56,7 @@ class ProfileStore:
         self._cfs: List[np.ndarray] = []
         self._lidx: Dict[Tuple, int] = {}
         self._sidx: Dict[Tuple, int] = {}
+        self._stacked: Dict[str, Tuple[int, np.ndarray]] = {}
 
     # -- population -------------------------------------------------------
     def add_load(self, key, profile) -> int:
@@ -109,13 +110,32 @@ class ProfileStore:
     def ensure(self, agents) -> None:
         """Hook for sources that fetch lazily (no-op for the in-memory store)."""
 
+    def ensure_frame(self, df) -> None:
+        """ensure() over an agent DataFrame (one fetch per distinct key)."""
+
+    @property
+    def n_load(self) -> int:
+        return len(self._shapes)
+
+    @property
+    def n_solar(self) -> int:
+        return len(self._cfs)
+
+    def _stack(self, name: str, rows: List[np.ndarray], dtype) -> np.ndarray:
+        hit = self._stacked.get(name)
+        if hit is not None and hit[0] == len(rows):
+            return hit[1]
+        a = np.stack(rows) if rows else np.zeros((0, NH), dtype)
+        self._stacked[name] = (len(rows), a)
+        return a
+
     @property
     def shapes(self) -> np.ndarray:
-        return np.stack(self._shapes) if self._shapes else np.zeros((0, NH), np.float32)
+        return self._stack("shapes", self._shapes, np.float32)
 
     @property
     def cfs(self) -> np.ndarray:
-        return np.stack(self._cfs) if self._cfs else np.zeros((0, NH), np.int32)
+        return self._stack("cfs", self._cfs, np.int32)
 
 
 class SqlProfileSource(ProfileStore):
@@ -142,6 +162,11 @@ class SqlProfileSource(ProfileStore):
         finally:
             cur.close()
         return row
+
+    def ensure_frame(self, df) -> None:
+        cols = ["bldg_id", "sector_abbr", "state_abbr", "solar_re_9809_gid", "tilt", "azimuth"]
+        uniq = df[cols].drop_duplicates()
+        self.ensure([dict(zip(cols, r)) for r in uniq.itertuples(index=False, name=None)])
 
     def ensure(self, agents) -> None:
         for agent in agents:

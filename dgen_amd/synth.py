@@ -14,6 +14,7 @@ from dataclasses import dataclass
 from typing import Dict, Optional
 
 import numpy as np
+import pandas as pd
 
 from . import _lib
 from .columnar import assign_scratch, empty_columns
@@ -32,6 +33,9 @@ CONFIGS = {
     # they are compiled and billed (parity unpinned)
     "com_dc_batt": (4, "com", "nem_dc", "synthetic commercial, demand charges billed, with battery"),
     "national_mixed": (5, "mixed", "mixed", "national mixed population"),
+    # parity case (not a bench line): tariffs spread over SAM's metering
+    # options 0-4 (the reference passes ur_metering_option through, ff:586)
+    "metering_mix": (6, "mixed", "all", "mixed population, metering options 0-4"),
 }
 
 
@@ -112,7 +116,8 @@ def wholesale_rows(rng, n_rows: int) -> np.ndarray:
 def random_tariffs(rng, n: int, metering: str):
     """256-ish synthetic URDB-style tariffs: P 1..4, T 1..3 (mostly BIG caps),
     prices U[0.06, 0.40] $/kWh, fixed U[0, 25] $/month; legacy e_* and ur_*
-    forms mixed.  metering: 'nem' -> mo 0; 'nb' -> mo 2; 'mixed' -> 20 % mo 2."""
+    forms mixed.  metering: 'nem' -> mo 0; 'nb' -> mo 2; 'mixed' -> 20 % mo 2;
+    'all' -> uniform over options 0-4."""
     out = []
     for k in range(n):
         P = int(rng.integers(1, 5))
@@ -124,7 +129,10 @@ def random_tariffs(rng, n: int, metering: str):
         for p in range(1, P):
             wk[:, (on0 + 2 * p) % 24:(on0 + 2 * p + 3) % 24 or 24] = p
         we = np.zeros((12, 24), dtype=int)
-        mo = 0 if metering in ("nem", "nem_dc") else (2 if metering == "nb" else int(rng.random() < 0.2) * 2)
+        if metering == "all":
+            mo = int(rng.integers(0, 5))
+        else:
+            mo = 0 if metering in ("nem", "nem_dc") else (2 if metering == "nb" else int(rng.random() < 0.2) * 2)
         lv = None
         if T > 1:
             lv = np.sort(rng.choice([250.0, 400.0, 600.0, 900.0], size=(T, P)), axis=0)
@@ -287,3 +295,63 @@ def subset(pop: Population, idx) -> Population:
     return Population(shapes=pop.shapes, cfs=pop.cfs, wholesale=pop.wholesale, tariffs=pop.tariffs,
                       switches=pop.switches, cols=cols, n_scratch=n_scratch, config=pop.config,
                       state_ix=pick(pop.state_ix), demand=pop.demand, county_ix=pick(pop.county_ix))
+
+
+def reference_frame(n: int, seed: int = 20260811, n_load: int = 512, n_cf: int = 256, n_counties: int = 64,
+                    n_tariffs: int = 64, n_util: int = 300):
+    """An agent DataFrame in the reference's schema (the columns
+    calc_system_size_and_performance reads, ff:330-421) with the objects a
+    merged agent file carries: tariff dicts and per-county wholesale arrays
+    shared by the rows that merged them, profile keys into a ProfileStore,
+    and a rate_switch_table (elec.py:828-836 columns).  Returns (df, store,
+    switch_table).  For the drop-in path's tests and bench_dropin.py."""
+    from .profiles import ProfileStore
+    rng = np.random.default_rng(seed)
+    shapes = np.concatenate([load_shapes(rng, n_load // 2, False), load_shapes(rng, n_load - n_load // 2, True)])
+    cfs = solar_cfs(rng, n_cf)
+    whl = wholesale_rows(rng, n_counties)
+    whl_obj = [whl[c] for c in range(n_counties)]          # one array object per county
+    raws = random_tariffs(rng, n_tariffs, "mixed")
+    is_res = rng.random(n) < 0.8
+    st = np.array(STATES)[rng.integers(0, len(STATES), n)]
+    store = ProfileStore()
+    lrow = np.where(is_res, rng.integers(0, n_load // 2, n), n_load // 2 + rng.integers(0, n_load - n_load // 2, n))
+    crow = rng.integers(0, n_cf, n)
+    keys_l = {}
+    bldg = np.empty(n, np.int64)
+    for i in range(n):
+        k = (int(lrow[i]) + 100000, "res" if is_res[i] else "com", str(st[i]))
+        if k not in keys_l:
+            keys_l[k] = store.add_load(k, shapes[lrow[i]])
+        bldg[i] = k[0]
+    for j in range(n_cf):
+        store.add_solar((j + 7000, 25, 180), cfs[j])
+    county = rng.integers(0, n_counties, n)
+    eia = rng.integers(0, n_util, n)
+    tix = rng.integers(0, n_tariffs, n)
+    df = pd.DataFrame({
+        "agent_id": np.arange(n) * 2 + 1, "sector_abbr": np.where(is_res, "res", "com"), "state_abbr": st,
+        "bldg_id": bldg, "solar_re_9809_gid": crow + 7000, "tilt": 25, "azimuth": 180, "eia_id": eia,
+        "tariff_id": tix + 1000, "tariff_dict": [raws[k] for k in tix], "county_id": county,
+        "wholesale_prices": [whl_obj[c] for c in county],
+        "load_kwh_per_customer_in_bin": np.where(is_res, rng.lognormal(np.log(10000.0), 0.35, n),
+                                                 np.clip(rng.lognormal(np.log(150000.0), 1.2, n), 1e4, 5e7)),
+        "elec_price_multiplier": rng.uniform(0.9, 1.1, n), "elec_price_escalator": rng.uniform(-0.01, 0.01, n),
+        "economic_lifetime_yrs": 25, "loan_term_yrs": np.where(is_res, 20, 30), "inflation_rate": 0.025,
+        "pv_degradation_factor": 0.005, "down_payment_fraction": np.where(is_res, 0.3, 1.0), "tax_rate": 0.2574,
+        "real_discount_rate": np.where(is_res, 0.05, 0.0378), "itc_fraction_of_capex": 0.3,
+        "system_capex_per_kw": np.where(is_res, 4637.5, 1672.9),
+        "system_capex_per_kw_combined": np.where(is_res, 4500.0, 1600.0),
+        "batt_capex_per_kwh_combined": np.where(is_res, 431.0, 197.3), "cap_cost_multiplier": rng.uniform(0.9, 1.2, n),
+        "value_of_resiliency_usd": np.where(rng.random(n) < 0.2, rng.uniform(0.0, 300.0, n), 0.0),
+        "customers_in_bin": rng.uniform(10, 500, n),
+    }).set_index("agent_id", drop=False)
+    rows = []
+    for u in range(n_util):
+        for rc in ("R", "C"):
+            if rng.random() < 0.1:
+                k = int(rng.integers(0, n_tariffs))
+                rows.append({"tech": "solar", "rate_id_alias": 5000 + len(rows), "json": raws[k], "eia_id": u,
+                             "res_com": rc, "min_kw_limit": 0.0, "max_kw_limit": 10.0 if rc == "R" else 200.0,
+                             "one_time_charge": float(rng.uniform(0, 500))})
+    return df, store, pd.DataFrame(rows)

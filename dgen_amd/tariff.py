@@ -439,8 +439,10 @@ def pack_record(fields: Dict[str, Any]) -> np.ndarray:
     rec["fixed"] = float(fields["ur_monthly_fixed_charge"])
     mat = fields.get("ur_ec_tou_mat") or []
     flags = 0
-    if rec["mo"] not in (0, 2):
-        raise TariffError(f"metering option {int(rec['mo'])} is not produced by the reference path")
+    if rec["mo"] not in (0, 1, 2, 3, 4):
+        # SAM's ur_metering_option enumeration (the reference passes the
+        # tariff's value through to Utilityrate5, ff:586-588, 970-971)
+        raise TariffError(f"metering option {int(rec['mo'])} is not one of SAM's options 0-4")
     if not mat:
         flags |= ST_EMPTY_EC
         rec["P"], rec["T"] = 1, 1

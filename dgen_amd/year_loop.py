@@ -241,7 +241,8 @@ class YearLoop:
         self.hourly_export, self.hourly_chunk = bool(hourly_export), hourly_chunk
         n = len(pop.cols["load_kwh"])
         self.n = n
-        perm = profile_order(pop.cols) if order is None else np.asarray(order, np.int64)
+        perm = (profile_order(pop.cols, group=np.asarray(agents["state"])) if order is None
+                else np.asarray(order, np.int64))
         self.perm = perm
         inv = np.empty(n, np.int64)
         inv[perm] = np.arange(n, dtype=np.int64)
@@ -305,7 +306,12 @@ class YearLoop:
         s_idx = np.concatenate([np.asarray(v, np.int64) for v in s_first.values()]) if n else \
             np.zeros(0, np.int64)
         self.s_off = np.concatenate([[0], np.cumsum([len(v) for v in s_first.values()])]).astype(np.int64)
-        self.s_dev_idx = inv[s_idx]                   # device column of each state member
+        # device column of each state member, ascending within the state: with
+        # the state-major device order each state is one contiguous range and
+        # the export's plane reads are coalesced (the sum order is the
+        # kernel's own fixed order either way)
+        self.s_dev_idx = np.concatenate([np.sort(inv[np.asarray(v, np.int64)]) for v in s_first.values()]) \
+            if n else np.zeros(0, np.int64)
         self.s_dev = torch.as_tensor(self.s_dev_idx, device=dev)
         self.state_dev_order = np.asarray(st, np.int64)[perm]   # state of each device row
         # carry (market_last_year), device order

@@ -158,13 +158,27 @@ static double month_energy_charge(const orc_tariff* t, int m, const double* u) {
     return charge;
 }
 
-/* One year's bill (undiscounted, before the escalation factor).  mo 0: monthly
- * net kWh per period with per-period kWh credit carry-over, year-end true-up in
- * December at ur_nm_yearend_sell_rate.  mo 2: hourly imports billed, exports
- * credited at the period's tier-1 sell rate or the 8760 TS sell rate. */
-static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* net /*[12][P] mo0*/,
-                        const double* imp, const double* exv /*[12][P] $ or kWh*/, int ts) {
-    double total = 0.0;
+/* One year's bill (undiscounted, before the escalation factor), by metering
+ * option (SAM's enumeration; the reference passes the tariff's value through,
+ * ff:586-588, 970-971; only 0 and 2 have the reference's semantics pinned by
+ * its own code paths, all of them are SSC restatements, parity unpinned):
+ *   0  net metering, kWh credits: monthly net kWh per period, surplus kWh
+ *      carried per period, December true-up at ur_nm_yearend_sell_rate;
+ *   1  net metering, $ credits: monthly net kWh per period, imports billed,
+ *      surplus kWh credited at the period's tier-1 sell rate; the month's
+ *      energy bill floors at 0 with the excess $ carried to the next month
+ *      (lost at year end);
+ *   2  net billing: hourly imports billed, hourly exports credited at the
+ *      period's tier-1 sell rate or the 8760 TS sell rate;
+ *   3  net billing with carryover: as 2, the month's energy bill floors at 0
+ *      and the excess $ carries to the next month (lost at year end);
+ *   4  buy all / sell all: all load billed, all generation credited at the
+ *      period's tier-1 sell rate.
+ * Fixed charges are always billed. */
+static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* net /*[12][P]*/,
+                        const double* imp, const double* exv /*[12][P] $ or kWh*/, const double* lbin,
+                        const double* gbin, int ts) {
+    double total = 0.0, carry = 0.0;
     double credit[ORC_MAXP];
     for (int p = 0; p < ORC_MAXP; p++) credit[p] = 0.0;
     for (int m = 0; m < 12; m++) {
@@ -188,16 +202,40 @@ static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* n
                 for (int p = 0; p < t->P; p++) c += credit[p];
                 bill -= c * cfg->nm_yearend_sell_rate;
             }
+        } else if (t->mo == 1) {
+            double cr = 0.0;
+            for (int p = 0; p < t->P; p++) {
+                double n = net[m * ORC_MAXP + p];
+                u[p] = n > 0.0 ? n : 0.0;
+                cr += (n < 0.0 ? -n : 0.0) * t->sell[p][0];
+            }
+            double e = month_energy_charge(t, m, u) - cr - carry;
+            carry = e < 0.0 ? -e : 0.0;
+            bill += e < 0.0 ? 0.0 : e;
+        } else if (t->mo == 4) {
+            double cr = 0.0;
+            for (int p = 0; p < t->P; p++) {
+                u[p] = lbin[m * ORC_MAXP + p];
+                cr += gbin[m * ORC_MAXP + p] * t->sell[p][0];
+            }
+            bill += month_energy_charge(t, m, u) - cr;
         } else {
             double cr = 0.0;
             for (int p = 0; p < t->P; p++) u[p] = imp[m * ORC_MAXP + p];
-            bill += month_energy_charge(t, m, u);
+            double charge = month_energy_charge(t, m, u);
             if (ts) {
                 for (int p = 0; p < t->P; p++) cr += exv[m * ORC_MAXP + p];
             } else {
                 for (int p = 0; p < t->P; p++) cr += exv[m * ORC_MAXP + p] * t->sell[p][0];
             }
-            bill -= cr;
+            if (t->mo == 3) {
+                double e = charge - cr - carry;
+                carry = e < 0.0 ? -e : 0.0;
+                bill += e < 0.0 ? 0.0 : e;
+            } else {
+                bill += charge;
+                bill -= cr;
+            }
         }
         total += bill;
     }
@@ -207,13 +245,15 @@ static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* n
 /* Bins one year: gen scaled by s (degradation), hour by hour in time order. */
 static void bin_year(const orc_tariff* t, const int* mon, const int* per, const double* gen,
                      const double* load, const double* ts, double s, double* net, double* imp,
-                     double* exv) {
-    for (int i = 0; i < 12 * ORC_MAXP; i++) net[i] = imp[i] = exv[i] = 0.0;
+                     double* exv, double* lbin, double* gbin) {
+    for (int i = 0; i < 12 * ORC_MAXP; i++) net[i] = imp[i] = exv[i] = lbin[i] = gbin[i] = 0.0;
     for (int h = 0; h < ORC_NH; h++) {
         double g = gen ? gen[h] * s : 0.0;
         double d = load[h] - g;            /* > 0: import */
         int b = mon[h] * ORC_MAXP + per[h];
         net[b] += d;
+        lbin[b] += load[h];
+        gbin[b] += g;
         if (d > 0.0) {
             imp[b] += d;
         } else {
@@ -276,18 +316,19 @@ int orc_ur5(const orc_tariff* t, const orc_cfg* cfg, const double* gen, const do
     int ts = (t->mo == 2) && ts_sell != NULL;
     const double* tsp = ts ? ts_sell : NULL;
     double net[12 * ORC_MAXP], imp[12 * ORC_MAXP], exv[12 * ORC_MAXP];
+    double lbin[12 * ORC_MAXP], gbin[12 * ORC_MAXP];
     double rate_base = 1.0 + inflation_pct * 0.01 + escal_pct * 0.01;
     double sys_base = 1.0 - degr_pct * 0.01;
 
-    bin_year(t, mon, per, NULL, load, tsp, 1.0, net, imp, exv);
-    double wo1 = year_bill(t, cfg, net, imp, exv, ts);
+    bin_year(t, mon, per, NULL, load, tsp, 1.0, net, imp, exv, lbin, gbin);
+    double wo1 = year_bill(t, cfg, net, imp, exv, lbin, gbin, ts);
     if (t->dc_on) wo1 += year_demand(t, NULL, load, 1.0);
     bill_w[0] = bill_wo[0] = aev[0] = 0.0;
     for (int i = 0; i < nyears; i++) {
         double r = pow_int(rate_base, i);
         double s = pow_int(sys_base, i);
-        bin_year(t, mon, per, gen, load, tsp, s, net, imp, exv);
-        double wb = year_bill(t, cfg, net, imp, exv, ts);
+        bin_year(t, mon, per, gen, load, tsp, s, net, imp, exv, lbin, gbin);
+        double wb = year_bill(t, cfg, net, imp, exv, lbin, gbin, ts);
         if (t->dc_on) wb += year_demand(t, gen, load, s);
         double w = wb * r;
         double wo = wo1 * r;

@@ -120,3 +120,48 @@ def test_sql_source_runs_reference_queries():
     src.ensure(agents)
     assert np.array_equal(src.shapes[src.load_row(agents[0])], arr["shapes"][1])
     assert np.array_equal(src.cfs[src.solar_row(agents[0])], arr["cfs"][0])
+
+
+def _frame_vs_rows(df, store, table):
+    from dgen_amd.columnar import columnize_frame
+    rows = []
+    for aid, row in df.iterrows():
+        r = row.copy()
+        r.name = aid
+        rows.append(r)
+    b1 = ff._columnarize(rows, store, table)
+    c1 = b1.columns()
+    b2 = columnize_frame(df, store, table)
+    c2 = b2.frame_columns
+    for k in c1:
+        assert np.array_equal(c1[k], c2[k], equal_nan=True), k
+        assert c1[k].dtype == c2[k].dtype, k
+    assert np.array_equal(b1.tariffs.array(), b2.tariffs.array())
+    assert np.array_equal(b1.switches.array(), b2.switches.array())
+    w1, w2 = b1.wholesale.array(), b2.wholesale.array()
+    assert (w1 is None and w2 is None) or np.array_equal(w1, w2)
+
+
+def test_columnize_frame_matches_row_builder_golden():
+    rows, store, table = helpers.golden_rows()
+    _frame_vs_rows(pd.DataFrame(rows), store, table)
+
+
+def test_columnize_frame_matches_row_builder_synthetic():
+    """Shared tariff dicts / wholesale arrays (as merges leave them), CA rows,
+    rate-switch candidates, and wholesale arrays that only some multipliers
+    make non-finite in float32 (the row enters the table at its first valid
+    use, as in the row builder)."""
+    from dgen_amd.synth import reference_frame
+    df, store, table = reference_frame(3000, seed=11)
+    # the same county array with a multiplier that overflows float32 first
+    big = np.full(8760, 1e36)
+    idx = df.index[df["state_abbr"] != "CA"][:6]
+    df.loc[idx[:3], "wholesale_prices"] = pd.Series([big, big, big], index=idx[:3])
+    df.loc[idx[0], "elec_price_multiplier"] = 1e3          # 1e39 -> inf in f32: no TS row
+    df.loc[idx[1], "elec_price_multiplier"] = 1.0
+    nan_arr = np.full(8760, 0.03)
+    nan_arr[5] = np.nan
+    df.loc[idx[3:5], "wholesale_prices"] = pd.Series([nan_arr, nan_arr], index=idx[3:5])
+    df.loc[idx[5], "wholesale_prices"] = None
+    _frame_vs_rows(df, store, table)

@@ -17,7 +17,7 @@ from tests import helpers
 pytestmark = pytest.mark.gpu
 
 CASES = [("de_res", 300), ("res_1m_nem_tou", 600), ("ca_res_storage", 300), ("com_8m", 200),
-         ("national_mixed", 400)]
+         ("national_mixed", 400), ("metering_mix", 400)]
 
 
 def _small_pop(cfg, n):

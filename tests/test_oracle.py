@@ -159,3 +159,37 @@ def test_oracle_demand_charge_known_answer():
     c = orc.ur5(t_dc, cfg, gen2, load, None, 1, 2.5, 0.0, 0.0)
     d = orc.ur5(t_plain, cfg, gen2, load, None, 1, 2.5, 0.0, 0.0)
     assert c["bill_w"][1] - d["bill_w"][1] == pytest.approx(12 * 10.0 * L, rel=1e-12)
+
+
+@pytest.mark.parametrize("gen_kw,expect", [
+    # gen kW in hours 10-13 against a flat 1 kW load; $0.20 buy, $0.05 sell, one period
+    # (daily: load 24 kWh, generation 4 g, imports 20, exports 4 (g - 1))
+    (3.0, {0: 876.0, 1: 876.0, 2: 1314.0, 3: 1314.0, 4: 1533.0}),
+    (10.0, {0: -16 * 365 * 0.02, 1: 0.0, 2: 803.0, 3: 803.0, 4: 1022.0}),
+    (30.0, {0: -96 * 365 * 0.02, 1: 0.0, 2: -657.0, 3: 0.0, 4: 365 * (4.8 - 6.0)}),
+])
+def test_oracle_metering_options_known_answer(gen_kw, expect):
+    """Year-1 bills of SAM's five metering options (oracle/orc.c year_bill):
+    0 NEM kWh credits trued up at the year-end rate, 1 NEM $ credits floored
+    monthly (excess lost at year end), 2 net billing, 3 net billing with $
+    carryover floored monthly, 4 buy all / sell all."""
+    from tests.helpers import oracle_tariffs
+    from dgen_amd.tariff import TariffTable
+    ones = [[1] * 24 for _ in range(12)]
+    tt = TariffTable()
+    for mo in range(5):
+        tt.add({"ur_ec_tou_mat": [[1, 1, 1e38, 0, 0.2, 0.05]], "ur_ec_sched_weekday": ones,
+                "ur_ec_sched_weekend": ones, "ur_metering_option": mo}, False)
+    ts = oracle_tariffs(tt.array())
+    cfg = orc.make_cfg()
+    load = np.ones(orc.NH)
+    gen = np.zeros(orc.NH)
+    hod = np.arange(orc.NH) % 24
+    gen[(hod >= 10) & (hod < 14)] = gen_kw
+    for mo in range(5):
+        assert int(tt.array()["mo"][mo]) == mo
+        r = orc.ur5(ts[mo], cfg, gen, load, None, 1, 0.0, 0.0, 0.0)
+        # the compiler rounds rates to float32 (0.2 -> 0.2000000030): rel 1e-7
+        assert r["bill_w"][1] == pytest.approx(expect[mo], rel=1e-7, abs=1e-6), mo
+        # no system: every option bills the 24 kWh / day of load
+        assert r["bill_wo"][1] == pytest.approx(24 * 365 * 0.2, rel=1e-7), mo
