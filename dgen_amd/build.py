@@ -6,10 +6,12 @@ the repository snapshot.
 """
 from __future__ import annotations
 
+import json
 import os
 import shutil
 import subprocess
 import sys
+import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -39,21 +41,65 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__))
+    return any(os.path.getmtime(p) > t for p in (SRC, HDR, __file__, os.path.join(HERE, "spill_guard.py")))
+
+
+GUARD = os.path.join(OUT_DIR, "build_guard.json")
+
+
+def _compile(defines, verbose):
+    """One hipcc run in a scratch directory with -save-temps: the library and
+    the gfx950 assembly it was assembled from."""
+    work = tempfile.mkdtemp(prefix="dgen_build_")
+    tmp = os.path.join(work, "libdgen_hip.so")
+    cmd = [hipcc(), *FLAGS, *[f"-D{d}=1" for d in defines], "-save-temps", "-o", tmp, SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True, cwd=work)
+    if res.returncode != 0:
+        shutil.rmtree(work, ignore_errors=True)
+        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
+    asm = [f for f in os.listdir(work) if f.endswith(f"-hip-amdgcn-amd-amdhsa-{ARCH}.s")]
+    if not asm:
+        shutil.rmtree(work, ignore_errors=True)
+        raise RuntimeError("hipcc -save-temps left no device assembly to check")
+    return work, tmp, os.path.join(work, asm[0])
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile, then check the device assembly with the spill guard
+    (dgen_amd/spill_guard.py): a 32-lane kernel that spills a live value
+    ahead of a divergent branch's exec restore is withdrawn (its batches run
+    one agent per wave) and the library rebuilt; a flagged kernel without
+    that remedy fails the build.  The outcome is written to
+    dgen_amd/lib/build_guard.json."""
+    from . import spill_guard
     if not force and not needs_build():
         return OUT
     os.makedirs(OUT_DIR, exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-o", tmp, SRC]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
-    os.replace(tmp, OUT)
+    defines = []
+    first = None
+    for attempt in range(2):
+        work, lib, asm = _compile(defines, verbose)
+        try:
+            hits = spill_guard.scan(asm)
+            if attempt == 0:
+                first = {k: [b for b, _ in v] for k, v in hits.items()}
+            if not hits:
+                shutil.copyfile(lib, OUT + ".tmp")
+                os.replace(OUT + ".tmp", OUT)
+                break
+            macros, fatal = spill_guard.remedies(hits)
+            if fatal or attempt == 1 or set(macros) <= set(defines):
+                raise RuntimeError("spill guard: the compiled kernels spill live values ahead of an exec "
+                                   "restore (inactive lanes would reload stale data):\n" + spill_guard.report(hits))
+            defines = sorted(set(defines) | set(macros))
+            if verbose:
+                print("spill guard withdrew:", ", ".join(macros), flush=True)
+        finally:
+            shutil.rmtree(work, ignore_errors=True)
+    with open(GUARD, "w") as f:
+        json.dump({"flagged_first_build": first, "withdrawn": defines}, f, indent=1)
     return OUT
 
 

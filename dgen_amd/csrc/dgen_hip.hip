@@ -33,6 +33,23 @@
 
 #include "../../include/dgen_hip.h"
 
+// Two-agents-per-wave (32-lane) instantiations withdrawn by the build guard
+// (dgen_amd/spill_guard.py): set to 1 by dgen_amd/build.py when the compiled
+// kernel spills a live value ahead of a divergent branch's exec restore, so
+// that its batches run one agent per wave (wave-uniform branches) instead.
+#ifndef DGEN_NO2_SIZE
+#define DGEN_NO2_SIZE 0
+#endif
+#ifndef DGEN_NO2_SIZE_DC
+#define DGEN_NO2_SIZE_DC 0
+#endif
+#ifndef DGEN_NO2_FIN
+#define DGEN_NO2_FIN 0
+#endif
+#ifndef DGEN_NO2_FIN_DC
+#define DGEN_NO2_FIN_DC 0
+#endif
+
 namespace {
 
 constexpr int NH = DGEN_NH;
@@ -1395,7 +1412,17 @@ __device__ __forceinline__ double dc_tier_charge(double peak, const double* cap,
 // only the imports' own rounding differs from the oracle.  The TOU peaks live
 // in the lane's LDS column (S.at(0 .. DCP-1); the host sizes it, see
 // dgen_size_agents): held in registers they pushed k_size into spills.
-__device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& src, double s,
+// The reference's per-hour PV output at kW (ff:117-119, dc -> ac -> kWh), in
+// its own operation order: demand charges bill maxima, where a last-bit
+// difference can move a Brent comparison at a kink, so the demand passes form
+// each hour's generation exactly as the reference (and the oracle) does.
+__device__ __forceinline__ double ref_gen(double gpk, double kw) {
+    return (((gpk * kw) * 1000.0) * 0.96) / 1000.0;
+}
+
+// kw: the search's system kW (PV-only case; the battery case reads the
+// system-output plane, src.sysgen)
+__device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& src, double kw, double s,
                                            bool with_gen, const YLds& S) {
     double total = 0.0;
     int h = 0;
@@ -1424,10 +1451,10 @@ __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& sr
 #pragma unroll
                     for (int k = 0; k < 3; k++) {
                         const int4 cv = *reinterpret_cast<const int4*>(src.cf + h + 4 * k);
-                        g[4 * k] = cf_per_kw(cv.x) * src.gen_scale;
-                        g[4 * k + 1] = cf_per_kw(cv.y) * src.gen_scale;
-                        g[4 * k + 2] = cf_per_kw(cv.z) * src.gen_scale;
-                        g[4 * k + 3] = cf_per_kw(cv.w) * src.gen_scale;
+                        g[4 * k] = ref_gen(cf_per_kw(cv.x), kw);
+                        g[4 * k + 1] = ref_gen(cf_per_kw(cv.y), kw);
+                        g[4 * k + 2] = ref_gen(cf_per_kw(cv.z), kw);
+                        g[4 * k + 3] = ref_gen(cf_per_kw(cv.w), kw);
                     }
                 } else {
 #pragma unroll
@@ -1462,7 +1489,7 @@ __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& sr
 // the lines above M(t*) (a relative slack of 1e-10 keeps the set a superset
 // under rounding); an evaluation then takes the max over <= DC_NL lines per
 // group instead of re-scanning 8760 hours, with the hourly pass's arithmetic
-// per line (L = shape x load_scale, g = cf / 1e6, import = L - (g x kW') x s),
+// per line (L = shape x load_scale, g = cf / 1e6, import = L - ref_gen(g, kW) x s),
 // so the peaks are the hourly pass's peaks.  A group that needs more lines
 // sends the agent back to the hourly pass (yl_demand).
 // ---------------------------------------------------------------------------
@@ -1561,9 +1588,9 @@ __device__ bool yl_dc_build(const dgen_demand* D, const YSrc& src, double tlo, d
 }
 
 // One lane's year of demand charges from the envelopes (same month / period /
-// tier order as yl_demand): system output x s at generation kW' kws, or the
-// no-system peaks (max load) when !with_gen.
-__device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& E, double kws, double s,
+// tier order as yl_demand): system output x s at system kW kw (ref_gen, the
+// reference's operation order), or the no-system peaks (max load) when !with_gen.
+__device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& E, double kw, double s,
                                              bool with_gen, const YLds& S) {
     double total = 0.0;
     for (int m = 0; m < 12; m++) {
@@ -1576,7 +1603,7 @@ __device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& 
                     const double2* ln = E.lines + (m * DCP + q) * DC_NL;
                     for (int k = 0; k < n_l; k++) {
                         const double2 v = ln[k];
-                        const double imp = v.x - (v.y * kws) * s;
+                        const double imp = v.x - ref_gen(v.y, kw) * s;
                         pk = imp > pk ? imp : pk;
                     }
                 } else {
@@ -2014,8 +2041,8 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
             for (int pass = c.dem_wo_pending ? 0 : 1; pass < 2; pass++) {
                 const bool wg = pass == 1;
                 const double s = wg ? c.s_y : 1.0;
-                const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kws, s, wg, c.S)
-                                          : yl_demand(c.dem, c.src, s, wg, c.S);
+                const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, s, wg, c.S)
+                                          : yl_demand(c.dem, c.src, kw, s, wg, c.S);
                 if (wg) wb += v;
                 else c.wo1 += v;
             }
@@ -2258,7 +2285,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     if (DC && dem) {   // k_size's first_without already carries the no-system demand charge
         for (int pass = same_tariff ? 1 : 0; pass < 2; pass++) {
             const bool wg = pass == 1;
-            const double v = yl_demand(dem, src, wg ? s_y : 1.0, wg, S);
+            const double v = yl_demand(dem, src, 0.0, wg ? s_y : 1.0, wg, S);
             if (wg) wb += v;
             else wo1 += v;
         }
@@ -3000,10 +3027,13 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->nch[slot] = nch;
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK +
                        (size_t)(BLOCK / 64) * HB_DAY_BYTES;
-    // two agents per wave when every analysis period fits 32 lanes
-    const int lpa = (A->max_years >= 1 && A->max_years <= 32) ? 32 : WAVE;
-    const size_t ylds = ylds_bytes(lds_half(T->max_periods), lpa);
-    const int apb = WAVE / lpa;   // agents per year-lane block
+    // two agents per wave when every analysis period fits 32 lanes, unless the
+    // build guard withdrew that kernel's 32-lane instantiation (DGEN_NO2_*)
+    const bool fits32 = A->max_years >= 1 && A->max_years <= 32;
+    const int lpa_s = (fits32 && !(dc ? DGEN_NO2_SIZE_DC : DGEN_NO2_SIZE)) ? 32 : WAVE;
+    const int lpa_f = (fits32 && !(dc ? DGEN_NO2_FIN_DC : DGEN_NO2_FIN)) ? 32 : WAVE;
+    const size_t ylds_s = ylds_bytes(lds_half(T->max_periods), lpa_s);
+    const size_t ylds_f = ylds_bytes(lds_half(T->max_periods), lpa_f);
     hipStream_t s2 = c->s2;
     char* const nbws = n_scratch > 0 ? ws_nb(ws, n, n_scratch) : nullptr;
     HIP_TRY(hipEventRecord(c->fork, s));
@@ -3012,19 +3042,26 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         const int64_t i0 = (int64_t)j * csz, i1 = (i0 + csz < n) ? i0 + csz : n, m = i1 - i0;
         hipEvent_t* e = c->ev[slot][j];
         HIP_TRY(hipEventRecord(e[0], s));
-        const dim3 ygrid((unsigned)((m + apb - 1) / apb));
-        if (lpa == 32 && !dc)
-            hipLaunchKernelGGL((k_size_w<32, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               nullptr, nbws);
-        else if (lpa == 32)
-            hipLaunchKernelGGL((k_size_w<32, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               c->dc_buf, nbws);
-        else if (!dc)
-            hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               nullptr, nbws);
-        else
-            hipLaunchKernelGGL((k_size_w<WAVE, true>), ygrid, dim3(WAVE), ylds, s, *T, *A, *O, c->cfg, n, i0, i1,
-                               c->dc_buf, nbws);
+        // agents per year-lane block: WAVE / lpa
+        const dim3 ygrid_s((unsigned)((m + WAVE / lpa_s - 1) / (WAVE / lpa_s)));
+        const dim3 ygrid_f((unsigned)((m + WAVE / lpa_f - 1) / (WAVE / lpa_f)));
+        if (lpa_s == 32 && !dc) {
+#if !DGEN_NO2_SIZE
+            hipLaunchKernelGGL((k_size_w<32, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n, i0,
+                               i1, nullptr, nbws);
+#endif
+        } else if (lpa_s == 32) {
+#if !DGEN_NO2_SIZE_DC
+            hipLaunchKernelGGL((k_size_w<32, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n, i0,
+                               i1, c->dc_buf, nbws);
+#endif
+        } else if (!dc) {
+            hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n, i0,
+                               i1, nullptr, nbws);
+        } else {
+            hipLaunchKernelGGL((k_size_w<WAVE, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n, i0,
+                               i1, c->dc_buf, nbws);
+        }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
         HIP_TRY(hipEventRecord(e[2], s2));
@@ -3039,20 +3076,25 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                                    ws, n_scratch, i0, i1, m0, m1, c->battery);
         }
         HIP_TRY(hipEventRecord(e[3], s2));
-        if (!c->battery)
-            ;   // PV-only variant: no battery-case bill / cash flow
-        else if (lpa == 32 && !dc)
-            hipLaunchKernelGGL((k_batt_finance_w<32, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
-                               n, ws, n_scratch, i0, i1, nbws);
-        else if (lpa == 32)
-            hipLaunchKernelGGL((k_batt_finance_w<32, true>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O, c->cfg,
-                               n, ws, n_scratch, i0, i1, nbws);
-        else if (!dc)
-            hipLaunchKernelGGL((k_batt_finance_w<WAVE, false>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O,
+        if (!c->battery) {
+            // PV-only variant: no battery-case bill / cash flow
+        } else if (lpa_f == 32 && !dc) {
+#if !DGEN_NO2_FIN
+            hipLaunchKernelGGL((k_batt_finance_w<32, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
                                c->cfg, n, ws, n_scratch, i0, i1, nbws);
-        else
-            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true>), ygrid, dim3(WAVE), ylds, s2, *T, *A, *O,
+#endif
+        } else if (lpa_f == 32) {
+#if !DGEN_NO2_FIN_DC
+            hipLaunchKernelGGL((k_batt_finance_w<32, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
                                c->cfg, n, ws, n_scratch, i0, i1, nbws);
+#endif
+        } else if (!dc) {
+            hipLaunchKernelGGL((k_batt_finance_w<WAVE, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
+                               c->cfg, n, ws, n_scratch, i0, i1, nbws);
+        } else {
+            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
+                               c->cfg, n, ws, n_scratch, i0, i1, nbws);
+        }
         HIP_TRY(hipEventRecord(e[4], s2));
     }
     HIP_TRY(hipEventRecord(c->join, s2));

@@ -21,6 +21,10 @@ import pandas as pd
 from . import _lib
 
 ANCHOR_YEARS = (2014, 2016, 2018)
+# config.OBSERVED_DEPLOYMENT_BY_STATE of the reference (config.py:67): the CSV of
+# observed PV / storage deployment by (state, sector, year) that the anchor
+# years rescale to.  Set it, or pass observed_deployment= to calc_diffusion_solar.
+OBSERVED_DEPLOYMENT_BY_STATE = None
 
 _LAST_YEAR_COLS = ['agent_id', 'market_share', 'max_market_share', 'number_of_adopters',
                    'market_value', 'initial_number_of_adopters', 'initial_pv_kw', 'initial_batt_kw',
@@ -149,14 +153,65 @@ def diffusion_arrays(engine, cols: Dict[str, np.ndarray], is_first_year: bool) -
     return {k: v.cpu().numpy() for k, v in outs.items()}
 
 
+def _observed_table(observed_deployment) -> pd.DataFrame:
+    src = observed_deployment if observed_deployment is not None else OBSERVED_DEPLOYMENT_BY_STATE
+    if src is None:
+        raise FileNotFoundError("anchor years (2014/2016/2018) need the observed deployment table: "
+                                "set dgen_amd.diffusion.OBSERVED_DEPLOYMENT_BY_STATE (the reference's "
+                                "config.OBSERVED_DEPLOYMENT_BY_STATE) or pass observed_deployment=")
+    obs = src if isinstance(src, pd.DataFrame) else pd.read_csv(src)
+    if obs.duplicated(subset=['state_abbr', 'sector_abbr', 'year']).any():
+        raise ValueError("observed deployment table has duplicate (state, sector, year) rows: the "
+                         "reference's merge would duplicate agent rows")
+    return obs
+
+
+def anchor_to_observed(eng, df: pd.DataFrame, observed: pd.DataFrame) -> pd.DataFrame:
+    """diffusion_functions_elec.py:99-133 -- in an anchor year, rescale each
+    agent's PV cumulative capacity so its (state, sector, year) group totals
+    the observed MW, then re-derive adopters and market share from it (battery
+    columns untouched).  The group totals are device segment sums
+    (dgen_segment_sums, fixed order) over the agents sorted by group; pandas'
+    groupby sum skips NaN, so NaN capacities enter as 0.  Rows whose group key
+    has a NaN, or whose group the table lacks, get NaN capacity like the
+    reference's left merges."""
+    import torch
+    group_cols = ['state_abbr', 'sector_abbr', 'year']
+    n = len(df)
+    gid = df.groupby(group_cols, sort=False, dropna=True).ngroup().to_numpy(np.int64)
+    ok = gid >= 0
+    G = int(gid.max()) + 1 if ok.any() else 0
+    order = np.argsort(np.where(ok, gid, G), kind="stable")[:int(ok.sum())]
+    cnt = np.bincount(gid[ok], minlength=G)
+    off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    kw = df['system_kw_cum'].to_numpy(dtype=np.float64)
+    v = eng._to_dev(np.nan_to_num(kw[order], nan=0.0, posinf=np.inf, neginf=-np.inf), torch.float64)
+    tot = eng.segment_sums(v, off)[:, 0].cpu().numpy() if G else np.zeros(0)
+    state_sum = np.full(n, np.nan)
+    count = np.full(n, np.nan)
+    state_sum[ok] = tot[gid[ok]]
+    count[ok] = cnt[gid[ok]]
+    df = pd.merge(df, observed, how='left', on=group_cols)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        scale = np.where(state_sum == 0, 1.0 / count, kw / state_sum)
+    cum = scale * df['observed_solar_mw'].to_numpy(dtype=np.float64) * 1000.0
+    df['system_kw_cum'] = cum
+    df['number_of_adopters'] = np.where(df['sector_abbr'] == 'res', cum / 5.0, cum / 100.0)
+    w = df['developable_agent_weight'].to_numpy(dtype=np.float64)
+    with np.errstate(divide='ignore', invalid='ignore'):
+        df['market_share'] = np.where(w == 0, 0.0, df['number_of_adopters'].to_numpy() / w).astype(np.float64)
+    return df.drop(columns=['observed_solar_mw'])
+
+
 def calc_diffusion_solar(df, is_first_year, bass_params, year, override_p_value=None,
-                         override_q_value=None, override_teq_yr1_value=None, engine=None):
+                         override_q_value=None, override_teq_yr1_value=None, engine=None,
+                         observed_deployment=None):
     """diffusion_functions_elec.py:24 -- PV Bass diffusion for the solve year.
-    (The reference accepts but does not apply the override_* arguments.)"""
+    (The reference accepts but does not apply the override_* arguments.)
+    In the anchor years 2014/2016/2018 the PV cumulatives are rescaled to the
+    observed deployment table (anchor_to_observed)."""
     from .financial_functions import get_engine
-    if year in ANCHOR_YEARS:
-        raise NotImplementedError("historical anchoring years (2014/2016/2018) read "
-                                  "config.OBSERVED_DEPLOYMENT_BY_STATE; model years start in 2026")
+    observed = _observed_table(observed_deployment) if year in ANCHOR_YEARS else None
     eng = engine or get_engine()
     df = df.reset_index()
     bass_params = bass_params[bass_params['tech'] == 'solar']
@@ -181,5 +236,7 @@ def calc_diffusion_solar(df, is_first_year, bass_params, year, override_p_value=
     df['system_kw_cum'] = o['system_kw_cum']
     df['batt_kw_cum'] = df['batt_kw_cum_last_year']
     df['batt_kwh_cum'] = df['batt_kwh_cum_last_year']
+    if observed is not None:
+        df = anchor_to_observed(eng, df, observed)
     market_last_year = df[_LAST_YEAR_COLS].rename(columns=_LAST_YEAR_RENAME)
     return df, market_last_year

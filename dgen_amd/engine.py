@@ -362,19 +362,30 @@ def tile_hourly(p):
 
 def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
     """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly),
-    in caller order when `perm` (AgentBatch.perm) is given."""
+    in caller order when `perm` (AgentBatch.perm) is given.  The reorder to
+    caller order (and the hourly tiles' transpose) is one device gather per
+    array, so each crosses PCIe once, already in its final layout."""
+    torch = _torch()
     res = {}
+    inv = None
+    if perm is not None:
+        p = np.asarray(perm, np.int64)
+        iv = np.empty_like(p)
+        iv[p] = np.arange(p.size, dtype=np.int64)
+        dev = next(v.device for v in out.values() if v is not None and hasattr(v, "device"))
+        inv = torch.as_tensor(iv, device=dev)
+    host = lambda t: (t if inv is None else t.index_select(0, inv)).cpu().numpy()
     for name, _ in _lib.OUTPUT_SCALARS:
-        res[name] = out[name].cpu().numpy()
+        res[name] = host(out[name])
     for name in _lib.OUTPUT_YEARLY:
-        res[name] = out[name].cpu().numpy()
+        res[name] = host(out[name])
     for name in _lib.OUTPUT_HOURLY:
         t = out.get(name)
-        res[name] = None if t is None else hourly_agent_major(t).cpu().numpy()
-    if perm is not None:
-        for k, v in res.items():
-            if v is not None:
-                u = np.empty_like(v)
-                u[perm] = v
-                res[k] = u
+        if t is None:
+            res[name] = None
+        elif inv is None:
+            res[name] = hourly_agent_major(t).cpu().numpy()
+        else:
+            q, n, four = t.shape
+            res[name] = t.permute(1, 0, 2).index_select(0, inv).reshape(n, q * four).cpu().numpy()
     return res

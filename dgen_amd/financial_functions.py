@@ -148,9 +148,15 @@ def _device_tables(eng, src: ProfileStore, b: PopulationBuilder):
     eng.set_switches(b.switches.array())
 
 
-def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[dict] = None):
+def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[dict] = None,
+                net_weights: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+    """Size the batch; net_weights = (number_of_adopters, non-adopters) per
+    caller row also returns o["net_sum_kw"], size_chunk's hourly aggregate
+    summed on the device from the planes in place (k_state_hourly, one
+    segment, fixed order) instead of a host loop over the agents."""
     import time
     import torch
+    from .attachment import state_hourly
     from .engine import outputs_to_host, profile_order
     eng = get_engine()
     t0 = time.perf_counter()
@@ -160,9 +166,19 @@ def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[
     torch.cuda.synchronize(eng.dev)
     t1 = time.perf_counter()
     eng.size(batch, out)
+    net = None
+    if net_weights is not None:
+        perm = batch.perm if batch.perm is not None else np.arange(batch.n)
+        na = eng._to_dev(np.asarray(net_weights[0], np.float64)[perm], torch.float64)
+        nn = eng._to_dev(np.asarray(net_weights[1], np.float64)[perm], torch.float64)
+        pv = out["net_pvonly"]
+        net = state_hourly(eng, (out["baseline"], pv, pv), (na, torch.zeros_like(na), nn), None,
+                           [0, batch.n])[0] * 1000.0
     torch.cuda.synchronize(eng.dev)
     t2 = time.perf_counter()
     o = outputs_to_host(out, batch.perm)
+    if net is not None:
+        o["net_sum_kw"] = net.cpu().numpy()
     if timing is not None:
         timing.update(upload_s=t1 - t0, device_s=t2 - t1, download_s=time.perf_counter() - t2)
     return o
@@ -254,11 +270,17 @@ _DROP = ("adopter_load_hourly", "adopter_pv_hourly", "adopter_batt_to_load_hourl
 
 
 def _yearly_lists(a: np.ndarray, n1: np.ndarray):
-    return [a[i, :n1[i]].tolist() for i in range(a.shape[0])]
+    """Row i's first n1[i] values as a Python list, one tolist() per distinct
+    analysis length (the frame usually has one or two)."""
+    out = np.empty(a.shape[0], dtype=object)
+    for n in np.unique(n1):
+        ix = np.nonzero(n1 == n)[0]
+        out[ix] = a[ix, :n].tolist() if ix.size > 1 else [a[ix[0], :n].tolist()]
+    return list(out)
 
 
 def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
-               timing: Optional[dict] = None):
+               timing: Optional[dict] = None, net_weights=None):
     """The batched form of calc_system_size_and_performance over a whole agent
     frame (what size_chunk needs), built by column: the frame is columnised
     at once (columnar.columnize_frame), sized in one device call, and the
@@ -277,7 +299,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     cols = b.frame_columns
     t1 = time.perf_counter()
     dev_t: dict = {}
-    o = _run_device(b, cols, src, dev_t)
+    o = _run_device(b, cols, src, dev_t, net_weights)
     t2 = time.perf_counter()
     ids = df["agent_id"].tolist() if "agent_id" in df else list(df.index)
     _raise_for_status(o["status"], ids)
@@ -340,16 +362,16 @@ def size_chunk(static_agents_df: pd.DataFrame, sectors, rate_switch_table, mode=
     global _worker_conn
     if len(static_agents_df) == 0:
         return pd.DataFrame([]), {"mode": "simple", "n_hours": 0, "net_sum_kw": []}
-    df_out, o = size_frame(static_agents_df, _worker_conn, rate_switch_table, hourly=hourly, timing=timing)
-    num = lambda c: (np.array([_finite_float(v, 0.0) for v in df_out[c].tolist()], np.float64)
-                     if c in df_out else np.zeros(len(df_out)))
+    df = static_agents_df
+    num = lambda c: (np.array([_finite_float(v, 0.0) for v in df[c].tolist()], np.float64)
+                     if c in df else np.zeros(len(df)))
     n_cust, n_adopt = num("customers_in_bin"), num("number_of_adopters")
     n_non = np.maximum(n_cust - n_adopt, 0.0)
-    net_sum = np.zeros(NH)
-    adop, base = o["net_pvonly"], o["baseline"]
-    for k in range(len(df_out)):       # agent order, like the reference's running sum
-        if n_adopt[k] != 0.0 or n_non[k] != 0.0:
-            net_sum += adop[k].astype(np.float64) * n_adopt[k] + base[k].astype(np.float64) * n_non[k]
+    # net_sum_kw[h] = sum_agents adopter[h] * n_adopt + baseline[h] * n_non (ff:1186),
+    # on the device; the reference's running sum in agent order and the
+    # kernel's fixed-order tree agree to rounding (parity test: 1e-12 relative)
+    df_out, o = size_frame(df, _worker_conn, rate_switch_table, hourly=hourly, timing=timing,
+                           net_weights=(n_adopt, n_non))
     df_out = df_out.drop(columns=[c for c in _DROP if c in df_out.columns])
-    agg = {"mode": "simple", "n_hours": NH, "net_sum_kw": net_sum.tolist()}
+    agg = {"mode": "simple", "n_hours": NH, "net_sum_kw": o["net_sum_kw"].tolist()}
     return df_out, agg

@@ -4,12 +4,16 @@
     calc_equiv_time             diffusion_functions_elec.py:343-372
     calc_diffusion_market_share diffusion_functions_elec.py:251-292
     bass_diffusion              diffusion_functions_elec.py:323-338
-    calc_diffusion_solar        diffusion_functions_elec.py:24-156 (non-anchor years)
+    calc_diffusion_solar        diffusion_functions_elec.py:24-156
+    anchor-year rescale         diffusion_functions_elec.py:99-133 (anchor())
 
-Pinned by tests/golden/diffusion.json (the reference's own functions run on a
-synthetic frame, make_golden.py).
+Pinned by tests/golden/diffusion.json and tests/golden/anchor.json (the
+reference's own functions run on synthetic frames, make_golden.py /
+make_golden_anchor.py).
 """
 import numpy as np
+
+from oracle.market import group_sum_kahan
 
 
 def max_market_share(payback, sector, curve_sector, curve_pb, curve_mms, all_pb):
@@ -46,3 +50,30 @@ def diffusion(mms, msly, p, q, teq_yr1, dev_w, system_kw, capex, adopt_ly, mv_ly
                 market_share=ms, new_market_share=nms, new_adopters=na, new_market_value=nmv,
                 new_system_kw=nskw, number_of_adopters=adopt_ly + na, market_value=mv_ly + nmv,
                 system_kw_cum=skc_ly + nskw)
+
+
+def anchor(state, sector, year, dev_w, system_kw_cum, observed):
+    """Anchor-year rescale (diffusion_functions_elec.py:99-133): per (state,
+    sector, year) group the pandas groupby sum (Kahan, NaN skipped) of the PV
+    cumulative capacity and the member count; each agent's share of the group
+    total times the observed MW (observed: {(state, sector, year): mw}).
+    Returns (system_kw_cum, number_of_adopters, market_share)."""
+    kw = np.asarray(system_kw_cum, dtype=float)
+    keys = list(zip(state, sector, (int(y) for y in year)))
+    groups = {}
+    for i, k in enumerate(keys):
+        groups.setdefault(k, []).append(i)
+    tot = np.empty(len(kw))
+    cnt = np.empty(len(kw))
+    for k, ix in groups.items():
+        tot[ix] = group_sum_kahan(kw[ix])[0]
+        cnt[ix] = len(ix)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        scale = np.where(tot == 0, 1.0 / cnt, kw / tot)
+    mw = np.array([observed.get(k, np.nan) for k in keys], dtype=float)
+    cum = scale * mw * 1000.0
+    adopters = np.where(np.asarray(sector) == "res", cum / 5.0, cum / 100.0)
+    w = np.asarray(dev_w, dtype=float)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ms = np.where(w == 0, 0.0, adopters / w)
+    return cum, adopters, ms

@@ -80,6 +80,36 @@ VARIANTS = {
     "st_plain4": [('global_store_dwordx4 %0, %1, %2 nt"', 'global_store_dwordx4 %0, %1, %2"')],
     "no_bins": [("                    double2 b = bins[p * BLOCK];\n                    b.x += ld;\n                    b.y += st.sys;\n                    bins[p * BLOCK] = b;",
                  "                    asm volatile(\"\" :: \"v\"(p), \"v\"(st.sys));")],
+    # --- demand-charge two-agent k_size diagnosis ---------------------------
+    # agent-scope release before the envelope / split hand-offs (orders the
+    # month lanes' stores before the wait at compiler level)
+    "dc_rel": [("    // buffer_inv sc1, once per build.\n    __builtin_amdgcn_s_waitcnt(0);",
+                "    // buffer_inv sc1, once per build.\n    __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"agent\");\n    __builtin_amdgcn_s_waitcnt(0);"),
+               ("    // hand-off to the other lanes through global memory, as yl_dc_build\n    __builtin_amdgcn_s_waitcnt(0);",
+                "    // hand-off to the other lanes through global memory, as yl_dc_build\n    __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"agent\");\n    __builtin_amdgcn_s_waitcnt(0);")],
+    # no envelopes: every demand charge from the hourly pass (yl_demand)
+    "dc_noenv": [("            if (c.dem_wo_pending) c.env_ok = c.env.lines && yl_dc_build(c.dem, c.src, c.tlo, c.thi, c.env, c.g);",
+                  "            if (c.dem_wo_pending) c.env_ok = false;")],
+    # envelopes built, evaluations from the hourly pass
+    "dc_noeval": [("                const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kws, s, wg, c.S)\n                                          : yl_demand(c.dem, c.src, s, wg, c.S);",
+                   "                const double v = yl_demand(c.dem, c.src, s, wg, c.S);")],
+    # per-evaluation capture of the demand-charge objective for agents 0-3
+    # (read back with dgen_debug_dcdbg; scripts/dbg_dc_eval.py)
+    "dc_dbg": [("constexpr size_t DCW_BYTES =",
+                "__device__ double g_dcdbg[4][24][64][6];\nconstexpr size_t DCW_BYTES ="),
+               ("    Seg<LPA> g;\n    int y, N;\n    bool active;",
+                "    Seg<LPA> g;\n    int y, N;\n    bool active;\n    int dbg_i, dbg_e;"),
+               ("    c.dem_wo_pending = false;\n    c.env_ok = false;\n    c.env.lines = nullptr;",
+                "    c.dem_wo_pending = false;\n    c.env_ok = false;\n    c.env.lines = nullptr;\n    c.dbg_i = (int)i; c.dbg_e = 0;"),
+               ("                if (wg) wb += v;\n                else c.wo1 += v;",
+                "                if (wg && c.dbg_i < 4 && c.dbg_e < 24) {\n"
+                "                    double* r = g_dcdbg[c.dbg_i][c.dbg_e][c.g.lane];\n"
+                "                    r[0] = kws; r[1] = s; r[2] = v; r[3] = wb; r[4] = c.env_ok ? 1.0 : 0.0; r[5] = c.r_y;\n"
+                "                }\n"
+                "                if (wg) wb += v;\n                else c.wo1 += v;"),
+               ("            c.dem_wo_pending = false;\n        }\n    }",
+                "            c.dem_wo_pending = false;\n            c.dbg_e++;\n        }\n    }"),
+               ('extern "C" {', 'extern "C" {\nint32_t dgen_debug_dcdbg(void* dst) { return (int32_t)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dcdbg), sizeof(g_dcdbg)); }')],
 }
 
 

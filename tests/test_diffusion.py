@@ -59,3 +59,34 @@ def test_oracle_diffusion(gold, phase):
     for k, v in o.items():
         assert np.array_equal(v, d[k].to_numpy(float), equal_nan=True), k
     assert g["columns"][-3:] == ["system_kw_cum", "batt_kw_cum", "batt_kwh_cum"]
+
+
+@pytest.fixture(scope="module")
+def anchor_gold():
+    with open(os.path.join(GOLDEN, "anchor.json")) as f:
+        return json.load(f)
+
+
+def _observed_map(g):
+    o = g["observed"]
+    return {(s, c, int(y)): float(mw) for s, c, y, mw in
+            zip(o["state_abbr"], o["sector_abbr"], o["year"], o["observed_solar_mw"])}
+
+
+@pytest.mark.parametrize("year", ["2014", "2016", "2018"])
+def test_oracle_anchor_years(anchor_gold, year):
+    """Anchor-year rescale (diffusion_functions_elec.py:99-133) against the
+    reference's own output: pre-anchor cumulative = last year + new capacity,
+    Kahan group totals, observed MW -> bit-exact."""
+    r = pd.DataFrame(anchor_gold["years"][year]["df"])
+    pre = r["system_kw_cum_last_year"].to_numpy(float) + r["new_system_kw"].to_numpy(float)
+    cum, ad, ms = od.anchor(r["state_abbr"].tolist(), r["sector_abbr"].tolist(), r["year"].tolist(),
+                            r["developable_agent_weight"].to_numpy(float), pre,
+                            _observed_map(anchor_gold))
+    assert np.array_equal(cum, r["system_kw_cum"].to_numpy(float), equal_nan=True)
+    assert np.array_equal(ad, r["number_of_adopters"].to_numpy(float), equal_nan=True)
+    assert np.array_equal(ms, r["market_share"].to_numpy(float), equal_nan=True)
+    # the fixture covers the NaN (state without observed rows) and all-zero-group branches
+    assert np.isnan(cum).any() and np.isfinite(cum).any()
+    zero = (r["state_abbr"] == "DE") & (r["sector_abbr"] == "ind")
+    assert zero.any() and np.all(pre[zero.to_numpy()] == 0.0)

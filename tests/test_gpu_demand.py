@@ -75,7 +75,9 @@ def _check(o, ref, life, pop):
                          ("cash_flow", "cash_flow")):
             assert np.allclose(o[k_o][i, :N1], r[k_r], rtol=1e-6, atol=1e-5), (i, k_o)
     print(f"demand-charge Brent path flips: {flipped} of {len(ref)}", flush=True)
-    assert flipped <= max(1, len(ref) // 50), flipped
+    # measured: 0, 0 and 1 of 160 (the net-billing long-life case, whose energy
+    # bills re-associate the split sums); each flipped agent is held to xatol above
+    assert flipped <= 1, flipped
 
 
 @pytest.mark.parametrize("net_billing,long_life", [(False, False), (True, False), (True, True)])
