@@ -85,6 +85,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
             hits = spill_guard.scan(asm)
             if attempt == 0:
                 first = {k: [b for b, _ in v] for k, v in hits.items()}
+            # k_hourly_batt's counted next-day DMA wait must cover the DMA
+            dma_k, dma_issued = spill_guard.day_dma_wait(asm)
+            if dma_issued < dma_k:
+                raise RuntimeError(f"k_hourly_batt: the day read-back waits vmcnt({dma_k}) but only "
+                                   f"{dma_issued} vector-memory ops follow the next-day DMA on every path")
             if not hits:
                 shutil.copyfile(lib, OUT + ".tmp")
                 os.replace(OUT + ".tmp", OUT)
@@ -99,7 +104,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
         finally:
             shutil.rmtree(work, ignore_errors=True)
     with open(GUARD, "w") as f:
-        json.dump({"flagged_first_build": first, "withdrawn": defines}, f, indent=1)
+        json.dump({"flagged_first_build": first, "withdrawn": defines,
+                   "day_dma_wait_vmcnt": dma_k, "vmem_ops_after_day_dma": dma_issued}, f, indent=1)
     return OUT
 
 
