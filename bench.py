@@ -33,7 +33,7 @@ NH = 8760
 ROW_BYTES = NH * 4              # one f32 load-shape row or one i32 cf row
 PLANE_BYTES = NH * 4            # one f32 hourly output plane per agent
 SYS_BYTES = NH * 8              # the battery case's f64 system-output plane per agent
-NB_BYTES = 9280                 # net-billing split record per scratch slot (DGEN_NB_BYTES)
+NB_BYTES = 59968                # net-billing split record per scratch slot (DGEN_NB_BYTES)
 
 
 def algorithmic_bytes(cols, hourly: bool, battery: bool):

@@ -99,7 +99,7 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
-ABI_VERSION = 4   # include/dgen_hip.h DGEN_ABI_VERSION
+ABI_VERSION = 5   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
 

@@ -1642,32 +1642,42 @@ __device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& 
 // caller's workspace.
 // ---------------------------------------------------------------------------
 constexpr int NB_CAPM = 192;
+// an M entry carries the hour's own inputs, so an evaluation reads one
+// contiguous record instead of gathering the shape / cf (or system-output) /
+// TS rows at scattered hours: load L, generation term g (cf / 1e6 per kW in
+// the search, the system output in the battery case), the float32 sell
+// weight w and the period
+struct NbEnt {
+    double L, g;
+    float w;
+    int p;
+};
+static_assert(sizeof(NbEnt) == 24, "24-B mixed-hour entries");
 constexpr size_t NB_SUMS_BYTES = (size_t)12 * MAXP * 4 * sizeof(double);
-constexpr size_t NB_BYTES = NB_SUMS_BYTES + 64 + (size_t)12 * NB_CAPM * sizeof(uint16_t);
+constexpr size_t NB_BYTES = NB_SUMS_BYTES + 64 + (size_t)12 * NB_CAPM * sizeof(NbEnt);
 static_assert(NB_BYTES % 16 == 0, "per-slot net-billing records stay 16-B aligned");
 static_assert(NB_BYTES == DGEN_NB_BYTES, "include/dgen_hip.h DGEN_NB_BYTES");
-// an M entry: hour within the month (< 744) | period << 10
-constexpr int NB_HBITS = 10;
 
 struct NbRec {
     double* sums;        // [12][MAXP][4]: SA_L, SA_g, SX_gw, SX_Lw
     int* cnt;            // [12] M hours per month
-    uint16_t* ent;       // [12][NB_CAPM]
+    NbEnt* ent;          // [12][NB_CAPM]
 };
 __device__ __forceinline__ NbRec nb_rec(char* p) {
     NbRec r;
     r.sums = reinterpret_cast<double*>(p);
     r.cnt = reinterpret_cast<int*>(p + NB_SUMS_BYTES);
-    r.ent = reinterpret_cast<uint16_t*>(p + NB_SUMS_BYTES + 64);
+    r.ent = reinterpret_cast<NbEnt*>(p + NB_SUMS_BYTES + 64);
     return r;
 }
 
 // The sell weight of an exported kWh: the float32-rounded TS sell rate
 // (ff:756) when the reference enables it, else 1 (the period's sell column is
 // applied per month).
-__device__ __forceinline__ double nb_weight(const YSrc& src, int h) {
-    return src.ts ? (double)(float)(src.ts[h] * src.ts_mult) : 1.0;
+__device__ __forceinline__ float nb_weight_f(const YSrc& src, int h) {
+    return src.ts ? (float)(src.ts[h] * src.ts_mult) : 1.0f;
 }
+__device__ __forceinline__ double nb_weight(const YSrc& src, int h) { return (double)nb_weight_f(src, h); }
 
 // Month lane m < 12 of the segment builds month m (accumulators in its LDS
 // column, at(4 p + q), 4 P <= 4 half).  Returns true when every month's M
@@ -1682,8 +1692,7 @@ __device__ bool yl_nb_build(const dgen_tariff& t, const YSrc& src, double tlo, d
         const int P = t.P;
         for (int k = 0; k < 4 * P; k++) S.at(k) = 0.0;
         int n_m = 0;
-        const int h0m = c_month_start_day[m] * 24;
-        uint16_t* ent = R.ent + m * NB_CAPM;
+        NbEnt* ent = R.ent + m * NB_CAPM;
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             const uint8_t* sc = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
 #pragma unroll 1
@@ -1716,7 +1725,14 @@ __device__ bool yl_nb_build(const dgen_tariff& t, const YSrc& src, double tlo, d
                         S.at(4 * p + 2) += gk * w;
                         S.at(4 * p + 3) += L * w;
                     } else {
-                        if (n_m < NB_CAPM) ent[n_m] = (uint16_t)((p << NB_HBITS) | (h + k - h0m));
+                        if (n_m < NB_CAPM) {
+                            NbEnt e;
+                            e.L = L;
+                            e.g = gk;
+                            e.w = nb_weight_f(src, h + k);
+                            e.p = p;
+                            ent[n_m] = e;
+                        }
                         n_m++;
                     }
                 }
@@ -1750,35 +1766,24 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
             S.at(p) = q[0] - (q[1] * kws) * s;
             S.at(half + p) = (q[2] * kws) * s - q[3];
         }
-        const int h0m = c_month_start_day[m] * 24;
         const int n_m = R.cnt[m];
-        const uint16_t* ent = R.ent + m * NB_CAPM;
+        const NbEnt* ent = R.ent + m * NB_CAPM;
         int cur = 0;
         double ci = S.at(0), ce = S.at(half);
 #pragma unroll 1
         for (int j = 0; j < n_m; j += 4) {
-            // four entries in one 8-B load, then their inputs together
-            const uint2 e2 = *reinterpret_cast<const uint2*>(ent + j);
-            const uint32_t ev[4] = {e2.x & 0xffffu, e2.x >> 16, e2.y & 0xffffu, e2.y >> 16};
-            float sh[4];
-            double gv[4], tsv[4];
+            // four entries' loads together (96 contiguous bytes of the record)
+            NbEnt ev[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int hh = h0m + ((j + k < n_m) ? (int)(ev[k] & ((1u << NB_HBITS) - 1u)) : 0);
-                sh[k] = src.shape[hh];
-                // the hourly pass's generation term: cf / 1e6 x kW', or the
-                // battery case's system output as is
-                gv[k] = src.sysgen ? src.sysgen[(int64_t)(hh >> 2) * src.sys_stride * 4 + (hh & 3)]
-                                   : (double)src.cf[hh];
-                tsv[k] = src.ts ? src.ts[hh] : 0.0;
-            }
+            for (int k = 0; k < 4; k++) ev[k] = ent[(j + k < n_m) ? j + k : j];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
                 if (j + k >= n_m) break;
-                const int p = (int)(ev[k] >> NB_HBITS);
-                const double load = (double)sh[k] * src.load_scale;
-                const double gg = src.sysgen ? gv[k] : cf_per_kw((int32_t)gv[k]) * kws;
-                const double dd = load - gg * s;
+                const int p = ev[k].p;
+                // the hourly pass's arithmetic: load, generation cf / 1e6 x kW'
+                // (the battery case's system output as is), x the year's factor
+                const double gg = src.sysgen ? ev[k].g : ev[k].g * kws;
+                const double dd = ev[k].L - gg * s;
                 if (p != cur) {
                     S.at(cur) = ci;
                     S.at(half + cur) = ce;
@@ -1790,7 +1795,7 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
                     ci += dd;
                 } else {
                     double e = -dd;
-                    if (src.ts) e *= (double)(float)(tsv[k] * src.ts_mult);
+                    if (src.ts) e *= (double)ev[k].w;
                     ce += e;
                 }
             }

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 4
+#define DGEN_ABI_VERSION 5
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_NH    8760   /* hours per year                                    */
@@ -247,8 +247,11 @@ int32_t dgen_prep_cfs(dgen_ctx* ctx, const int32_t* cfs, int64_t n_rows, double*
 /* Workspace bytes for a batch of n agents with n_scratch scratch slots (agents
  * whose tariffs can bill net or carry demand charges):
  *   8 x (4 x 144 n + n + 8760 n_scratch)   bins, carries, battery output plane
- *   + DGEN_NB_BYTES x n_scratch             net-billing split records (k_size)  */
-#define DGEN_NB_BYTES 9280
+ *   + DGEN_NB_BYTES x n_scratch             net-billing split records (k_size,
+ *                                           k_batt_finance): per (month, period)
+ *                                           4 f64 sums, 12 counts, 12 x 192
+ *                                           mixed-hour entries of 24 B       */
+#define DGEN_NB_BYTES 59968
 size_t dgen_workspace_bytes(int64_t n, int64_t n_scratch);
 
 /* Size a batch: Brent over PV kW with 25-year bills + cash flow per
