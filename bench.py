@@ -74,18 +74,21 @@ def algorithmic_bytes(cols, hourly: bool, battery: bool):
 
 
 def pmc_traffic(pmc_dir: str, workload: str):
-    """Per-agent HBM bytes per kernel measured by rocprofv3 PMC on THIS workload
-    (profiles/pmc/<workload>.json, written by scripts/pmc_summary.py), or {}."""
+    """Per-agent HBM bytes and VALU-busy fraction per kernel measured by
+    rocprofv3 PMC on THIS workload (profiles/pmc/<workload>.json, written by
+    scripts/pmc_summary.py): ({kernel: bytes}, {kernel: valu_busy}, source)."""
     path = os.path.join(pmc_dir, f"{workload}.json")
     if not os.path.exists(path):
-        return {}, None
+        return {}, {}, None
     try:
         with open(path) as f:
             pm = json.load(f)
-        return {k.replace("_w", "") if k.endswith("_w") else k: float(v["hbm_bytes_per_agent"])
-                for k, v in pm.items() if "hbm_bytes_per_agent" in v}, os.path.relpath(path, REPO)
+        key = lambda k: k[:-2] if k.endswith("_w") else k
+        return ({key(k): float(v["hbm_bytes_per_agent"]) for k, v in pm.items() if "hbm_bytes_per_agent" in v},
+                {key(k): float(v["valu_busy_frac"]) for k, v in pm.items() if "valu_busy_frac" in v},
+                os.path.relpath(path, REPO))
     except Exception:
-        return {}, None
+        return {}, {}, None
 
 
 def parse():
@@ -219,7 +222,7 @@ def main():
     value = total_agents / el
 
     nbytes = algorithmic_bytes(pop.cols, not args.no_hourly, not args.no_batt)
-    traffic_pa, traffic_src = pmc_traffic(args.pmc_dir, args.config)
+    traffic_pa, valu_busy, traffic_src = pmc_traffic(args.pmc_dir, args.config)
     # launches per step: k_hourly_batt sweeps the year in month-segment launches
     # per pipeline chunk; the year-lane kernels launch once per chunk
     launches = {"k_size": eng.chunks, "k_hourly_batt": -(-12 // eng.hb_months) * eng.chunks,
@@ -231,7 +234,8 @@ def main():
         per_kernel[k] = {"ms_per_step": t, "launches_per_step": launches[k],
                          "algorithmic_bytes_per_step": nbytes[k], "achieved_gbs": gbs,
                          "hbm_frac": (gbs / HBM_PEAK_GBS) if gbs else None,
-                         "traffic_per_step": (traffic_pa[k] * args.agents) if k in traffic_pa else None}
+                         "traffic_per_step": (traffic_pa[k] * args.agents) if k in traffic_pa else None,
+                         "valu_busy_frac_pmc": valu_busy.get(k)}
     dom = max(kms, key=lambda k: kms[k])
     d = per_kernel[dom]
     nl = max(launches[dom], 1)
@@ -242,9 +246,13 @@ def main():
             "algorithmic_bytes_per_launch": nbytes[dom] / nl, "launches_per_step": nl,
             "kernel_ms": kms, "per_kernel": per_kernel, "dominant_kernel": dom, "event_samples": cnt,
             "traffic_source": traffic_src if dom in traffic_pa else None,
-            "note": ("k_hourly_batt streams its rows and planes: HBM is its roofline" if dom == "k_hourly_batt"
+            # the VALU side of the same kernel (PMC of this workload): share of
+            # its dispatch the SIMDs spend issuing VALU (scripts/pmc_summary.py)
+            "valu_busy_frac": valu_busy.get(dom),
+            "note": ("k_hourly_batt streams its rows and planes (HBM roofline) and is co-limited by fp64 "
+                     "VALU (valu_busy_frac)" if dom == "k_hourly_batt"
                      else f"{dom} is fp64-VALU / latency bound (the year lanes re-bill per evaluation): "
-                          "its HBM fraction is reported for completeness, not as its bound")}
+                          "valu_busy_frac is its bound; the HBM fraction is reported for completeness")}
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:

@@ -452,11 +452,10 @@ __device__ __forceinline__ void sort24_desc(double (&v)[24]) {
 
 __device__ __forceinline__ double day_target_sorted(const double (&s)[24], double power,
                                                     double avail) {
-    double need0 = 0.0;
-#pragma unroll
-    for (int k = 0; k < 24; k++) need0 += fmin(s[k], power);
-    if (need0 <= avail) return 0.0;
     if (s[0] <= power) {
+        // no hour above the power limit: need0 = sum_k min(s_k, P) is the
+        // scan's total S_24 (the same additions in the same order), so one
+        // pass decides the early-out and the target
         double S = 0.0, SK = s[0];
         int K = 1;
 #pragma unroll
@@ -466,8 +465,13 @@ __device__ __forceinline__ double day_target_sorted(const double (&s)[24], doubl
             K = ok ? k : K;
             SK = ok ? S : SK;
         }
+        if (S <= avail) return 0.0;
         return (SK - avail) / (double)K;
     }
+    double need0 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 24; k++) need0 += fmin(s[k], power);
+    if (need0 <= avail) return 0.0;
     int a_lo = 0, b_lo = 0;
 #pragma unroll
     for (int k = 0; k < 24; k++) {
@@ -1987,7 +1991,11 @@ struct YCtx {
     __device__ explicit YCtx(int lane) : g(lane) {}
 };
 
-template <int LPA, bool DC>
+// NET: the batch may bill net (it has scratch slots, dgen_size_agents); the
+// NEM-only instantiation compiles the net-billing paths out, so the common
+// case's register allocation does not carry them (an agent that would still
+// reach one flags DGEN_ST_SCRATCH, which assign_scratch rules out).
+template <int LPA, bool DC, bool NET>
 __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
     c.tp = stage_tariff(c.tariffs + tix, c.S, c.g);
     const dgen_tariff& t = *c.tp;
@@ -1999,13 +2007,16 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);
-    } else {
+    } else if constexpr (NET) {
         // net billing: the no-system bill from the load bins, then the split
         // of the search's hours for this tariff's periods
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_mo2_nogen(t, c.S);
         c.nb_ok = c.nb && yl_nb_build(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g);
+    } else {
+        c.status |= DGEN_ST_SCRATCH;
+        c.wo1 = NAN;
     }
     if constexpr (DC) {   // its no-system charge is added by the next objective
         c.dem = tariff_demand(c.dem_table, c.n_dem, true, t);
@@ -2016,7 +2027,7 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
 // calc_system_performance(kw, en_batt=False) with lanes = years; returns -NPV
 // (wave-uniform).  Every evaluation leaves its per-lane results in `c.last`:
 // after the search they are the outputs of the last evaluation (ff:449-474).
-template <int LPA, bool DC>
+template <int LPA, bool DC, bool NET>
 __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double otc = 0.0;
     if (kw > 0.0) {
@@ -2024,7 +2035,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
         otc = rate_switch(c.sw_rows, c.sw_cnt, kw, &nt);
         if (nt >= 0) {
             c.switched = 1;
-            if (nt != c.tariff) yl_set_tariff<LPA, DC>(c, nt);
+            if (nt != c.tariff) yl_set_tariff<LPA, DC, NET>(c, nt);
         }
     }
     const dgen_tariff& t = *c.tp;
@@ -2033,9 +2044,11 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double wb;
     if (!net_hourly(t)) {
         wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
-    } else {
+    } else if constexpr (NET) {
         c.src.gen_scale = kws;
         wb = c.nb_ok ? yl_bill_nb(t, c.src, c.s_y, c.nb, c.S) : yl_bill_mo2(t, c.src, c.s_y, true, c.S);
+    } else {
+        wb = NAN;
     }
     if constexpr (DC) {
         if (c.dem) {
@@ -2073,7 +2086,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 // build runs at 1 wave per SIMD: capped at 2 it spilled (156-180 B/lane) and
 // those builds returned wrong, build-dependent Brent results (DESIGN.md
 // section 3); with no scratch it matches the oracle.
-template <int LPA, bool DC>
+template <int LPA, bool DC, bool NET>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
          void* dcws, char* nbws) {
@@ -2161,12 +2174,12 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         c.tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
         c.thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
     }
-    yl_set_tariff<LPA, DC>(c, t0);
+    yl_set_tariff<LPA, DC, NET>(c, t0);
     int nfev = 0;
     double x_last = 0.0;
     double kw_star = brent_bounded(
         [&](double x) __attribute__((always_inline)) {
-            return yl_objective<LPA, DC>(c, x);
+            return yl_objective<LPA, DC, NET>(c, x);
         },
         low, high, xatol, &nfev, &x_last);
     const YLast& l = c.last;
@@ -2203,7 +2216,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
 }
 
 // Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
-template <int LPA, bool DC>
+template <int LPA, bool DC, bool NET>
 __global__ void __launch_bounds__(WAVE)
 k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
                  int64_t n_scratch, int64_t i0, int64_t i1, char* nbws) {
@@ -2250,7 +2263,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         src.ts = (t.mo == 2 && !is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
         src.ts_mult = A.price_mult[i];
     }
-    double wo1, wb;
+    double wo1 = NAN, wb = NAN;
     if (!mo2) {
         const double2* lg = W.LGb + (int64_t)i * NBIN;
         for (int cell = g.sl; cell < 12 * t.P; cell += LPA) {
@@ -2262,7 +2275,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         wave_lds_sync();
         wo1 = same_tariff ? O.first_without[i] : yl_bill_nem(t, S, 0.0, cfg.nm_yearend_sell_rate);
         wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
-    } else {
+    } else if constexpr (NET) {
         if (same_tariff) {
             wo1 = O.first_without[i];
         } else {   // k_size's no-system form: the slot-sum load bins
@@ -3050,22 +3063,33 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         // agents per year-lane block: WAVE / lpa
         const dim3 ygrid_s((unsigned)((m + WAVE / lpa_s - 1) / (WAVE / lpa_s)));
         const dim3 ygrid_f((unsigned)((m + WAVE / lpa_f - 1) / (WAVE / lpa_f)));
+        // net billing compiled in only when the batch has scratch slots (an
+        // agent whose tariffs can bill net always gets one, assign_scratch)
+        const bool net = n_scratch > 0;
         if (lpa_s == 32 && !dc) {
 #if !DGEN_NO2_SIZE
-            hipLaunchKernelGGL((k_size_w<32, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n, i0,
-                               i1, nullptr, nbws);
+            if (net)
+                hipLaunchKernelGGL((k_size_w<32, false, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
+                                   n, i0, i1, nullptr, nbws);
+            else
+                hipLaunchKernelGGL((k_size_w<32, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                                   c->cfg, n, i0, i1, nullptr, nbws);
 #endif
         } else if (lpa_s == 32) {
 #if !DGEN_NO2_SIZE_DC
-            hipLaunchKernelGGL((k_size_w<32, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n, i0,
-                               i1, c->dc_buf, nbws);
+            hipLaunchKernelGGL((k_size_w<32, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n,
+                               i0, i1, c->dc_buf, nbws);
 #endif
         } else if (!dc) {
-            hipLaunchKernelGGL((k_size_w<WAVE, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n, i0,
-                               i1, nullptr, nbws);
+            if (net)
+                hipLaunchKernelGGL((k_size_w<WAVE, false, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                                   c->cfg, n, i0, i1, nullptr, nbws);
+            else
+                hipLaunchKernelGGL((k_size_w<WAVE, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                                   c->cfg, n, i0, i1, nullptr, nbws);
         } else {
-            hipLaunchKernelGGL((k_size_w<WAVE, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n, i0,
-                               i1, c->dc_buf, nbws);
+            hipLaunchKernelGGL((k_size_w<WAVE, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
+                               n, i0, i1, c->dc_buf, nbws);
         }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
@@ -3085,19 +3109,27 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             // PV-only variant: no battery-case bill / cash flow
         } else if (lpa_f == 32 && !dc) {
 #if !DGEN_NO2_FIN
-            hipLaunchKernelGGL((k_batt_finance_w<32, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
-                               c->cfg, n, ws, n_scratch, i0, i1, nbws);
+            if (net)
+                hipLaunchKernelGGL((k_batt_finance_w<32, false, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws);
+            else
+                hipLaunchKernelGGL((k_batt_finance_w<32, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws);
 #endif
         } else if (lpa_f == 32) {
 #if !DGEN_NO2_FIN_DC
-            hipLaunchKernelGGL((k_batt_finance_w<32, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
+            hipLaunchKernelGGL((k_batt_finance_w<32, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
                                c->cfg, n, ws, n_scratch, i0, i1, nbws);
 #endif
         } else if (!dc) {
-            hipLaunchKernelGGL((k_batt_finance_w<WAVE, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
-                               c->cfg, n, ws, n_scratch, i0, i1, nbws);
+            if (net)
+                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws);
+            else
+                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
+                                   *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws);
         } else {
-            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
+            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
                                c->cfg, n, ws, n_scratch, i0, i1, nbws);
         }
         HIP_TRY(hipEventRecord(e[4], s2));

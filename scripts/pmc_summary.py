@@ -18,6 +18,8 @@ import glob
 import json
 import sys
 
+SIMDS = 256 * 4          # MI355X: 256 CUs x 4 SIMDs
+XCDS = 8
 pattern, agents, out_json = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 hb_launches = int(sys.argv[4]) if len(sys.argv) > 4 else 12
 agg = collections.defaultdict(list)
@@ -45,6 +47,13 @@ for kn in sorted({k for k, _ in agg}):
         rec["valu_wave_insts_per_agent"] = means["SQ_INSTS_VALU"] * per_call / agents
     if "SQ_ACTIVE_INST_VALU" in means and "SQ_ACTIVE_INST_ANY" in means and means["SQ_ACTIVE_INST_ANY"]:
         rec["valu_share_of_active"] = means["SQ_ACTIVE_INST_VALU"] / means["SQ_ACTIVE_INST_ANY"]
+    if "SQ_INSTS_VALU" in means and means.get("GRBM_GUI_ACTIVE"):
+        # VALU issue share of the dispatch: a wave64 VALU instruction holds its
+        # SIMD 4 cycles (16 lanes / clock, fp64 and 32-bit alike on CDNA4);
+        # GRBM_GUI_ACTIVE sums the busy clocks of the 8 XCDs
+        cycles = means["GRBM_GUI_ACTIVE"] / XCDS
+        rec["valu_busy_frac"] = means["SQ_INSTS_VALU"] * 4.0 / (SIMDS * cycles)
+        rec["valu_busy_note"] = "SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)"
     res[kn] = rec
     print(kn, {k: (round(v, 4) if isinstance(v, float) else v) for k, v in rec.items() if k != "counters_per_dispatch"})
     for c, v in sorted(means.items()):
