@@ -650,8 +650,11 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const int lr = A.load_row[i], cr = A.cf_row[i];
     const double kwh = A.load_kwh[i];
     const double ls = kwh / T.shape_sum[lr];                     // load = shape * ls
-    const double kw_star = O.system_kw[i];
-    const double x_last = O.x_last[i];
+    // an agent k_size left unsized (kWh/kW tier units) keeps its no-system
+    // hourly planes (load as is), so per-state and chunk sums stay finite
+    const bool unsized = (O.status[i] & DGEN_ST_UNIT) != 0;
+    const double kw_star = unsized ? 0.0 : O.system_kw[i];
+    const double x_last = unsized ? 0.0 : O.x_last[i];
     // pv = cf * (c / 1e6), c = ((kW * 1000) * 0.96) / 1000   (ff:118-120)
     const double cl6 = (((x_last * 1000.0) * 0.96) / 1000.0) / 1e6;
     const double cs6 = (((kw_star * 1000.0) * 0.96) / 1000.0) / 1e6;
@@ -841,7 +844,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     O.capacity_factor[i] = naep / 8760.0;
     O.batt_kw[i] = has_batt ? power : 0.0;
     O.batt_kwh[i] = bank;
-    if (!batt_on) O.npv_pv_batt[i] = NAN;   // k_batt_finance does not run
+    if (!batt_on || unsized) O.npv_pv_batt[i] = NAN;   // k_batt_finance does not run
     // battery run on the PV run's tariff: k_batt_finance reuses its no-system
     // bill (same load, same tariff -> the same bill, as in the oracle)
     W.aux[i] = (tariff != O.tariff_final[i]) ? 1.0 : 0.0;
@@ -2150,6 +2153,10 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     bool bad = false;
     if (c.N < 1 || c.N > MAXY || c.N > LPA) { c.status |= DGEN_ST_YEARS; bad = true; }
     if (t0 < 0 || t0 >= T.n_tariffs) { c.status |= DGEN_ST_TARIFF; bad = true; }
+    // kWh/kW tier units (SSC scales those caps by the month's peak demand, not
+    // restated here): the agent is reported unsized, per agent (DGEN_ST_UNIT),
+    // instead of being billed with the wrong caps
+    else if (T.tariffs[t0].flags & DGEN_ST_UNIT) { c.status |= DGEN_ST_UNIT; bad = true; }
     const double max_load = c.kwh / naep0;                         // ff:440-444
     const double low = max_load * 0.8, high = max_load * 1.25;
     const double span = high - low;
@@ -2163,7 +2170,14 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
             O.status[i] = c.status;
             O.nfev[i] = 0;
             O.system_kw[i] = NAN; O.x_last[i] = NAN; O.npv[i] = NAN;
+            O.payback_raw[i] = NAN; O.payback_period[i] = NAN;
+            O.first_with[i] = NAN; O.first_without[i] = NAN; O.price_per_kwh[i] = NAN;
             O.tariff_final[i] = t0; O.switched[i] = 0;
+        }
+        const int64_t row = i * (MAXY + 1);
+        for (int k = sl; k <= MAXY; k += LPA) {
+            O.cash_flow[row + k] = NAN; O.cfev_pv[row + k] = NAN;
+            O.bill_w_pv[row + k] = NAN; O.bill_wo_pv[row + k] = NAN;
         }
         return;
     }
@@ -2224,7 +2238,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
     const int st = O.status[i];
-    if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH)) return;
+    if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH | DGEN_ST_UNIT)) return;
     const Seg<LPA> g(lane);
     const int y = g.sl + 1;
     const int half = lds_half(T.max_periods);

@@ -109,7 +109,18 @@ def _columnarize(rows, src: ProfileStore, rate_switch_table):
 
 
 def _raise_for_status(status: np.ndarray, agent_ids) -> None:
-    bad = np.nonzero(status & (_lib.ST_FATAL | _lib.ST_ZERO_LOAD | _lib.ST_EMPTY_EC))[0]
+    """Raise like the reference for a chunk-fatal agent status.  Agents whose
+    tariff has kWh/kW tier units (ST_UNIT) are not fatal: they come back
+    unsized (NaN outputs, no-system hourly planes) with a warning, and the
+    rest of the chunk is sized."""
+    unit = np.nonzero(status & _lib.ST_UNIT)[0]
+    if unit.size:
+        import warnings
+        ids = [agent_ids[int(k)] for k in unit[:5]]
+        warnings.warn(f"{unit.size} agent(s) left unsized: tariff usage unit kWh/kW (tiers scaled by "
+                      f"peak demand) is not supported; NaN outputs (first: {ids})", RuntimeWarning,
+                      stacklevel=3)
+    bad = np.nonzero(status & ((_lib.ST_FATAL & ~_lib.ST_UNIT) | _lib.ST_ZERO_LOAD | _lib.ST_EMPTY_EC))[0]
     if bad.size == 0:
         return
     k = int(bad[0])
@@ -123,8 +134,6 @@ def _raise_for_status(status: np.ndarray, agent_ids) -> None:
     if s & _lib.ST_EMPTY_EC:
         raise _lib.DgenError(f"agent {who}: tariff has no energy-charge matrix "
                              "(the reference would price it with stale PySAM state)")
-    if s & _lib.ST_UNIT:
-        raise _lib.DgenError(f"agent {who}: tariff usage unit kWh/kW is not supported")
     if s & _lib.ST_DEMAND:
         raise _lib.DgenError(f"agent {who}: demand-charge matrix outside SSC's limits "
                              "(0-based month, 1-based period <= 8, contiguous tiers <= 4)")
@@ -177,6 +186,11 @@ def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[
     torch.cuda.synchronize(eng.dev)
     t2 = time.perf_counter()
     o = outputs_to_host(out, batch.perm)
+    unsized = (o["status"] & _lib.ST_UNIT) != 0
+    if unsized.any():          # kWh/kW tier units: every sizing output NaN
+        for k, v in o.items():
+            if v is not None and k not in _lib.OUTPUT_HOURLY and v.dtype.kind == "f":
+                v[unsized] = np.nan
     if net is not None:
         o["net_sum_kw"] = net.cpu().numpy()
     if timing is not None:

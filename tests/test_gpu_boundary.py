@@ -64,3 +64,30 @@ def test_zero_load_raises_like_reference():
     r["load_kwh_per_customer_in_bin"] = 0.0
     with pytest.raises(ZeroDivisionError):
         ff.calc_system_size_and_performance(store, r, None, table)
+
+
+def test_kwh_per_kw_units_leave_only_that_agent_unsized():
+    """kWh/kW tier units (unit code 1) are not restated: that agent comes back
+    unsized (NaN outputs, a RuntimeWarning) and the rest of the chunk is sized
+    exactly as without it; its no-system planes keep the aggregate finite."""
+    import warnings
+    rows, store, table = helpers.golden_rows()
+    df = pd.DataFrame(rows[:6]).copy()
+    ones = [[1] * 24 for _ in range(12)]
+    df.at[df.index[2], "tariff_dict"] = {"ur_ec_tou_mat": [[1, 1, 500.0, 1, 0.2, 0.0], [1, 2, 1e38, 1, 0.25, 0.0]],
+                                         "ur_ec_sched_weekday": ones, "ur_ec_sched_weekend": ones,
+                                         "ur_metering_option": 0}
+    ff._worker_conn = store
+    with pytest.warns(RuntimeWarning, match="kWh/kW"):
+        out, agg = ff.size_chunk(df, None, table, "simple")
+    r = out.iloc[2]
+    for k in ("system_kw", "npv", "payback_period", "batt_kw"):
+        assert np.isnan(r[k]), k
+    assert np.isnan(np.asarray(r["cash_flow"], float)).all()
+    assert np.isfinite(agg["net_sum_kw"]).all()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        ref, _ = ff.size_chunk(df.drop(index=df.index[2]), None, table, "simple")
+    got = out.drop(index=df.index[2])
+    for k in ("system_kw", "npv", "payback_period", "batt_kwh", "npv_pv_batt" if "npv_pv_batt" in ref else "npv"):
+        assert np.array_equal(got[k].to_numpy(float), ref[k].to_numpy(float), equal_nan=True), k
