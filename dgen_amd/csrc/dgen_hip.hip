@@ -2085,12 +2085,14 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 // occupancy floor of 3 waves per SIMD (<= 168 VGPRs): the 32-lane variant
 // otherwise takes 181 and runs 2 (measured 23.3 -> 18.6 ms at 1M agents)
 // DC: demand charges billed (extension mode) -- a separate instantiation so
-// the reference mode's register allocation is untouched.  The two-agent DC
-// build runs at 1 wave per SIMD: capped at 2 it spilled (156-180 B/lane) and
-// those builds returned wrong, build-dependent Brent results (DESIGN.md
-// section 3); with no scratch it matches the oracle.
+// the reference mode's register allocation is untouched.  Both DC builds run
+// at 2 waves per SIMD (the two-agent one spills; 78 -> 47 ms for C4 200k vs 1
+// wave).  Round 1's wrong two-agent results came from a spill placed ahead of
+// a divergent join's exec restore; the build guard
+// (dgen_amd/spill_guard.py) rejects any build with that pattern and falls
+// back to one agent per wave for the flagged kernel.
 template <int LPA, bool DC, bool NET>
-__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)))
+__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
          void* dcws, char* nbws) {
     const int lane = threadIdx.x;

@@ -72,7 +72,7 @@ VARIANTS = {
     "bill_unroll12": [("    double total = 0.0;\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn",
                        "    double total = 0.0;\n#pragma unroll\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn")],
     # reference-mode k_size at 2 waves per SIMD (no spills) instead of 3
-    "ks_occ2": [("amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)", "amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 2)")],
+    "ks_occ2": [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? 2 : 2)")],
     # hourly-plane store cache policy (MI355X_MICROARCH.md: plain / sc0 / nt keep the
     # line in the XCD's L2, sc1 / sc0 sc1 write through and drop it)
     "st_sc1": [('global_store_dwordx4 %0, %1, %2 nt"', 'global_store_dwordx4 %0, %1, %2 sc1"')],
@@ -110,6 +110,8 @@ VARIANTS = {
                ("            c.dem_wo_pending = false;\n        }\n    }",
                 "            c.dem_wo_pending = false;\n            c.dbg_e++;\n        }\n    }"),
                ('extern "C" {', 'extern "C" {\nint32_t dgen_debug_dcdbg(void* dst) { return (int32_t)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dcdbg), sizeof(g_dcdbg)); }')],
+    # two-agent demand-charge k_size at 1 wave per SIMD (round 1's no-spill build; now 2 waves)
+    "ks_dc_occ1": [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)")],
 }
 
 
