@@ -1414,11 +1414,6 @@ __device__ __forceinline__ double dc_tier_charge(double peak, const double* cap,
     return charge;
 }
 
-// One lane's year of demand charges (system output x s; no system when
-// !with_gen).  Peaks are maxima, so they are exact whatever the hour order;
-// only the imports' own rounding differs from the oracle.  The TOU peaks live
-// in the lane's LDS column (S.at(0 .. DCP-1); the host sizes it, see
-// dgen_size_agents): held in registers they pushed k_size into spills.
 // The reference's per-hour PV output at kW (ff:117-119, dc -> ac -> kWh), in
 // its own operation order: demand charges bill maxima, where a last-bit
 // difference can move a Brent comparison at a kink, so the demand passes form
@@ -1427,6 +1422,11 @@ __device__ __forceinline__ double ref_gen(double gpk, double kw) {
     return (((gpk * kw) * 1000.0) * 0.96) / 1000.0;
 }
 
+// One lane's year of demand charges (system output x s; no system when
+// !with_gen).  Peaks are maxima, so they are exact whatever the hour order;
+// only the imports' own rounding differs from the oracle.  The TOU peaks live
+// in the lane's LDS column (S.at(0 .. DCP-1); the host sizes it, see
+// dgen_size_agents): held in registers they pushed k_size into spills.
 // kw: the search's system kW (PV-only case; the battery case reads the
 // system-output plane, src.sysgen)
 __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& src, double kw, double s,
@@ -1475,6 +1475,96 @@ __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& sr
                     double& pk = S.at(p < DCP ? p : 0);
                     pk = imp > pk ? imp : pk;
                 }
+            }
+        }
+        double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
+        for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
+        total += c;
+    }
+    return total;
+}
+
+// Battery-case demand charges with the hours staged through LDS: every year
+// lane of a segment bills the same hours (only its degradation factor s
+// differs), so the segment loads each batch of DEM_BATCH hours once --
+// lane k takes DEM_BATCH / LPA of them (load L = shape x load_scale, system
+// output, demand period) -- and stores them grouped by demand period
+// (a counting sort by ballots), with the group offsets.  Every lane then
+// scans each period's run from LDS (broadcast reads) with a plain running max:
+// no per-hour branch or LDS write in the scan.  The same imports as yl_demand
+// (L - sys x s) and the same maxima (a max does not depend on the order).
+constexpr int DEM_BATCH = 64;
+struct DemStage {
+    double2 lg[DEM_BATCH];       // (L, system output) of the batch's hours, grouped by period
+    int off[DCP + 1];            // period q's hours: [off[q], off[q + 1])
+    int pad[(16 - (DCP + 1) % 16) % 16];
+};
+constexpr size_t DEM_STAGE_BYTES = sizeof(DemStage);
+static_assert(DEM_STAGE_BYTES % 16 == 0, "stage keeps 16-B alignment");
+
+template <int LPA>
+__device__ double yl_demand_staged(const dgen_demand* D, const YSrc& src, double s, bool with_gen,
+                                   const YLds& S, DemStage* st, const Seg<LPA>& g) {
+    constexpr int HPL = DEM_BATCH / LPA;              // hours each lane stages (1 or 2)
+    const uint64_t segmask = LPA == WAVE ? ~0ull : (((1ull << LPA) - 1ull) << g.base);
+    const uint64_t below = ((1ull << g.lane) - 1ull) & segmask;   // segment lanes before this one
+    const int k0 = g.sl * HPL;
+    double total = 0.0;
+    for (int m = 0; m < 12; m++) {
+        double flat = 0.0;
+        for (int q = 0; q < DCP; q++) S.at(q) = 0.0;
+        const int h_lo = c_month_start_day[m] * 24, h_hi = c_month_start_day[m + 1] * 24;
+#pragma unroll 1
+        for (int hb = h_lo; hb < h_hi; hb += DEM_BATCH) {
+            const int nb = (h_hi - hb) < DEM_BATCH ? (h_hi - hb) : DEM_BATCH;
+            double Lv[HPL], gv[HPL];
+            int pv[HPL];
+#pragma unroll
+            for (int u = 0; u < HPL; u++) {
+                const bool valid = k0 + u < nb;
+                const int hu = hb + (valid ? k0 + u : 0);
+                const int d = hu / 24, hod = hu - d * 24;
+                const int pp = ((d % 7) >= 5) ? D->wkend[m][hod] : D->wkday[m][hod];
+                pv[u] = valid ? (pp < DCP ? pp : 0) : -1;
+                Lv[u] = (double)src.shape[hu] * src.load_scale;
+                gv[u] = with_gen ? src.sysgen[(int64_t)(hu >> 2) * src.sys_stride * 4 + (hu & 3)] : 0.0;
+            }
+            wave_lds_sync();                          // previous batch fully read
+            int base_q = 0;
+#pragma unroll 1
+            for (int q = 0; q < DCP; q++) {
+                uint64_t b[HPL];
+                int cnt = 0;
+#pragma unroll
+                for (int u = 0; u < HPL; u++) {
+                    b[u] = __ballot(pv[u] == q) & segmask;
+                    cnt += __popcll(b[u]);
+                }
+                int pos = base_q;
+#pragma unroll
+                for (int u = 0; u < HPL; u++) pos += __popcll(b[u] & below);
+#pragma unroll
+                for (int u = 0; u < HPL; u++) {
+                    if (pv[u] == q) st->lg[pos++] = make_double2(Lv[u], gv[u]);
+                }
+                if (g.sl == 0) st->off[q] = base_q;
+                base_q += cnt;
+            }
+            if (g.sl == 0) st->off[DCP] = base_q;
+            wave_lds_sync();
+            for (int q = 0; q < DCP; q++) {
+                const int lo = st->off[q], hi = st->off[q + 1];
+                if (lo == hi) continue;
+                double mx = -INFINITY;
+#pragma unroll 4
+                for (int k = lo; k < hi; k++) {
+                    const double2 v = st->lg[k];           // one ds_read_b128 per hour
+                    const double imp = v.x - v.y * s;
+                    mx = imp > mx ? imp : mx;
+                }
+                flat = mx > flat ? mx : flat;
+                double& pk = S.at(q);
+                pk = mx > pk ? mx : pk;
             }
         }
         double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
@@ -2319,7 +2409,10 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     if (DC && dem) {   // k_size's first_without already carries the no-system demand charge
         for (int pass = same_tariff ? 1 : 0; pass < 2; pass++) {
             const bool wg = pass == 1;
-            const double v = yl_demand(dem, src, 0.0, wg ? s_y : 1.0, wg, S);
+            // the segment's LDS stage sits after the year-lane layout
+            DemStage* stage = reinterpret_cast<DemStage*>(reinterpret_cast<char*>(dyn_lds) +
+                                                          ylds_bytes(half, LPA)) + (lane / LPA);
+            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);
             if (wg) wb += v;
             else wo1 += v;
         }
@@ -3067,7 +3160,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     const int lpa_s = (fits32 && !(dc ? DGEN_NO2_SIZE_DC : DGEN_NO2_SIZE)) ? 32 : WAVE;
     const int lpa_f = (fits32 && !(dc ? DGEN_NO2_FIN_DC : DGEN_NO2_FIN)) ? 32 : WAVE;
     const size_t ylds_s = ylds_bytes(lds_half(T->max_periods), lpa_s);
-    const size_t ylds_f = ylds_bytes(lds_half(T->max_periods), lpa_f);
+    // k_batt_finance's demand-charge instantiations stage hours per segment
+    const size_t ylds_f = ylds_bytes(lds_half(T->max_periods), lpa_f) +
+                          (dc ? (size_t)(WAVE / lpa_f) * DEM_STAGE_BYTES : 0);
     hipStream_t s2 = c->s2;
     char* const nbws = n_scratch > 0 ? ws_nb(ws, n, n_scratch) : nullptr;
     HIP_TRY(hipEventRecord(c->fork, s));

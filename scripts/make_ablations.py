@@ -112,6 +112,9 @@ VARIANTS = {
                ('extern "C" {', 'extern "C" {\nint32_t dgen_debug_dcdbg(void* dst) { return (int32_t)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dcdbg), sizeof(g_dcdbg)); }')],
     # two-agent demand-charge k_size at 1 wave per SIMD (round 1's no-spill build; now 2 waves)
     "ks_dc_occ1": [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)")],
+    # k_batt_finance without its battery-case demand pass (what the rest costs)
+    "kf_no_dem": [("            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);",
+                   "            const double v = 0.0 * (double)(size_t)stage;")],
 }
 
 
