@@ -753,6 +753,11 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     DayRaw r;
     for (int m = m_lo; m < m_hi; m++) {
         for (int p = 0; p < P; p++) bins[p * BLOCK] = make_double2(0.0, 0.0);
+        // the current period's bin in registers (the same additions in the same
+        // order as a per-hour LDS read-modify-write), written back when the
+        // period changes and at the month's end
+        int bcur = 0;
+        double2 bacc = make_double2(0.0, 0.0);
         // the month's weekday / weekend period rows (24 bytes each, 8-aligned)
         // in 6 registers, loaded once per month: the day loop below then
         // issues no compiler-visible load (see the pipeline note above); the
@@ -818,13 +823,17 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 }
                 if (!mo2) {   // NEM energy bill from bins (demand charges also read the plane)
                     const int p = (int)((sched[hh >> 3] >> (8 * (hh & 7))) & 0xffu);
-                    double2 b = bins[p * BLOCK];
-                    b.x += ld;
-                    b.y += st.sys;
-                    bins[p * BLOCK] = b;
+                    if (p != bcur) {
+                        bins[bcur * BLOCK] = bacc;
+                        bcur = p;
+                        bacc = bins[p * BLOCK];
+                    }
+                    bacc.x += ld;
+                    bacc.y += st.sys;
                 }
             }
         }
+        if (!mo2) bins[bcur * BLOCK] = bacc;
         if (!mo2) {
             // agent-major (load, system) pairs: k_batt_finance's lanes read the
             // agent's 12 P cells as one contiguous run
