@@ -90,7 +90,8 @@ OUTPUT_HOURLY = ["baseline", "net_pvonly", "net_with_batt"]
 class Outputs(ctypes.Structure):
     _fields_ = ([(name, _vp) for name, _ in OUTPUT_SCALARS]
                 + [(name, _vp) for name in OUTPUT_YEARLY]
-                + [(name, _vp) for name in OUTPUT_HOURLY])
+                + [(name, _vp) for name in OUTPUT_HOURLY]
+                + [("hourly_f64", ctypes.c_int32), ("pad_", ctypes.c_int32)])
 
 
 class DgenError(RuntimeError):
@@ -99,7 +100,7 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
-ABI_VERSION = 5   # include/dgen_hip.h DGEN_ABI_VERSION
+ABI_VERSION = 6   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
 

@@ -176,9 +176,9 @@ def export_weights(engine, customers_in_bin, number_of_adopters, batt_kw_cum_las
 
 def state_hourly(engine, planes, weights, idx, seg_off):
     """k_state_hourly: planes = (baseline, pvonly, with_batt) device tensors,
-    float32 in dgen_size_agents' hour-quad tiles [n_hours / 4, n, 4] (the sizing
-    outputs in place; engine.tile_hourly makes them from [n_hours, n]) or
-    float64 [n_hours, n]; weights from export_weights(), idx: plane column of
+    float32 or float64 in dgen_size_agents' hour-quad tiles [n_hours / 4, n, 4]
+    (the sizing outputs in place; engine.tile_hourly makes them from
+    [n_hours, n]) or float64 [n_hours, n]; weights from export_weights(), idx: plane column of
     each group member (None: identity), seg_off [S+1].  Returns a [S, n_hours]
     float64 device tensor in MW."""
     import torch
@@ -187,16 +187,19 @@ def state_hourly(engine, planes, weights, idx, seg_off):
     base, pvo, wbt = planes
     if any(p.shape != base.shape or p.dtype != base.dtype for p in (pvo, wbt)):
         raise ValueError("state_hourly: the three planes must share shape and dtype")
-    if base.dtype == torch.float32:
-        if base.dim() != 3 or base.shape[2] != 4:
-            raise ValueError("state_hourly: float32 planes must be hour-quad tiles [n_hours/4, n, 4]")
-        nh, n = base.shape[0] * 4, base.shape[1]
-    elif base.dtype == torch.float64:
-        if base.dim() != 2:
-            raise ValueError("state_hourly: float64 planes must be [n_hours, n]")
-        nh, n = base.shape
-    else:
+    if base.dtype not in (torch.float32, torch.float64):
         raise TypeError("state_hourly: planes must be float32 or float64")
+    if base.dim() == 3:
+        if base.shape[2] != 4:
+            raise ValueError("state_hourly: tiled planes must be hour-quad tiles [n_hours/4, n, 4]")
+        nh, n = base.shape[0] * 4, base.shape[1]
+        layout = 1 if base.dtype == torch.float32 else 2
+    elif base.dtype == torch.float64 and base.dim() == 2:
+        nh, n = base.shape
+        layout = 0
+    else:
+        raise ValueError("state_hourly: float32 planes must be hour-quad tiles [n_hours/4, n, 4]; "
+                         "float64 planes tiles or [n_hours, n]")
     if any(w.numel() != n for w in weights):
         raise ValueError("state_hourly: one weight per plane column")
     so = np.asarray(seg_off, dtype=np.int64)
@@ -216,7 +219,7 @@ def state_hourly(engine, planes, weights, idx, seg_off):
     keep = [p.contiguous() for p in planes] + [w.contiguous() for w in weights]
     t_off = eng._to_dev(so, torch.int64)
     _lib.check(L.dgen_state_hourly(eng.ctx, keep[0].data_ptr(), keep[1].data_ptr(),
-                                   keep[2].data_ptr(), int(base.dtype == torch.float32),
+                                   keep[2].data_ptr(), layout,
                                    keep[3].data_ptr(), keep[4].data_ptr(), keep[5].data_ptr(),
                                    None if ti is None else ti.data_ptr(), n, nh, t_off.data_ptr(),
                                    S, out.data_ptr(), eng.stream_handle()), "dgen_state_hourly")

@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <type_traits>
 
 #include "../../include/dgen_hip.h"
 
@@ -533,6 +534,15 @@ __device__ __forceinline__ void st_f32x4(char* row, uint32_t off, const float (&
     const f32x4 v = {q[0], q[1], q[2], q[3]};
     asm volatile("global_store_dwordx4 %0, %1, %2 nt" :: "v"(off), "v"(v), "s"(row) : "memory");
 }
+// The fp64 planes' form (dgen_outputs.hourly_f64): the lane's 4 hours as 32 B,
+// two stores
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_f32x4(char* row, uint32_t off, const double (&q)[4]) {
+    const f64x2 a = {q[0], q[1]}, b = {q[2], q[3]};
+    asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\t"
+                 "global_store_dwordx4 %0, %3, %2 offset:16 nt"
+                 :: "v"(off), "v"(a), "s"(row), "v"(b) : "memory");
+}
 
 // One hour of the dispatch (same arithmetic as the oracle's branchy
 // orc_batt_dispatch, written without divergence): charge when the net load is
@@ -631,7 +641,9 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
     }
 }
 
-template <bool HOURLY>
+// F64: the hourly planes as doubles (the reference's fp64 lists) instead of
+// floats: the same values the scan computes, 32 B per lane per hour quad.
+template <bool HOURLY, bool F64>
 __global__ void __launch_bounds__(BLOCK, 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on) {
@@ -711,10 +723,12 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // at ((h / 4) * n + i) * 4 + h % 4, so a lane stores 16 B and a wave 1 KB
     // contiguous per plane every 4 hours (measured 29.3 -> 27.9 ms vs one
     // 4-B store per lane-hour)
-    const uint32_t off16 = (uint32_t)i * 16u;
-    const size_t row16 = (size_t)n * 16u;
+    using PT = typename std::conditional<F64, double, float>::type;
+    constexpr uint32_t QB = 4 * sizeof(PT);          // bytes per lane per hour quad
+    const uint32_t off16 = (uint32_t)i * QB;
+    const size_t row16 = (size_t)n * QB;
     size_t q16 = (size_t)d_lo * 6 * row16;
-    float qb[4], qp[4], qw[4];
+    PT qb[4], qp[4], qw[4];
 
     // Software pipeline over days through LDS: the next day's raw profile
     // values (96 B of the shape row + 96 B of the cf row per lane) are DMA'd
@@ -770,7 +784,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             swe[0] = b[0]; swe[1] = b[1]; swe[2] = b[2];
         }
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
-            if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA>(dlane, r);
+            if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);
             else day_read<0>(dlane, r);
             const bool wkend = (d % 7) >= 5;
             const uint64_t sched[3] = {wkend ? swe[0] : swd[0], wkend ? swe[1] : swd[1],
@@ -802,9 +816,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                                         in_per_bank, out_per_bank);
                 if constexpr (HOURLY) {
                     const double dn = ld - pl;
-                    qb[hh & 3] = (float)ld;
-                    qp[hh & 3] = (float)fmax(dn, 0.0);
-                    qw[hh & 3] = (float)st.g2l;
+                    qb[hh & 3] = (PT)ld;
+                    qp[hh & 3] = (PT)fmax(dn, 0.0);
+                    qw[hh & 3] = (PT)st.g2l;
                     if ((hh & 3) == 3) {
                         st_f32x4(ob + q16, off16, qb);
                         st_f32x4(op + q16, off16, qp);
@@ -2739,7 +2753,7 @@ __global__ void k_export_weights(const double* __restrict__ customers, const dou
 // state-major device order); a scattered idx fetches a 128-B line per 16-B
 // quad.  Fixed reduction order.
 constexpr int SH_TILE = 32;
-template <typename V>
+template <typename V, bool TILED>
 __global__ void __launch_bounds__(256)
 k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
                const V* __restrict__ wbt, const double* __restrict__ w_pvo,
@@ -2758,18 +2772,32 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
     for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
         const int64_t c = idx ? idx[i] : i;
         const double a = w_pvo[c], b = w_batt[c], d = w_non[c];
-        if constexpr (sizeof(V) == 4) {
+        if constexpr (TILED) {
             // nh % 4 == 0 (host), h0 % 4 == 0: whole quads
 #pragma unroll
             for (int q = 0; q < SH_TILE / 4; q++) {
                 if (4 * q < nt) {
                     const int64_t r = (((int64_t)(h0 >> 2) + q) * n + c) * 4;
-                    const f32x4 vp = *reinterpret_cast<const f32x4*>(pvo + r);
-                    const f32x4 vw = *reinterpret_cast<const f32x4*>(wbt + r);
-                    const f32x4 vb = *reinterpret_cast<const f32x4*>(base + r);
+                    double vp[4], vw[4], vb[4];
+                    if constexpr (sizeof(V) == 4) {
+                        const f32x4 xp = *reinterpret_cast<const f32x4*>(pvo + r);
+                        const f32x4 xw = *reinterpret_cast<const f32x4*>(wbt + r);
+                        const f32x4 xb = *reinterpret_cast<const f32x4*>(base + r);
+#pragma unroll
+                        for (int u = 0; u < 4; u++) { vp[u] = xp[u]; vw[u] = xw[u]; vb[u] = xb[u]; }
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 4; u += 2) {
+                            const double2 xp = *reinterpret_cast<const double2*>(pvo + r + u);
+                            const double2 xw = *reinterpret_cast<const double2*>(wbt + r + u);
+                            const double2 xb = *reinterpret_cast<const double2*>(base + r + u);
+                            vp[u] = xp.x; vp[u + 1] = xp.y; vw[u] = xw.x; vw[u + 1] = xw.y;
+                            vb[u] = xb.x; vb[u + 1] = xb.y;
+                        }
+                    }
 #pragma unroll
                     for (int u = 0; u < 4; u++)
-                        acc[4 * q + u] += ((double)vp[u] * a + (double)vw[u] * b) + (double)vb[u] * d;
+                        acc[4 * q + u] += (vp[u] * a + vw[u] * b) + vb[u] * d;
                 }
             }
         } else {
@@ -3113,9 +3141,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     }
     // k_hourly_batt forms a 32-bit per-lane byte offset i x 16 into the hourly tiles
     if (n >= ((int64_t)1 << 29) || n_scratch >= ((int64_t)1 << 28) ||
-        (hourly && n >= ((int64_t)1 << 28))) {
-        set_err("dgen_size_agents: batch too large (n < 2^29, n < 2^28 with hourly planes, "
-                "n_scratch < 2^28 per call)");
+        (hourly && n >= ((int64_t)1 << (O->hourly_f64 ? 27 : 28)))) {
+        set_err("dgen_size_agents: batch too large (n < 2^29, n < 2^28 with f32 hourly planes, "
+                "2^27 with f64, n_scratch < 2^28 per call)");
         return DGEN_E_ARG;
     }
     if (!ws || ws_bytes < dgen_workspace_bytes(n, n_scratch)) {
@@ -3217,11 +3245,14 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         dim3 grid((unsigned)((m + BLOCK - 1) / BLOCK)), block(BLOCK);
         for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
-            if (hourly)
-                hipLaunchKernelGGL(k_hourly_batt<true>, grid, block, lds, s2, *T, *A, *O, c->cfg, n,
+            if (hourly && O->hourly_f64)
+                hipLaunchKernelGGL((k_hourly_batt<true, true>), grid, block, lds, s2, *T, *A, *O, c->cfg, n,
+                                   ws, n_scratch, i0, i1, m0, m1, c->battery);
+            else if (hourly)
+                hipLaunchKernelGGL((k_hourly_batt<true, false>), grid, block, lds, s2, *T, *A, *O, c->cfg, n,
                                    ws, n_scratch, i0, i1, m0, m1, c->battery);
             else
-                hipLaunchKernelGGL(k_hourly_batt<false>, grid, block, lds, s2, *T, *A, *O, c->cfg, n,
+                hipLaunchKernelGGL((k_hourly_batt<false, false>), grid, block, lds, s2, *T, *A, *O, c->cfg, n,
                                    ws, n_scratch, i0, i1, m0, m1, c->battery);
         }
         HIP_TRY(hipEventRecord(e[3], s2));
@@ -3427,6 +3458,10 @@ int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
         set_err("dgen_state_hourly: bad argument");
         return DGEN_E_ARG;
     }
+    if (planes_f32 < 0 || planes_f32 > 2) {
+        set_err("dgen_state_hourly: planes_f32 must be 0 (f64 [h][n]), 1 (f32 tiles) or 2 (f64 tiles)");
+        return DGEN_E_ARG;
+    }
     if (planes_f32 && n_hours % 4 != 0) {
         set_err("dgen_state_hourly: f32 (hour-quad tiled) planes need n_hours %% 4 == 0");
         return DGEN_E_ARG;
@@ -3434,12 +3469,16 @@ int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
     if (n_seg == 0) return DGEN_OK;
     HIP_TRY(hipSetDevice(c->device));
     const dim3 grid((unsigned)n_seg, (unsigned)((n_hours + SH_TILE - 1) / SH_TILE));
-    if (planes_f32)
-        hipLaunchKernelGGL(k_state_hourly<float>, grid, dim3(256), 0, (hipStream_t)stream,
+    if (planes_f32 == 2)
+        hipLaunchKernelGGL((k_state_hourly<double, true>), grid, dim3(256), 0, (hipStream_t)stream,
+                           (const double*)baseline, (const double*)pvonly, (const double*)with_batt,
+                           w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);
+    else if (planes_f32)
+        hipLaunchKernelGGL((k_state_hourly<float, true>), grid, dim3(256), 0, (hipStream_t)stream,
                            (const float*)baseline, (const float*)pvonly, (const float*)with_batt,
                            w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);
     else
-        hipLaunchKernelGGL(k_state_hourly<double>, grid, dim3(256), 0, (hipStream_t)stream,
+        hipLaunchKernelGGL((k_state_hourly<double, false>), grid, dim3(256), 0, (hipStream_t)stream,
                            (const double*)baseline, (const double*)pvonly, (const double*)with_batt,
                            w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);
     HIP_TRY(hipGetLastError());

@@ -239,7 +239,10 @@ class Engine:
                       or int((off.long() + cnt.long()).max().item()) > T.n_switches):
                 raise ValueError(f"rate-switch ({k}) offsets out of range")
 
-    def alloc_outputs(self, n: int, hourly: bool = True) -> Dict[str, object]:
+    def alloc_outputs(self, n: int, hourly: bool = True, hourly_f64: bool = False) -> Dict[str, object]:
+        """Device output buffers for n agents.  hourly_f64: the three hourly
+        planes as float64 (the reference's fp64 lists, the kernels' own
+        values) instead of float32 (half the bytes; the default)."""
         torch = _torch()
         out = {}
         for name, dt in _lib.OUTPUT_SCALARS:
@@ -249,8 +252,8 @@ class Engine:
             out[name] = torch.zeros((n, _lib.MAXY + 1), dtype=torch.float64, device=self.dev)
         for name in _lib.OUTPUT_HOURLY:
             # hour-quad tiles (include/dgen_hip.h): [NH / 4][n][4]
-            out[name] = (torch.empty((_lib.NH // 4, n, 4), dtype=torch.float32, device=self.dev)
-                         if hourly else None)
+            out[name] = (torch.empty((_lib.NH // 4, n, 4), dtype=torch.float64 if hourly_f64 else torch.float32,
+                                     device=self.dev) if hourly else None)
         return out
 
     @staticmethod
@@ -258,6 +261,12 @@ class Engine:
         fields = {name: _ptr(out[name]) for name, _ in _lib.OUTPUT_SCALARS}
         fields.update({name: _ptr(out[name]) for name in _lib.OUTPUT_YEARLY})
         fields.update({name: _ptr(out.get(name)) for name in _lib.OUTPUT_HOURLY})
+        planes = [out.get(name) for name in _lib.OUTPUT_HOURLY if out.get(name) is not None]
+        dts = {p.dtype for p in planes}
+        if len(dts) > 1:
+            raise TypeError("hourly planes must share one dtype")
+        torch = _torch()
+        fields["hourly_f64"] = int(bool(planes) and planes[0].dtype == torch.float64)
         return _lib.Outputs(**fields)
 
     def size(self, batch: AgentBatch, out: Dict[str, object], c_out: Optional[_lib.Outputs] = None):

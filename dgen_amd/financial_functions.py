@@ -171,7 +171,8 @@ def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[
     t0 = time.perf_counter()
     _device_tables(eng, src, b)
     batch = eng.upload_agents(cols, order=profile_order(cols))
-    out = eng.alloc_outputs(batch.n, hourly=True)
+    # fp64 hourly planes: the reference's hourly lists are fp64 (ff:523,536-539)
+    out = eng.alloc_outputs(batch.n, hourly=True, hourly_f64=True)
     torch.cuda.synchronize(eng.dev)
     t1 = time.perf_counter()
     eng.size(batch, out)
@@ -301,7 +302,8 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     output columns are assigned whole.  Same values and columns as mapping
     calc_system_size_and_performance over the rows (ff:449-565 write order);
     hourly: "list" (the reference's fp64 lists), "array" (each cell a row
-    view of one [n, 8760] float32 array, no per-agent copy) or "none".
+    view of one [n, 8760] float64 array, no per-agent copy) or "none".  The
+    device computes the hourly planes in fp64 for this path.
     timing: filled with the host / device phases (seconds)."""
     import time
     if rate_switch_table is None:
@@ -348,7 +350,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     out["utility_bill_w_sys_pv_batt"] = _yearly_lists(o["bill_w_batt"], n1)
     out["utility_bill_wo_sys_pv_batt"] = _yearly_lists(o["bill_wo_batt"], n1)
     if hourly != "none":
-        conv = ((lambda a: [r.astype(np.float64).tolist() for r in a]) if hourly == "list"
+        conv = ((lambda a: a.tolist()) if hourly == "list"
                 else (lambda a: list(a)))
         out["baseline_net_hourly"] = conv(o["baseline"])
         out["adopter_net_hourly_pvonly"] = conv(o["net_pvonly"])

@@ -109,23 +109,30 @@ def day_dma_wait(path, kernel="k_hourly_battILb1E"):
     order, so the 12 global_load_lds_dwordx4 of the previous day have landed if
     at least K vector-memory ops are issued after the last of them on every
     path to the wait.  Counts the ops between the last DMA and the loop's back
-    edge outside blocks an `s_cbranch_execz` can skip.  Returns (K, issued)."""
+    edge outside blocks an `s_cbranch_execz` can skip.  Every instantiation
+    whose symbol contains `kernel` is checked; returns the (K, issued) pair
+    with the smallest margin."""
     lines = open(path).read().split("\n")
-    st = next(i for i, l in enumerate(lines) if re.match(r"_Z\S*" + kernel + r"\S*:", l))
-    en = next(i for i in range(st, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
-    body = [l.strip() for l in lines[st:en]]
-    waits = [int(re.search(r"vmcnt\((\d+)\)", body[i]).group(1)) for i in range(len(body) - 1)
-             if body[i].startswith("s_waitcnt") and "vmcnt(" in body[i] and body[i + 1].startswith("ds_read_b128")]
-    k = max(waits)
-    last = max(i for i, l in enumerate(body) if l.startswith("global_load_lds_dwordx4"))
-    issued, cond = 0, False
-    for l in body[last + 1:]:
-        if l.startswith(".LBB"):
-            cond = False
-        elif l.startswith("s_cbranch_execz"):
-            cond = True
-        elif l.startswith("s_branch"):
-            break
-        elif re.match(r"(global_|buffer_|scratch_)", l) and not cond:
-            issued += 1
-    return k, issued
+    starts = [i for i, l in enumerate(lines) if re.match(r"_Z\S*" + kernel + r"\S*:", l)]
+    worst = None
+    for st in starts:
+        en = next(i for i in range(st, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
+        body = [l.strip() for l in lines[st:en]]
+        waits = [int(re.search(r"vmcnt\((\d+)\)", body[i]).group(1)) for i in range(len(body) - 1)
+                 if body[i].startswith("s_waitcnt") and "vmcnt(" in body[i]
+                 and body[i + 1].startswith("ds_read_b128")]
+        k = max(waits)
+        last = max(i for i, l in enumerate(body) if l.startswith("global_load_lds_dwordx4"))
+        issued, cond = 0, False
+        for l in body[last + 1:]:
+            if l.startswith(".LBB"):
+                cond = False
+            elif l.startswith("s_cbranch_execz"):
+                cond = True
+            elif l.startswith("s_branch"):
+                break
+            elif re.match(r"(global_|buffer_|scratch_)", l) and not cond:
+                issued += 1
+        if worst is None or issued - k < worst[1] - worst[0]:
+            worst = (k, issued)
+    return worst

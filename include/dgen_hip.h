@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 5
+#define DGEN_ABI_VERSION 6
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_NH    8760   /* hours per year                                    */
@@ -219,9 +219,13 @@ typedef struct {
     double* cfev_batt;             /* [n][MAXY+1] cf_energy_value_pv_batt             */
     double* bill_w_batt;           /* [n][MAXY+1] utility_bill_w_sys_pv_batt          */
     double* bill_wo_batt;          /* [n][MAXY+1] utility_bill_wo_sys_pv_batt         */
-    float*  baseline;              /* [2190][n][4] baseline_net_hourly (may be NULL)  */
-    float*  net_pvonly;            /* [2190][n][4] adopter_net_hourly_pvonly          */
-    float*  net_with_batt;         /* [2190][n][4] adopter_net_hourly_with_batt       */
+    void*   baseline;              /* [2190][n][4] baseline_net_hourly (may be NULL)  */
+    void*   net_pvonly;            /* [2190][n][4] adopter_net_hourly_pvonly          */
+    void*   net_with_batt;         /* [2190][n][4] adopter_net_hourly_with_batt       */
+    int32_t hourly_f64;            /* plane element type: 0 float (default), 1 double */
+                                   /* (the reference's fp64 lists, bit-for-bit the    */
+                                   /* values the kernels compute; 2 x the bytes)      */
+    int32_t pad_;
 } dgen_outputs;
 
 typedef struct dgen_ctx dgen_ctx;
@@ -366,9 +370,10 @@ int32_t dgen_export_weights(dgen_ctx* ctx, const double* customers_in_bin,
                             double* w_batt, double* w_non, void* stream);
 
 /* Per-state hourly net sums in MW (:179-198) from the three hourly planes
- * (float32 when planes_f32 != 0: dgen_size_agents' hourly outputs in place,
- * in their hour-quad tiles [n_hours / 4][n][4], n_hours % 4 == 0; else
- * float64 [n_hours][n]) and the per-column weights:
+ * (planes_f32 = 1: float32 in dgen_size_agents' hour-quad tiles
+ * [n_hours / 4][n][4], its hourly outputs in place, n_hours % 4 == 0;
+ * 2: the same tiles in float64 (dgen_outputs.hourly_f64); 0: float64
+ * [n_hours][n]) and the per-column weights:
  * out[s * n_hours + h].  Members of state s are the plane columns
  * idx[seg_off[s] .. seg_off[s+1]) (idx NULL: columns seg_off[s] ..
  * seg_off[s+1]).  Fixed summation order (deterministic); the reference's

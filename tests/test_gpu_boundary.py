@@ -29,7 +29,11 @@ def _check_row(out, g, i, arr, hourly=True):
         for k in ("baseline_net_hourly", "adopter_net_hourly_pvonly", "adopter_net_hourly_with_batt"):
             ref = arr[f"{i}__{k}"]
             assert len(out[k]) == 8760
-            assert np.allclose(out[k], ref, rtol=2e-6, atol=2e-6 * max(1.0, np.abs(ref).max())), (g["tag"], k)
+            # the drop-in path computes the planes in fp64 (dgen_outputs.hourly_f64),
+            # like the reference's lists: only the generation term's association
+            # (cf x (kW x 0.96 / 1e6) vs ((cf / 1e6) x kW ...)) differs in the last bits
+            assert isinstance(out[k][0], float)
+            assert np.allclose(out[k], ref, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(ref).max())), (g["tag"], k)
 
 
 def test_calc_system_size_and_performance_single_rows():

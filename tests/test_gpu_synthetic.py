@@ -185,3 +185,39 @@ def test_pv_only_variant(engine, cfg):
     pv = cf * (((kw * 1000.0) * 0.96) / 1000.0)[:, None]
     ref = np.maximum(load - pv, 0.0).astype(np.float32)
     assert np.allclose(b["net_with_batt"], ref, rtol=1e-5, atol=1e-4)
+
+
+def test_hourly_f64_planes(engine):
+    """dgen_outputs.hourly_f64: the planes as doubles are the values the scan
+    computes -- rounding them to float32 gives the float32 planes bit for bit --
+    and they match the oracle's fp64 hourly outputs to 1e-12; the per-state
+    export reads either tile type."""
+    from dgen_amd.attachment import state_hourly
+    pop = _small_pop("national_mixed", 300)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    o32 = engine.alloc_outputs(batch.n, hourly=True)
+    o64 = engine.alloc_outputs(batch.n, hourly=True, hourly_f64=True)
+    engine.size(batch, o32)
+    engine.size(batch, o64)
+    torch.cuda.synchronize()
+    for k in ("baseline", "net_pvonly", "net_with_batt"):
+        assert o64[k].dtype == torch.float64
+        assert torch.equal(o64[k].to(torch.float32), o32[k]), k
+    h = outputs_to_host(o64)
+    opop = helpers.oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs,
+                                     pop.wholesale)
+    ref = opop.run(orc.make_cfg(), hourly=True)
+    for i, r in enumerate(ref):
+        for k_o, k_r in (("net_pvonly", "adopter_net_hourly_pvonly"),
+                         ("net_with_batt", "adopter_net_hourly_with_batt")):
+            a, b = h[k_o][i], np.asarray(r[k_r], float)
+            assert np.allclose(a, b, rtol=1e-12, atol=1e-12 * max(1.0, np.abs(b).max())), (i, k_o)
+    n = batch.n
+    w = tuple(torch.rand(n, dtype=torch.float64, device=engine.dev) for _ in range(3))
+    seg = [0, n // 3, n]
+    s32 = state_hourly(engine, (o32["baseline"], o32["net_pvonly"], o32["net_with_batt"]), w, None, seg)
+    s64 = state_hourly(engine, (o64["baseline"], o64["net_pvonly"], o64["net_with_batt"]), w, None, seg)
+    assert torch.allclose(s32, s64, rtol=1e-6, atol=1e-9)
