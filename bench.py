@@ -215,6 +215,11 @@ def main():
     el = timed_region(lambda: eng.size(batch, out, c_out), args.steps, torch.cuda.synchronize,
                       dist if ws > 1 else None, eng.dev)
     ms_size, ms_hourly, ms_fin, cnt = eng.kernel_times()
+    if os.environ.get("DGEN_PHASE_PROF") and hasattr(eng.lib, "dgen_phase_read"):   # ablation builds only
+        import ctypes
+        ph = (ctypes.c_uint64 * 16)()
+        if eng.lib.dgen_phase_read(ph, 0) == 0:
+            print(json.dumps({"phase_cycles": list(ph)}), file=sys.stderr, flush=True)
 
     st = out["status"].cpu().numpy()
     n_bad = int(((st & 0x3B) != 0).sum())

@@ -921,6 +921,24 @@ struct Seg {
     __device__ __forceinline__ double bcast(double v, int k) const { return __shfl(v, base + k, WAVE); }
 };
 
+// Phase timers (DGEN_PHASE_PROF=1 ablation builds only): per-segment shader
+// cycles spent in a phase, summed over segments, read by dgen_phase_read.
+#ifndef DGEN_PHASE_PROF
+#define DGEN_PHASE_PROF 0
+#endif
+#if DGEN_PHASE_PROF
+__device__ unsigned long long g_phase[16];
+#define PH_T0(v) const unsigned long long v = __builtin_readcyclecounter()
+#define PH_ADD(k, v, lead) \
+    do { if (lead) atomicAdd(&g_phase[k], __builtin_readcyclecounter() - (v)); } while (0)
+#define PH_CNT(k, n, lead) \
+    do { if (lead) atomicAdd(&g_phase[k], (unsigned long long)(n)); } while (0)
+#else
+#define PH_T0(v) do {} while (0)
+#define PH_ADD(k, v, lead) do {} while (0)
+#define PH_CNT(k, n, lead) do {} while (0)
+#endif
+
 // LDS hand-off between the lanes of one wave (every year-lane block is one
 // wave): orders the LDS stores before the loads without s_barrier, so it is
 // also correct where the two agents of a wave have diverged.
@@ -1799,11 +1817,24 @@ __device__ __forceinline__ float nb_weight_f(const YSrc& src, int h) {
 }
 __device__ __forceinline__ double nb_weight(const YSrc& src, int h) { return (double)nb_weight_f(src, h); }
 
+// The segment builds the split cooperatively: lane k < 24 of the segment
+// takes hour k of every day (all days of a month share one period per hour
+// and day type), so a month is ~30 steps of 24 hours in parallel instead of
+// 730 serial hours on one lane.  Each hour lane sums its own import / export
+// terms per day type in registers (day order); at the month's end the lanes
+// hand them over through their LDS columns and lane r = 4 p + q adds the
+// (hour, day type) partials whose period is p, hours in order, weekdays
+// first -- a fixed order, a re-association of the serial hour sums.  The
+// mixed hours are appended in hour order (ballot rank within the day).
+// Returns true when every month's M hours fit (segment-uniform).
+#ifndef DGEN_NB_SERIAL
+#define DGEN_NB_SERIAL 0
+#endif
 // Month lane m < 12 of the segment builds month m (accumulators in its LDS
 // column, at(4 p + q), 4 P <= 4 half).  Returns true when every month's M
 // hours fit (segment-uniform).
 template <int LPA>
-__device__ bool yl_nb_build(const dgen_tariff& t, const YSrc& src, double tlo, double thi, char* nbp,
+__device__ bool yl_nb_build_serial(const dgen_tariff& t, const YSrc& src, double tlo, double thi, char* nbp,
                             const YLds& S, const Seg<LPA>& g) {
     bool ok = true;
     const int m = g.sl;
@@ -1870,40 +1901,238 @@ __device__ bool yl_nb_build(const dgen_tariff& t, const YSrc& src, double tlo, d
     return g.first(!ok) < 0;
 }
 
+// days per load batch: the battery case's f64 system output takes twice the
+// registers of the cf row, and k_batt_finance stays at 3 waves with 4
+#ifndef DGEN_NB_DB_CF
+#define DGEN_NB_DB_CF 8
+#endif
+#ifndef DGEN_NB_DB_SYS
+#define DGEN_NB_DB_SYS 4
+#endif
+template <bool SYS>
+struct NbDays {
+    static constexpr int D = SYS ? DGEN_NB_DB_SYS : DGEN_NB_DB_CF;
+    float sh[D], w[D];
+    int32_t cf[SYS ? 1 : D];
+    double sg[SYS ? D : 1];
+};
+template <bool SYS>
+__device__ __forceinline__ void nb_load_days(const YSrc& src, int d0, int hd, bool act, NbDays<SYS>& b) {
+#pragma unroll
+    for (int k = 0; k < NbDays<SYS>::D; k++) {
+        const int h = (d0 + k) * 24 + hd;
+        const bool v = act && d0 + k < 365;
+        b.sh[k] = v ? src.shape[h] : 0.0f;
+        b.w[k] = (v && src.ts) ? (float)(src.ts[h] * src.ts_mult) : 1.0f;
+        if constexpr (SYS) b.sg[k] = v ? src.sysgen[(int64_t)(h >> 2) * src.sys_stride * 4 + (h & 3)] : 0.0;
+        else b.cf[k] = v ? src.cf[h] : 0;
+    }
+}
+
+// The segment builds the split cooperatively: lane k < 24 of the segment
+// takes hour k of every day (all days of a month share one period per hour
+// and day type), so a month is ~30 steps of 24 hours in parallel instead of
+// 730 serial hours on one lane; the loads of the next batch of days are issued
+// before the current ones are classified.  Each hour lane sums its own
+// import / export terms per day type in registers (day order); at the month's
+// end the lanes hand them over through their LDS columns and lane r = 4 p + q
+// adds the (hour, day type) partials whose period is p, hours in order,
+// weekdays first -- a fixed order, a re-association of the serial hour sums.
+// The mixed hours are appended in hour order (ballot rank within the day).
+// Returns true when every month's M hours fit (segment-uniform).  SYS: the
+// battery case's system output (k_batt_finance), else the per-kW cf row.
+template <bool SYS, int LPA>
+__device__ __forceinline__ bool yl_nb_build(const dgen_tariff& t, const YSrc& src, double tlo, double thi,
+                                            char* nbp, const YLds& S, const Seg<LPA>& g) {
+    const NbRec R = nb_rec(nbp);
+    const int P = t.P;
+    const int hd = g.sl;
+    const bool act = hd < 24;
+    const unsigned long long segm = (LPA == WAVE) ? ~0ull : (((1ull << LPA) - 1ull) << g.base);
+    const unsigned long long below = (1ull << g.lane) - 1ull;
+    double* col0 = S.lane - g.sl;          // the segment's first lane's LDS column
+    bool ok = true;
+    constexpr int DB = NbDays<SYS>::D;
+    NbDays<SYS> cur, nxt;
+    nb_load_days<SYS>(src, 0, hd, act, cur);
+    for (int m = 0; m < 12; m++) {
+        const int pd = act ? (int)t.wkday[m][hd] : 0, pe = act ? (int)t.wkend[m][hd] : 0;
+        double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0};
+        int n_m = 0;
+        NbEnt* ent = R.ent + m * NB_CAPM;
+        const int de = c_month_start_day[m + 1];
+#pragma unroll 1
+        for (int d0 = c_month_start_day[m]; d0 < de; d0 += DB) {
+            nb_load_days<SYS>(src, d0 + DB < de ? d0 + DB : de, hd, act, nxt);
+#pragma unroll
+            for (int k = 0; k < DB; k++) {
+                const int d = d0 + k;
+                if (d >= de) break;
+                const bool we = (d % 7) >= 5;
+                const double L = (double)cur.sh[k] * src.load_scale;
+                double gk;
+                if constexpr (SYS) gk = cur.sg[k];
+                else gk = cf_per_kw(cur.cf[k]);
+                const float w = cur.w[k];
+                const double vlo = L - gk * tlo, vhi = L - gk * thi;
+                const double slack = 1e-10 * (fabs(L) + fabs(gk) * thi);
+                const bool imp = act && fmin(vlo, vhi) > slack;            // imports at every t
+                const bool exq = act && !imp && fmax(vlo, vhi) < -slack;   // exports at every t
+                const double wd = (double)w;
+                const double i0 = imp ? L : 0.0, i1 = imp ? gk : 0.0;
+                const double x0 = exq ? gk * wd : 0.0, x1 = exq ? L * wd : 0.0;
+                if (we) {
+                    a1[0] += i0; a1[1] += i1; a1[2] += x0; a1[3] += x1;
+                } else {
+                    a0[0] += i0; a0[1] += i1; a0[2] += x0; a0[3] += x1;
+                }
+                const bool mx = act && !imp && !exq;
+                const unsigned long long bm = __ballot(mx) & segm;
+                if (mx) {
+                    const int pos = n_m + __popcll(bm & below);
+                    if (pos < NB_CAPM) {
+                        NbEnt e;
+                        e.L = L;
+                        e.g = gk;
+                        e.w = w;
+                        e.p = we ? pe : pd;
+                        ent[pos] = e;
+                    }
+                }
+                n_m += __popcll(bm);
+            }
+            cur = nxt;
+        }
+        ok = ok && n_m <= NB_CAPM;
+        if (g.sl == 0) R.cnt[m] = n_m;
+        // (hour, day type) partials -> (period, quantity) sums
+        // lane r and (4 MAXP > LPA) lane r + LPA
+        constexpr int NR = (4 * MAXP + LPA - 1) / LPA;
+        double v[NR];
+#pragma unroll
+        for (int k = 0; k < NR; k++) v[k] = 0.0;
+        for (int dt = 0; dt < 2; dt++) {
+            wave_lds_sync();
+#pragma unroll
+            for (int q = 0; q < 4; q++) S.at(q) = dt ? a1[q] : a0[q];
+            wave_lds_sync();
+            const uint8_t* sc = dt ? t.wkend[m] : t.wkday[m];
+#pragma unroll
+            for (int k = 0; k < NR; k++) {
+                const int r = g.sl + k * LPA;
+                if (r < 4 * P) {
+                    const int p = r >> 2, q = r & 3;
+                    for (int hh = 0; hh < 24; hh++)
+                        if ((int)sc[hh] == p) v[k] += col0[q * WAVE + hh];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NR; k++) {
+            const int r = g.sl + k * LPA;
+            if (r < 4 * P) R.sums[(m * MAXP + (r >> 2)) * 4 + (r & 3)] = v[k];
+        }
+    }
+    // hand-off to the other lanes through global memory, as yl_dc_build
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    wave_lds_sync();
+    return ok;
+}
+
 // Net-billing bill of the lane's year from the split (generation kW' =
 // src.gen_scale, degradation factor s; battery case: src.sysgen with
 // gen_scale 1): yl_bill_mo2's result up to the rounding of the re-associated
 // import / export sums.
+// The M entries reach the lanes through LDS in chunks of LPA: lane k loads
+// entry j0 + k of the next chunk (one coalesced 24-B record per lane) while
+// the segment bills the current chunk out of the lanes' LDS columns (slots
+// 2 half .. 2 half + 2, broadcast reads), so the record's load latency is
+// paid about once per evaluation instead of once per 4 entries; the month's
+// four sums per period are staged the same way (slots 2 half + 3 ..), fetched
+// one month ahead.  Needs 4 half >= 2 half + 3 + NR (dgen_size_agents raises
+// max_periods to 3 for net-billing batches).  Same per-entry arithmetic and
+// order as the hourly pass on the M hours.
+template <int LPA>
 __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& src, double s, char* nbp,
-                                             const YLds& S) {
+                                             const YLds& S, const Seg<LPA>& g) {
     const NbRec R = nb_rec(nbp);
     const int P = t.P, half = S.half;
     const double kws = src.gen_scale;
+    const bool sysg = src.sysgen != nullptr, tsw = src.ts != nullptr;
+    double* col0 = S.lane - g.sl;
+    const int E = 2 * half;                      // staged entry: L, g, (w, p)
+    constexpr int NR = (4 * MAXP + LPA - 1) / LPA;
+    const int EQ = E + 3;                        // staged month sums
+    const int cnt_l = g.sl < 12 ? R.cnt[g.sl] : 0;
+    double xL = 0.0, xg = 0.0, xwp = 0.0;        // this lane's entry of the fetched chunk
+    int fm = -1, fj = 0;                         // which chunk the registers hold
+    auto fetch = [&](int m, int j0, int n) __attribute__((always_inline)) {
+        const int j = j0 + g.sl;
+        if (j < n) {
+            const double* e = reinterpret_cast<const double*>(R.ent + m * NB_CAPM + j);
+            xL = e[0];
+            xg = e[1];
+            xwp = e[2];
+        }
+        fm = m;
+        fj = j0;
+    };
+    double sv[NR];
+    auto fetch_sums = [&](int m) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < NR; k++) {
+            const int r = g.sl + k * LPA;
+            sv[k] = r < 4 * P ? R.sums[(m * MAXP + (r >> 2)) * 4 + (r & 3)] : 0.0;
+        }
+    };
+    fetch_sums(0);
+    {
+        const int n0 = __shfl(cnt_l, g.base, WAVE);
+        fetch(0, 0, n0);
+    }
     double total = 0.0, carry = 0.0;
     for (int m = 0; m < 12; m++) {
+        const int n_m = __shfl(cnt_l, g.base + m, WAVE);
+        const int n_n = __shfl(cnt_l, g.base + (m + 1 < 12 ? m + 1 : 11), WAVE);
+        if (n_m > 0 && !(fm == m && fj == 0)) fetch(m, 0, n_m);
+        wave_lds_sync();
+#pragma unroll
+        for (int k = 0; k < NR; k++) S.at(EQ + k) = sv[k];
+        wave_lds_sync();
         for (int p = 0; p < P; p++) {
-            const double* q = R.sums + (m * MAXP + p) * 4;
-            S.at(p) = q[0] - (q[1] * kws) * s;
-            S.at(half + p) = (q[2] * kws) * s - q[3];
+            const double q0 = col0[(EQ + (4 * p) / LPA) * WAVE + (4 * p) % LPA];
+            const double q1 = col0[(EQ + (4 * p + 1) / LPA) * WAVE + (4 * p + 1) % LPA];
+            const double q2 = col0[(EQ + (4 * p + 2) / LPA) * WAVE + (4 * p + 2) % LPA];
+            const double q3 = col0[(EQ + (4 * p + 3) / LPA) * WAVE + (4 * p + 3) % LPA];
+            S.at(p) = q0 - (q1 * kws) * s;
+            S.at(half + p) = (q2 * kws) * s - q3;
         }
-        const int n_m = R.cnt[m];
-        const NbEnt* ent = R.ent + m * NB_CAPM;
+        if (m + 1 < 12) fetch_sums(m + 1);
         int cur = 0;
         double ci = S.at(0), ce = S.at(half);
-#pragma unroll 1
-        for (int j = 0; j < n_m; j += 4) {
-            // four entries' loads together (96 contiguous bytes of the record)
-            NbEnt ev[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) ev[k] = ent[(j + k < n_m) ? j + k : j];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (j + k >= n_m) break;
-                const int p = ev[k].p;
+        for (int j0 = 0; j0 < n_m; j0 += LPA) {
+            wave_lds_sync();
+            S.at(E) = xL;
+            S.at(E + 1) = xg;
+            S.at(E + 2) = xwp;
+            wave_lds_sync();
+            if (j0 + LPA < n_m) fetch(m, j0 + LPA, n_m);
+            else if (m + 1 < 12 && n_n > 0) fetch(m + 1, 0, n_n);
+            const int kn = (n_m - j0 < LPA) ? n_m - j0 : LPA;
+#pragma unroll 4
+            for (int k = 0; k < kn; k++) {
+                const double eL = col0[E * WAVE + k];
+                const double eg = col0[(E + 1) * WAVE + k];
+                const double ewp = col0[(E + 2) * WAVE + k];
+                const int64_t wpb = __double_as_longlong(ewp);
+                const float ew = __int_as_float((int)(wpb & 0xffffffff));
+                const int p = (int)(wpb >> 32);
                 // the hourly pass's arithmetic: load, generation cf / 1e6 x kW'
                 // (the battery case's system output as is), x the year's factor
-                const double gg = src.sysgen ? ev[k].g : ev[k].g * kws;
-                const double dd = ev[k].L - gg * s;
+                const double gg = sysg ? eg : eg * kws;
+                const double dd = eL - gg * s;
                 if (p != cur) {
                     S.at(cur) = ci;
                     S.at(half + cur) = ce;
@@ -1915,7 +2144,7 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
                     ci += dd;
                 } else {
                     double e = -dd;
-                    if (src.ts) e *= (double)ev[k].w;
+                    if (tsw) e *= (double)ew;
                     ce += e;
                 }
             }
@@ -1929,6 +2158,7 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
         }
         total += nb_month(t, yl_month_charge(t, m, S, 0), cr, carry);
     }
+    wave_lds_sync();
     return total;
 }
 
@@ -2129,7 +2359,10 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_mo2_nogen(t, c.S);
-        c.nb_ok = c.nb && yl_nb_build(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g);
+        PH_T0(tb);
+        c.nb_ok = c.nb && (DGEN_NB_SERIAL ? yl_nb_build_serial(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g) : yl_nb_build<false>(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g));
+        PH_ADD(1, tb, c.g.sl == 0);
+        PH_CNT(7, 1, c.g.sl == 0);
     } else {
         c.status |= DGEN_ST_SCRATCH;
         c.wo1 = NAN;
@@ -2162,7 +2395,10 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
         wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
     } else if constexpr (NET) {
         c.src.gen_scale = kws;
-        wb = c.nb_ok ? yl_bill_nb(t, c.src, c.s_y, c.nb, c.S) : yl_bill_mo2(t, c.src, c.s_y, true, c.S);
+        PH_T0(te);
+        wb = c.nb_ok ? yl_bill_nb(t, c.src, c.s_y, c.nb, c.S, c.g) : yl_bill_mo2(t, c.src, c.s_y, true, c.S);
+        PH_ADD(c.nb_ok ? 2 : 3, te, c.g.sl == 0);
+        PH_CNT(8, 1, c.g.sl == 0);
     } else {
         wb = NAN;
     }
@@ -2303,6 +2539,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         c.tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
         c.thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
     }
+    PH_T0(t_all);
     yl_set_tariff<LPA, DC, NET>(c, t0);
     int nfev = 0;
     double x_last = 0.0;
@@ -2342,6 +2579,8 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         O.switched[i] = c.switched;
         O.status[i] = c.status;
     }
+    PH_ADD(0, t_all, sl == 0);
+    PH_CNT(9, nfev, sl == 0);
 }
 
 // Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
@@ -2354,6 +2593,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     if (i >= i1) return;
     const int st = O.status[i];
     if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH | DGEN_ST_UNIT)) return;
+    PH_T0(t_all);
     const Seg<LPA> g(lane);
     const int y = g.sl + 1;
     const int half = lds_half(T.max_periods);
@@ -2424,8 +2664,13 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             const double s_lo = sN < 1.0 ? sN : 1.0, s_hi = sN > 1.0 ? sN : 1.0;
             src.gen_scale = 1.0;
             char* nbp = nbws + (size_t)slot * NB_BYTES;
-            nb_ok = yl_nb_build(t, src, s_lo, s_hi, nbp, S, g);
-            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S);
+            PH_T0(tb);
+            nb_ok = DGEN_NB_SERIAL ? yl_nb_build_serial(t, src, s_lo, s_hi, nbp, S, g)
+                                   : yl_nb_build<true>(t, src, s_lo, s_hi, nbp, S, g);
+            PH_ADD(5, tb, g.sl == 0);
+            PH_T0(te);
+            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S, g);
+            PH_ADD(6, te, g.sl == 0);
         }
         if (!nb_ok) wb = yl_bill_net(t, src, s_y, true, S);
     }
@@ -2456,6 +2701,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         O.bill_w_batt[row + y] = w;
         O.bill_wo_batt[row + y] = wo;
     }
+    PH_ADD(4, t_all, g.sl == 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -3007,6 +3253,18 @@ static int fold_one(dgen_ctx* c, int slot) {
 
 extern "C" {
 
+#if DGEN_PHASE_PROF
+__attribute__((visibility("default"))) int dgen_phase_read(uint64_t* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(uint64_t) * 16) != hipSuccess) return -1;
+    if (reset) {
+        static const uint64_t z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
 int32_t dgen_abi_version(void) { return DGEN_ABI_VERSION; }
 
 int32_t dgen_last_error(char* buf, size_t n) {
@@ -3156,6 +3414,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     dgen_tables Tk = *T;
     const bool dc = c->cfg.skip_demand_charges == 0 && Tk.n_demand > 0;
     if (dc && 4 * lds_half(Tk.max_periods) < DCP) Tk.max_periods = (DCP + 3) / 4;
+    // yl_bill_nb stages its entries and month sums in slots 2 half .. 2 half + 4
+    if (n_scratch > 0 && lds_half(Tk.max_periods) < 3) Tk.max_periods = 3;
     T = &Tk;
     HIP_TRY(hipSetDevice(c->device));
     if (dc && (size_t)n * DCW_BYTES > c->dc_cap) {   // envelope storage (context-owned)

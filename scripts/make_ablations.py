@@ -28,6 +28,14 @@ def occ(decl, w):
 
 VARIANTS = {
     "base": [],
+    # per-phase shader-cycle counters (bench.py prints them with DGEN_PHASE_PROF=1)
+    "phase": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1")],
+    "phase_serial": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
+                     ("#define DGEN_NB_SERIAL 0", "#define DGEN_NB_SERIAL 1")],
+    "db_cf4": [("#define DGEN_NB_DB_CF 8", "#define DGEN_NB_DB_CF 4")],
+    "db_cf12": [("#define DGEN_NB_DB_CF 8", "#define DGEN_NB_DB_CF 12")],
+    "nb_serial": [("#define DGEN_NB_SERIAL 0", "#define DGEN_NB_SERIAL 1")],
+    "nb_noinl": [("__device__ __forceinline__ bool yl_nb_build(", "__device__ bool yl_nb_build(")],
     "hb_w3": [(HB, occ(HB, 3))],
     "hb_w4": [(HB, occ(HB, 4))],
     "ks_w3": [(KS, occ(KS, 3))],
@@ -115,6 +123,16 @@ VARIANTS = {
     # k_batt_finance without its battery-case demand pass (what the rest costs)
     "kf_no_dem": [("            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);",
                    "            const double v = 0.0 * (double)(size_t)stage;")],
+    # C2 (net billing) split of k_size: evaluations without the split bill / without the build
+    "ks_nb_noeval": [("        wb = c.nb_ok ? yl_bill_nb(t, c.src, c.s_y, c.nb, c.S) : yl_bill_mo2(t, c.src, c.s_y, true, c.S);",
+                      "        wb = c.nb_ok ? 1000.0 - kws * c.s_y : yl_bill_mo2(t, c.src, c.s_y, true, c.S);")],
+    "ks_nb_nobuild": [("        c.nb_ok = c.nb && yl_nb_build(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g);",
+                       "        c.nb_ok = c.nb != nullptr;"),
+                      ("        wb = c.nb_ok ? yl_bill_nb(t, c.src, c.s_y, c.nb, c.S) : yl_bill_mo2(t, c.src, c.s_y, true, c.S);",
+                       "        wb = c.nb_ok ? 1000.0 - kws * c.s_y : yl_bill_mo2(t, c.src, c.s_y, true, c.S);")],
+    # k_batt_finance net-billing: without the split build / bill
+    "kf_nb_none": [("            nb_ok = yl_nb_build(t, src, s_lo, s_hi, nbp, S, g);\n            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S);",
+                    "            nb_ok = true; wb = 1000.0 * s_y + (double)(size_t)nbp * 0.0;")],
 }
 
 
