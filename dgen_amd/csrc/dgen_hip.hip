@@ -300,7 +300,10 @@ __device__ __forceinline__ double np_sign(double v) {
     return (v > 0.0) ? 1.0 : ((v < 0.0) ? -1.0 : 0.0);
 }
 
-// scipy 1.15.3 _minimize_scalar_bounded, op for op (maxfun 500).
+// scipy 1.15.3 _minimize_scalar_bounded, op for op (maxfun 500).  The
+// objective is called from one site (the loop head), so the kernel carries one
+// inlined copy of it: scipy's first evaluation and its loop evaluations run
+// through the same call, the first one only seeding the state.
 template <class Obj>
 __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, double xatol, int* nfev,
                                 double* x_last) {
@@ -311,14 +314,35 @@ __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, d
     double nfc = fulc, xf = fulc;
     double rat = 0.0, e = 0.0;
     double x = xf;
-    double fx = f(x);
-    *x_last = x;
-    int num = 1;
-    double ffulc = fx, fnfc = fx;
-    double xm = 0.5 * (a + b);
-    double tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
-    double tol2 = 2.0 * tol1;
-    while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {
+    double fx = 0.0, ffulc = 0.0, fnfc = 0.0;
+    int num = 0;
+    for (;;) {
+        const double fu = f(x);
+        *x_last = x;
+        num += 1;
+        if (num == 1) {
+            fx = fu;
+            ffulc = fu;
+            fnfc = fu;
+        } else if (fu <= fx) {
+            if (x >= xf) a = xf; else b = xf;
+            fulc = nfc; ffulc = fnfc;
+            nfc = xf; fnfc = fx;
+            xf = x; fx = fu;
+        } else {
+            if (x < xf) a = x; else b = x;
+            if ((fu <= fnfc) || (nfc == xf)) {
+                fulc = nfc; ffulc = fnfc;
+                nfc = x; fnfc = fu;
+            } else if ((fu <= ffulc) || (fulc == xf) || (fulc == nfc)) {
+                fulc = x; ffulc = fu;
+            }
+        }
+        const double xm = 0.5 * (a + b);
+        const double tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+        const double tol2 = 2.0 * tol1;
+        if (num >= 500) break;
+        if (!(fabs(xf - xm) > (tol2 - 0.5 * (b - a)))) break;
         bool golden = true;
         if (fabs(e) > tol1) {
             golden = false;
@@ -348,27 +372,6 @@ __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, d
         double si = np_sign(rat) + ((rat == 0.0) ? 1.0 : 0.0);
         double ar = fabs(rat);
         x = xf + si * (ar > tol1 ? ar : tol1);
-        double fu = f(x);
-        *x_last = x;
-        num += 1;
-        if (fu <= fx) {
-            if (x >= xf) a = xf; else b = xf;
-            fulc = nfc; ffulc = fnfc;
-            nfc = xf; fnfc = fx;
-            xf = x; fx = fu;
-        } else {
-            if (x < xf) a = x; else b = x;
-            if ((fu <= fnfc) || (nfc == xf)) {
-                fulc = nfc; ffulc = fnfc;
-                nfc = x; fnfc = fu;
-            } else if ((fu <= ffulc) || (fulc == xf) || (fulc == nfc)) {
-                fulc = x; ffulc = fu;
-            }
-        }
-        xm = 0.5 * (a + b);
-        tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
-        tol2 = 2.0 * tol1;
-        if (num >= 500) break;
     }
     *nfev = num;
     return xf;
@@ -2045,6 +2048,22 @@ __device__ __forceinline__ bool yl_nb_build(const dgen_tariff& t, const YSrc& sr
 // src.gen_scale, degradation factor s; battery case: src.sysgen with
 // gen_scale 1): yl_bill_mo2's result up to the rounding of the re-associated
 // import / export sums.
+// max of a segment-uniform count in [0, LPA] over the wave's segments
+// (wave-uniform).  A segment whose lanes are inactive here (the wave's other
+// agent on another path) contributes a stale value, so the result is clamped
+// to LPA: extra trips are predicated off by the caller.
+template <int LPA>
+__device__ __forceinline__ int nb_wave_max(int v) {
+    int r;
+    if constexpr (LPA == WAVE) {
+        r = __builtin_amdgcn_readfirstlane(v);
+    } else {
+        const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, LPA);
+        r = a > b ? a : b;
+    }
+    return r < LPA ? r : LPA;
+}
+
 // The M entries reach the lanes through LDS in chunks of LPA: lane k loads
 // entry j0 + k of the next chunk (one coalesced 24-B record per lane) while
 // the segment bills the current chunk out of the lanes' LDS columns (slots
@@ -2066,6 +2085,8 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
     constexpr int NR = (4 * MAXP + LPA - 1) / LPA;
     const int EQ = E + 3;                        // staged month sums
     const int cnt_l = g.sl < 12 ? R.cnt[g.sl] : 0;
+    const unsigned long long segm = (LPA == WAVE) ? ~0ull : (((1ull << LPA) - 1ull) << g.base);
+    const unsigned long long below = (1ull << g.lane) - 1ull;
     double xL = 0.0, xg = 0.0, xwp = 0.0;        // this lane's entry of the fetched chunk
     int fm = -1, fj = 0;                         // which chunk the registers hold
     auto fetch = [&](int m, int j0, int n) __attribute__((always_inline)) {
@@ -2112,43 +2133,68 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
         if (m + 1 < 12) fetch_sums(m + 1);
         int cur = 0;
         double ci = S.at(0), ce = S.at(half);
+        PH_T0(tl);
+        PH_CNT(10, n_m, g.sl == 0);
         for (int j0 = 0; j0 < n_m; j0 += LPA) {
+            const int kn = (n_m - j0 < LPA) ? n_m - j0 : LPA;
+            // the chunk is staged grouped by period (hour order within a
+            // period), so the running accumulator switches at most P times a
+            // chunk while each period still adds its entries in hour order;
+            // the slots past the chunk's kn entries hold zero entries of its
+            // last period (they add exact zeros), so both segments of the wave
+            // run the same trip count
+            const int myp = g.sl < kn ? (int)(__double_as_longlong(xwp) >> 32) : MAXP;
+            int dst = g.sl, lastp = 0;
+            {
+                int base = 0;
+                for (int q = 0; q < P; q++) {
+                    const unsigned long long bm = __ballot(myp == q) & segm;
+                    if (myp == q) dst = base + __popcll(bm & below);
+                    base += __popcll(bm);
+                    if (bm) lastp = q;
+                }
+            }
+            const double pad = __longlong_as_double((long long)lastp << 32);
             wave_lds_sync();
-            S.at(E) = xL;
-            S.at(E + 1) = xg;
-            S.at(E + 2) = xwp;
+            col0[E * WAVE + dst] = g.sl < kn ? xL : 0.0;
+            col0[(E + 1) * WAVE + dst] = g.sl < kn ? xg : 0.0;
+            col0[(E + 2) * WAVE + dst] = g.sl < kn ? xwp : pad;
             wave_lds_sync();
             if (j0 + LPA < n_m) fetch(m, j0 + LPA, n_m);
             else if (m + 1 < 12 && n_n > 0) fetch(m + 1, 0, n_n);
-            const int kn = (n_m - j0 < LPA) ? n_m - j0 : LPA;
+            const int kw = nb_wave_max<LPA>(kn);
+            // per entry, the hourly pass's arithmetic: load, generation
+            // cf / 1e6 x kW' (the battery case's system output as is), x the
+            // year's factor; an import adds dd, an export adds -dd (x the TS
+            // sell weight), the other side an exact 0
+            auto run = [&](auto tsw_c) __attribute__((always_inline)) {
+                constexpr bool TSW = decltype(tsw_c)::value;
 #pragma unroll 4
-            for (int k = 0; k < kn; k++) {
-                const double eL = col0[E * WAVE + k];
-                const double eg = col0[(E + 1) * WAVE + k];
-                const double ewp = col0[(E + 2) * WAVE + k];
-                const int64_t wpb = __double_as_longlong(ewp);
-                const float ew = __int_as_float((int)(wpb & 0xffffffff));
-                const int p = (int)(wpb >> 32);
-                // the hourly pass's arithmetic: load, generation cf / 1e6 x kW'
-                // (the battery case's system output as is), x the year's factor
-                const double gg = sysg ? eg : eg * kws;
-                const double dd = eL - gg * s;
-                if (p != cur) {
-                    S.at(cur) = ci;
-                    S.at(half + cur) = ce;
-                    cur = p;
-                    ci = S.at(p);
-                    ce = S.at(half + p);
-                }
-                if (dd > 0.0) {
-                    ci += dd;
-                } else {
-                    double e = -dd;
-                    if (tsw) e *= (double)ew;
+                for (int k = 0; k < kw; k++) {
+                    const double eL = col0[E * WAVE + k];
+                    const double eg = col0[(E + 1) * WAVE + k];
+                    const double ewp = col0[(E + 2) * WAVE + k];
+                    const int64_t wpb = __double_as_longlong(ewp);
+                    const int p = (int)(wpb >> 32);
+                    if (p != cur) {
+                        S.at(cur) = ci;
+                        S.at(half + cur) = ce;
+                        cur = p;
+                        ci = S.at(p);
+                        ce = S.at(half + p);
+                    }
+                    const double gg = sysg ? eg : eg * kws;
+                    const double dd = eL - gg * s;
+                    ci += fmax(dd, 0.0);
+                    double e = fmax(-dd, 0.0);
+                    if constexpr (TSW) e *= (double)__int_as_float((int)(wpb & 0xffffffff));
                     ce += e;
                 }
-            }
+            };
+            if (tsw) run(std::true_type{});
+            else run(std::false_type{});
         }
+        PH_ADD(11, tl, g.sl == 0);
         S.at(cur) = ci;
         S.at(half + cur) = ce;
         double cr = 0.0;

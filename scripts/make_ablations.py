@@ -30,17 +30,14 @@ VARIANTS = {
     "base": [],
     # per-phase shader-cycle counters (bench.py prints them with DGEN_PHASE_PROF=1)
     "phase": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1")],
-    "phase_serial": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
-                     ("#define DGEN_NB_SERIAL 0", "#define DGEN_NB_SERIAL 1")],
     "db_cf4": [("#define DGEN_NB_DB_CF 8", "#define DGEN_NB_DB_CF 4")],
     "db_cf12": [("#define DGEN_NB_DB_CF 8", "#define DGEN_NB_DB_CF 12")],
-    "nb_serial": [("#define DGEN_NB_SERIAL 0", "#define DGEN_NB_SERIAL 1")],
-    "nb_noinl": [("__device__ __forceinline__ bool yl_nb_build(", "__device__ bool yl_nb_build(")],
     "hb_w3": [(HB, occ(HB, 3))],
     "hb_w4": [(HB, occ(HB, 4))],
     "ks_w3": [(KS, occ(KS, 3))],
     "ks_w4": [(KS, occ(KS, 4))],
     "kf_w6": [(KF, occ(KF, 6))],
+    "kf_w3": [(KF, occ(KF, 3))],
     "no_target": [("                target = day_target_sorted(dv, power, avail);",
                    "                target = 0.0; asm volatile(\"\" :: \"v\"(dv[0]), \"v\"(dv[23]), \"v\"(avail));")],
     "no_bisect": [("    if (s[0] <= power) {\n        double S = 0.0, SK = s[0];", "    if (true) {\n        double S = 0.0, SK = s[0];")],
@@ -63,7 +60,7 @@ VARIANTS = {
     "plain_stores": [("    asm volatile(\"global_store_dword %0, %1, %2 nt\" :: \"v\"(off), \"v\"(v), \"s\"(row) : \"memory\");",
                       "    *reinterpret_cast<float*>(row + off) = v;")],
     # k_size: Brent stops after its first evaluation (per-evaluation cost)
-    "ks_one_eval": [("    while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {", "    while (false) {")],
+    "ks_one_eval": [("        if (!(fabs(xf - xm) > (tol2 - 0.5 * (b - a)))) break;", "        break;")],
     # k_size: no NEM bill (per-lane year bill replaced by a constant)
     "ks_no_bill": [("    return (t.P <= PREG) ? yl_bill_mo0_reg(t, S, gscale, yearend) : yl_bill_mo0(t, S, gscale, yearend);",
                     "    return 100.0 + gscale;")],
