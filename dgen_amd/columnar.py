@@ -9,7 +9,7 @@ switch table filter (elec.py:840-847) and the finance-column reads.
 from __future__ import annotations
 
 import hashlib
-from typing import Any, Dict, Hashable, List, Optional, Sequence, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import pandas as pd
@@ -51,8 +51,12 @@ class SwitchIndex:
 
     def candidates(self, tech: str, eia_id, sector_abbr, is_ca: bool) -> Tuple[int, int]:
         res_com = str(sector_abbr).upper()[0]
-        ckey = (tech, eia_id if isinstance(eia_id, Hashable) else repr(eia_id), res_com, is_ca)
-        hit = self._cache.get(ckey)
+        ckey = (tech, eia_id, res_com, is_ca)
+        try:
+            hit = self._cache.get(ckey)
+        except TypeError:          # unhashable eia_id
+            ckey = (tech, repr(eia_id), res_com, is_ca)
+            hit = self._cache.get(ckey)
         if hit is not None:
             return hit
         rows = self._lookup(tech, eia_id, res_com)
@@ -102,38 +106,61 @@ class WholesaleIndex:
             self.rows.append(a)
         return k
 
-    def add_cached(self, arr, mult: float, cache: Dict[int, Tuple]) -> int:
-        """add() with the conversion, finiteness scan and content hash done
-        once per distinct array object (cache: id -> (key, array, all finite,
-        max |x|)); a row enters the table at its first valid use, as in add().
-        The f32-finiteness of arr * mult (series_8760) follows from the largest
-        |x|: |x * mult| is monotone in |x|."""
-        if arr is None:
-            return -1
-        ent = cache.get(id(arr))
-        if ent is None:
-            try:
-                a = np.asarray(arr, dtype=np.float64).ravel()
-            except Exception:
-                a = None
-            if a is None or a.size != 8760:
-                ent = (None, None, False, 0.0)
-            else:
-                ent = (hashlib.blake2b(a.tobytes(), digest_size=16).digest(), a,
-                       bool(np.isfinite(a).all()), float(np.abs(a).max()))
-            cache[id(arr)] = ent
-        key, a, fin, mx = ent
-        if key is None or not fin or not np.isfinite(mult):
-            return -1
-        with np.errstate(over="ignore"):
-            if not np.isfinite(np.float32(mx * abs(mult))):
-                return -1
-        k = self._index.get(key)
-        if k is None:
-            k = len(self.rows)
-            self._index[key] = k
-            self.rows.append(a)
-        return k
+    def add_frame(self, arrs: Sequence, mult: np.ndarray, skip: np.ndarray) -> np.ndarray:
+        """add() over a whole frame column at once: conversion, finiteness scan
+        and content hash once per distinct array object (rows share them), the
+        per-row validity (arr * mult finite in float32 -- series_8760 -- which
+        follows from the largest |x|, |x * mult| being monotone in |x|)
+        vectorised, and table rows entered in the order of their first valid
+        use, exactly as add() row by row.  skip: rows that take -1 (CA)."""
+        n = len(arrs)
+        obj: Dict[int, int] = {}          # id(array object) -> distinct-object index
+        ckey: List[int] = []              # distinct object -> content index (-1: invalid)
+        cmax: List[float] = []
+        contents: Dict[bytes, int] = {}
+        carr: List[np.ndarray] = []
+        oix = np.empty(n, np.int64)
+        for i, arr in enumerate(arrs):
+            k = obj.get(id(arr))
+            if k is None:
+                k = obj[id(arr)] = len(ckey)
+                c, mx = -1, 0.0
+                if arr is not None:
+                    try:
+                        v = np.asarray(arr, dtype=np.float64).ravel()
+                    except Exception:
+                        v = None
+                    if v is not None and v.size == 8760 and bool(np.isfinite(v).all()):
+                        h = hashlib.blake2b(v.tobytes(), digest_size=16).digest()
+                        c = contents.get(h)
+                        if c is None:
+                            c = contents[h] = len(carr)
+                            carr.append(v)
+                        mx = float(np.abs(v).max())
+                ckey.append(c)
+                cmax.append(mx)
+            oix[i] = k
+        ck = np.asarray(ckey, np.int64)[oix] if n else np.zeros(0, np.int64)
+        mxr = np.asarray(cmax, np.float64)[oix] if n else np.zeros(0)
+        with np.errstate(over="ignore", invalid="ignore"):
+            ok = (ck >= 0) & ~np.asarray(skip, bool) & np.isfinite(mult) & \
+                np.isfinite((mxr * np.abs(mult)).astype(np.float32))
+        out = np.full(n, -1, np.int64)
+        if ok.any():
+            rows = np.nonzero(ok)[0]
+            u, first = np.unique(ck[rows], return_index=True)
+            order = np.argsort(first, kind="stable")          # first valid use
+            slot = np.empty(int(u.max()) + 1, np.int64)
+            key_of = {c: h for h, c in contents.items()}
+            for c in u[order].tolist():
+                h = key_of[c]
+                k = self._index.get(h)
+                if k is None:
+                    k = self._index[h] = len(self.rows)
+                    self.rows.append(carr[c])
+                slot[c] = k
+            out[rows] = slot[ck[rows]]
+        return out
 
     def array(self) -> Optional[np.ndarray]:
         return np.stack(self.rows) if self.rows else None
@@ -250,19 +277,40 @@ def columnize_frame(df, src, rate_switch_table=None, skip_demand_charges=None) -
     eia = df["eia_id"].tolist()
     mult = _num(df["elec_price_multiplier"])
     whl = df["wholesale_prices"].tolist() if "wholesale_prices" in df else [None] * n
-    wcache: Dict[int, Tuple] = {}
     W = b.wholesale
+    # one resolution per distinct (tariff object, CA?, eia_id, sector): rows
+    # repeat these combinations (pandas merges share the objects), and
+    # resolving a combination at its first row keeps the tariff and switch
+    # tables in the row-by-row order of first use
+    memo: Dict[Tuple, Tuple[int, int, int, int, int]] = {}
+    res: List[Tuple[int, int, int, int, int]] = []
+    ca_l = is_ca.tolist()
     for i in range(n):
-        raw = tdict[i]
-        key = tkey.get(id(raw))
-        if key is None:
-            key = tkey[id(raw)] = tariff_key(raw)
-        cols["tariff0"][i] = b.tariffs.add(raw, bool(is_ca[i]), key=key)
-        cols["sw_solar_off"][i], cols["sw_solar_cnt"][i] = b.switches.candidates("solar", eia[i], sector[i],
-                                                                                  bool(is_ca[i]))
-        cols["sw_storage_off"][i], cols["sw_storage_cnt"][i] = b.switches.candidates("storage", eia[i],
-                                                                                      sector[i], bool(is_ca[i]))
-        cols["wholesale_row"][i] = -1 if is_ca[i] else W.add_cached(whl[i], float(mult[i]), wcache)
+        raw, ca, e = tdict[i], ca_l[i], eia[i]
+        try:
+            ck = (id(raw), ca, e, sector[i])
+            hit = memo.get(ck)
+        except TypeError:          # unhashable eia_id: resolve the row on its own
+            ck, hit = None, None
+        if hit is None:
+            key = tkey.get(id(raw))
+            if key is None:
+                key = tkey[id(raw)] = tariff_key(raw)
+            t0 = b.tariffs.add(raw, ca, key=key)
+            so, sc = b.switches.candidates("solar", e, sector[i], ca)
+            to, tc = b.switches.candidates("storage", e, sector[i], ca)
+            hit = (t0, so, sc, to, tc)
+            if ck is not None:
+                memo[ck] = hit
+        res.append(hit)
+    res = np.array(res, np.int64).reshape(n, 5)
+    cols["tariff0"] = res[:, 0].astype(cols["tariff0"].dtype)
+    cols["sw_solar_off"] = res[:, 1].astype(cols["sw_solar_off"].dtype)
+    cols["sw_solar_cnt"] = res[:, 2].astype(cols["sw_solar_cnt"].dtype)
+    cols["sw_storage_off"] = res[:, 3].astype(cols["sw_storage_off"].dtype)
+    cols["sw_storage_cnt"] = res[:, 4].astype(cols["sw_storage_cnt"].dtype)
+    # wholesale rows do not interleave with the tables above: resolved whole
+    cols["wholesale_row"] = W.add_frame(whl, mult, is_ca).astype(cols["wholesale_row"].dtype)
     cols["flags"] = (is_res.astype(np.uint8) | (is_ca.astype(np.uint8) << 1)).astype(np.uint8)
     cols["econ_life"] = df["economic_lifetime_yrs"].astype(np.int64).to_numpy().astype(np.int32)
     cols["loan_term"] = df["loan_term_yrs"].astype(np.int64).to_numpy().astype(np.int32)

@@ -402,6 +402,25 @@ __host__ __device__ inline char* ws_nb(void* base, int64_t n, int64_t n_scratch)
                                                             (size_t)NH * (size_t)n_scratch);
 }
 
+// Phase timers (DGEN_PHASE_PROF=1 ablation builds only): per-segment shader
+// cycles spent in a phase, summed over segments, read by dgen_phase_read.
+// Slots 0-11: year-lane kernels; 12-15: k_hourly_batt day-target counters.
+#ifndef DGEN_PHASE_PROF
+#define DGEN_PHASE_PROF 0
+#endif
+#if DGEN_PHASE_PROF
+__device__ unsigned long long g_phase[16];
+#define PH_T0(v) const unsigned long long v = __builtin_readcyclecounter()
+#define PH_ADD(k, v, lead) \
+    do { if (lead) atomicAdd(&g_phase[k], __builtin_readcyclecounter() - (v)); } while (0)
+#define PH_CNT(k, n, lead) \
+    do { if (lead) atomicAdd(&g_phase[k], (unsigned long long)(n)); } while (0)
+#else
+#define PH_T0(v) do {} while (0)
+#define PH_ADD(k, v, lead) do {} while (0)
+#define PH_CNT(k, n, lead) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // k_hourly_batt: one sequential scan over the year per agent
 // ---------------------------------------------------------------------------
@@ -455,7 +474,7 @@ __device__ __forceinline__ void sort24_desc(double (&v)[24]) {
 }
 
 __device__ __forceinline__ double day_target_sorted(const double (&s)[24], double power,
-                                                    double avail) {
+                                                    double avail, int* its = nullptr) {
     if (s[0] <= power) {
         // no hour above the power limit: need0 = sum_k min(s_k, P) is the
         // scan's total S_24 (the same additions in the same order), so one
@@ -486,6 +505,7 @@ __device__ __forceinline__ double day_target_sorted(const double (&s)[24], doubl
     int a_hi = 0, b_hi = 0;
     for (int it = 0; it < 48; it++) {
         if (a_lo == a_hi && b_lo == b_hi) break;
+        if (its) ++*its;                 // phase-counter builds only
         const double mid = 0.5 * (lo + hi);
         double f = 0.0;
         int am = 0, bm = 0;
@@ -802,7 +822,22 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     dv[hh] = fmax((double)r.s[hh] * ls - (double)r.c[hh] * cs6, 0.0);
                 sort24_desc(dv);
                 const double avail = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
+#if DGEN_PHASE_PROF
+                int its = 0;
+                target = day_target_sorted(dv, power, avail, &its);
+                {   // 12: battery lane-days, 13: saturated lane-days, 14: wave-days with
+                    // a saturated lane, 15: sum over wave-days of the wave's bisection trips
+                    const unsigned long long act = __ballot(1), sat = __ballot(dv[0] > power);
+                    for (int o = 32; o > 0; o >>= 1) its = max(its, __shfl_xor(its, o));
+                    const bool lead = (int)(threadIdx.x & 63u) == __ffsll((long long)act) - 1;
+                    PH_CNT(12, __popcll(act), lead);
+                    PH_CNT(13, __popcll(sat), lead);
+                    PH_CNT(14, sat != 0ull, lead);
+                    PH_CNT(15, its, lead);
+                }
+#else
                 target = day_target_sorted(dv, power, avail);
+#endif
                 day_reread(dlane, r);
             }
             if (d < d_last) day_dma(d + 1);                     // after the last read of the buffer
@@ -924,23 +959,6 @@ struct Seg {
     __device__ __forceinline__ double bcast(double v, int k) const { return __shfl(v, base + k, WAVE); }
 };
 
-// Phase timers (DGEN_PHASE_PROF=1 ablation builds only): per-segment shader
-// cycles spent in a phase, summed over segments, read by dgen_phase_read.
-#ifndef DGEN_PHASE_PROF
-#define DGEN_PHASE_PROF 0
-#endif
-#if DGEN_PHASE_PROF
-__device__ unsigned long long g_phase[16];
-#define PH_T0(v) const unsigned long long v = __builtin_readcyclecounter()
-#define PH_ADD(k, v, lead) \
-    do { if (lead) atomicAdd(&g_phase[k], __builtin_readcyclecounter() - (v)); } while (0)
-#define PH_CNT(k, n, lead) \
-    do { if (lead) atomicAdd(&g_phase[k], (unsigned long long)(n)); } while (0)
-#else
-#define PH_T0(v) do {} while (0)
-#define PH_ADD(k, v, lead) do {} while (0)
-#define PH_CNT(k, n, lead) do {} while (0)
-#endif
 
 // LDS hand-off between the lanes of one wave (every year-lane block is one
 // wave): orders the LDS stores before the loads without s_barrier, so it is

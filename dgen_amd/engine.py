@@ -369,6 +369,78 @@ def tile_hourly(p):
     return p.reshape(nh // 4, 4, n).permute(0, 2, 1).contiguous()
 
 
+_STAGE: Dict[int, object] = {}      # pinned host staging buffers (reused across calls)
+_POOL: Dict[str, object] = {}
+
+
+def _host_empty(shape, dtype) -> np.ndarray:
+    """Uninitialised host array on an anonymous mapping advised for huge pages:
+    a multi-GB hourly plane is then first-touched 2 MB at a time instead of
+    4 KB at a time (the page faults, not the copy, bound a pageable download).
+    The mapping lives as long as the array (numpy keeps the buffer)."""
+    import mmap
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    if nbytes < (64 << 20):
+        return np.empty(shape, dtype)
+    m = mmap.mmap(-1, nbytes, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    try:
+        m.madvise(14)                   # MADV_HUGEPAGE (advice only)
+    except (AttributeError, OSError, ValueError):
+        pass
+    return np.frombuffer(m, dtype=dtype).reshape(shape)
+
+
+def _staging(k: int, nbytes: int):
+    torch = _torch()
+    t = _STAGE.get(k)
+    if t is None or t.numel() < nbytes:
+        t = _STAGE[k] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    return t
+
+
+def hourly_to_host(t, inv=None, chunk: int = 4096, threads: int = 8) -> np.ndarray:
+    """One hour-quad-tiled plane [NH/4][n][4] -> host [n][NH] (caller order when
+    `inv` gathers it): per chunk of agents, a device gather into agent-major
+    order, an async copy into one of two pinned staging buffers, and host
+    threads copying the previous chunk out into the destination while the
+    next chunk crosses PCIe."""
+    torch = _torch()
+    from concurrent.futures import ThreadPoolExecutor
+    q, n, four = t.shape
+    ncol = q * four
+    rowb = ncol * t.element_size()
+    dst = _host_empty((n, ncol), np.float64 if t.dtype == torch.float64 else np.float32)
+    if n == 0:
+        return dst
+    chunk = max(1, min(chunk, n))
+    pool = _POOL.get("copy")
+    if pool is None:
+        pool = _POOL["copy"] = ThreadPoolExecutor(threads, thread_name_prefix="dgen-d2h")
+    tp = t.permute(1, 0, 2)
+    pend = [[], []]
+    for k, c0 in enumerate(range(0, n, chunk)):
+        c1 = min(n, c0 + chunk)
+        m, b = c1 - c0, k & 1
+        for f in pend[b]:               # the buffer's previous chunk is out
+            f.result()
+        g = (tp.index_select(0, inv[c0:c1]) if inv is not None else tp[c0:c1]).reshape(m, ncol)
+        hv = _staging(b, chunk * rowb)[: m * rowb].view(t.dtype).view(m, ncol)
+        hv.copy_(g, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        hn = hv.numpy()
+
+        def part(lo, hi, ev=ev, hn=hn, c0=c0):
+            ev.synchronize()
+            np.copyto(dst[c0 + lo:c0 + hi], hn[lo:hi])
+        step = -(-m // threads)
+        pend[b] = [pool.submit(part, lo, min(m, lo + step)) for lo in range(0, m, step)]
+    for p in pend:
+        for f in p:
+            f.result()
+    return dst
+
+
 def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
     """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly),
     in caller order when `perm` (AgentBatch.perm) is given.  The reorder to
@@ -392,6 +464,8 @@ def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None) -
         t = out.get(name)
         if t is None:
             res[name] = None
+        elif t.shape[1] >= 16384:         # large planes: pinned, chunked, threaded
+            res[name] = hourly_to_host(t, inv)
         elif inv is None:
             res[name] = hourly_agent_major(t).cpu().numpy()
         else:

@@ -284,13 +284,22 @@ _DROP = ("adopter_load_hourly", "adopter_pv_hourly", "adopter_batt_to_load_hourl
          "generation_hourly", "batt_dispatch_profile", "net_hourly")
 
 
-def _yearly_lists(a: np.ndarray, n1: np.ndarray):
+def _yearly_lists(a: np.ndarray, n1: np.ndarray, fmt: str = "list"):
     """Row i's first n1[i] values as a Python list, one tolist() per distinct
-    analysis length (the frame usually has one or two)."""
+    analysis length (the frame usually has one or two); fmt "array": each
+    row as a float64 ndarray view of one [rows, n] block instead (no per-value
+    Python float)."""
+    uniq = np.unique(n1)
+    if fmt == "array" and uniq.size == 1:
+        return list(a[:, :int(uniq[0])])
     out = np.empty(a.shape[0], dtype=object)
-    for n in np.unique(n1):
+    for n in uniq:
         ix = np.nonzero(n1 == n)[0]
-        out[ix] = a[ix, :n].tolist() if ix.size > 1 else [a[ix[0], :n].tolist()]
+        if fmt == "array":
+            for j, r in zip(ix.tolist(), a[ix, :n]):
+                out[j] = r
+        else:
+            out[ix] = a[ix, :n].tolist() if ix.size > 1 else [a[ix[0], :n].tolist()]
     return list(out)
 
 
@@ -301,8 +310,10 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     at once (columnar.columnize_frame), sized in one device call, and the
     output columns are assigned whole.  Same values and columns as mapping
     calc_system_size_and_performance over the rows (ff:449-565 write order);
-    hourly: "list" (the reference's fp64 lists), "array" (each cell a row
-    view of one [n, 8760] float64 array, no per-agent copy) or "none".  The
+    hourly: "list" (the reference's fp64 lists), "array" (each hourly and
+    yearly cell a float64 row view of one [n, 8760] / [n, years] array, no
+    per-agent copy and no per-value Python float) or "none" (no hourly
+    columns, yearly lists).  The
     device computes the hourly planes in fp64 for this path.
     timing: filled with the host / device phases (seconds)."""
     import time
@@ -323,10 +334,11 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     if "agent_id" not in out.columns:
         out.insert(len(out.columns), "agent_id", list(df.index))
     n1 = df["economic_lifetime_yrs"].astype(np.int64).to_numpy() + 1
+    yfmt = "array" if hourly == "array" else "list"
     out["naep"] = o["naep"]
-    out["cf_energy_value_pv_only"] = _yearly_lists(o["cfev_pv"], n1)
-    out["utility_bill_w_sys_pv_only"] = _yearly_lists(o["bill_w_pv"], n1)
-    out["utility_bill_wo_sys_pv_only"] = _yearly_lists(o["bill_wo_pv"], n1)
+    out["cf_energy_value_pv_only"] = _yearly_lists(o["cfev_pv"], n1, yfmt)
+    out["utility_bill_w_sys_pv_only"] = _yearly_lists(o["bill_w_pv"], n1, yfmt)
+    out["utility_bill_wo_sys_pv_only"] = _yearly_lists(o["bill_wo_pv"], n1, yfmt)
     sw = np.nonzero(o["switched"] != 0)[0]
     if sw.size:
         # elec.py:852-855: the sticky switch rewrites the agent in place
@@ -346,9 +358,9 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
         if tid is not None:
             out["tariff_id"] = pd.Series(tid, index=out.index).infer_objects()
         out["tariff_dict"] = pd.Series(tdi, index=out.index)
-    out["cf_energy_value_pv_batt"] = _yearly_lists(o["cfev_batt"], n1)
-    out["utility_bill_w_sys_pv_batt"] = _yearly_lists(o["bill_w_batt"], n1)
-    out["utility_bill_wo_sys_pv_batt"] = _yearly_lists(o["bill_wo_batt"], n1)
+    out["cf_energy_value_pv_batt"] = _yearly_lists(o["cfev_batt"], n1, yfmt)
+    out["utility_bill_w_sys_pv_batt"] = _yearly_lists(o["bill_w_batt"], n1, yfmt)
+    out["utility_bill_wo_sys_pv_batt"] = _yearly_lists(o["bill_wo_batt"], n1, yfmt)
     if hourly != "none":
         conv = ((lambda a: a.tolist()) if hourly == "list"
                 else (lambda a: list(a)))
@@ -362,7 +374,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     out["price_per_kwh"] = o["price_per_kwh"]
     out["npv"] = o["npv"]
     out["payback_period"] = o["payback_period"]
-    out["cash_flow"] = _yearly_lists(o["cash_flow"], n1)
+    out["cash_flow"] = _yearly_lists(o["cash_flow"], n1, yfmt)
     out["batt_kw"] = o["batt_kw"]
     out["batt_kwh"] = o["batt_kwh"]
     t3 = time.perf_counter()

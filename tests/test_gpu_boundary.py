@@ -95,3 +95,20 @@ def test_kwh_per_kw_units_leave_only_that_agent_unsized():
     got = out.drop(index=df.index[2])
     for k in ("system_kw", "npv", "payback_period", "batt_kwh", "npv_pv_batt" if "npv_pv_batt" in ref else "npv"):
         assert np.array_equal(got[k].to_numpy(float), ref[k].to_numpy(float), equal_nan=True), k
+
+
+def test_size_chunk_array_mode_equals_list_mode():
+    """hourly="array" (ndarray row views for every list-valued column) carries
+    exactly the values of the reference's list form."""
+    rows, store, table = helpers.golden_rows()
+    df = pd.DataFrame(rows)
+    ff._worker_conn = store
+    lst, agg_l = ff.size_chunk(df, None, table, "simple", hourly="list")
+    arr, agg_a = ff.size_chunk(df, None, table, "simple", hourly="array")
+    assert list(arr.columns) == list(lst.columns)
+    assert agg_a["net_sum_kw"] == agg_l["net_sum_kw"]
+    for k in ARRAYS + ["baseline_net_hourly", "adopter_net_hourly_pvonly", "adopter_net_hourly_with_batt",
+                       "adopter_net_hourly"]:
+        for a, l in zip(arr[k], lst[k]):
+            assert isinstance(a, np.ndarray) and a.dtype == np.float64, k
+            assert np.array_equal(a, np.asarray(l, np.float64)), k

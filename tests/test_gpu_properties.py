@@ -70,12 +70,24 @@ def test_random_sample_vs_oracle(full):
     idx = np.sort(rng.choice(N, 150, replace=False))
     opop = helpers.oracle_population({k: v[idx] for k, v in pop.cols.items()}, pop.tariffs,
                                      pop.switches, pop.shapes, pop.cfs, pop.wholesale)
-    ref = opop.run(orc.make_cfg())
+    ref = opop.run(orc.make_cfg(), hourly=True)
     o = {k: out[k].cpu().numpy() for k in ("system_kw", "npv", "nfev", "payback_period",
                                            "batt_kwh", "annual_kwh")}
-    for j, r in zip(idx, ref):
+    # the sampled agents' hourly planes out of the [2190][n][4] hour-quad tiles
+    # (written by the DMA-pipelined k_hourly_batt at full scale)
+    ti = torch.as_tensor(idx, device=out["baseline"].device)
+    hp = {k: out[k].index_select(1, ti).permute(1, 0, 2).reshape(len(idx), -1).double().cpu().numpy()
+          for k in ("baseline", "net_pvonly", "net_with_batt")}
+    for n_j, (j, r) in enumerate(zip(idx, ref)):
         assert o["nfev"][j] == r["nfev"]
         assert abs(o["system_kw"][j] - r["system_kw"]) <= 1e-9 * r["system_kw"]
         assert np.isclose(o["npv"][j], r["npv"], rtol=1e-6, atol=1e-6)
         assert np.isclose(o["annual_kwh"][j], r["annual_kwh"], rtol=1e-9)
         assert o["payback_period"][j] == r["payback_period"]
+        assert np.isclose(o["batt_kwh"][j], r["batt_kwh"], rtol=1e-9)
+        for k_o, k_r in (("baseline", "baseline_net_hourly"), ("net_pvonly", "adopter_net_hourly_pvonly"),
+                         ("net_with_batt", "adopter_net_hourly_with_batt")):
+            ref_h = np.asarray(r[k_r], dtype=np.float64)
+            # fp32 planes: the float rounding of the kernel's doubles
+            assert np.allclose(hp[k_o][n_j], ref_h, rtol=2e-6,
+                               atol=2e-6 * max(1.0, np.abs(ref_h).max())), (j, k_o)
