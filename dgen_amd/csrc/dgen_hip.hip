@@ -404,9 +404,13 @@ __host__ __device__ inline char* ws_nb(void* base, int64_t n, int64_t n_scratch)
 
 // Phase timers (DGEN_PHASE_PROF=1 ablation builds only): per-segment shader
 // cycles spent in a phase, summed over segments, read by dgen_phase_read.
-// Slots 0-11: year-lane kernels; 12-15: k_hourly_batt day-target counters.
+// Slots 0-15: year-lane kernels; with DGEN_DAY_COUNTERS, 12-15 count
+// k_hourly_batt day targets instead.
 #ifndef DGEN_PHASE_PROF
 #define DGEN_PHASE_PROF 0
+#endif
+#ifndef DGEN_DAY_COUNTERS          // k_hourly_batt day-target counters (slots 12-15)
+#define DGEN_DAY_COUNTERS 0
 #endif
 #if DGEN_PHASE_PROF
 __device__ unsigned long long g_phase[16];
@@ -585,12 +589,16 @@ __device__ __forceinline__ HourStep batt_hour(double nn, double pv, double targe
     const double avail = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
     const double cc = fmin(fmin(-nn, power), room);
     const double dd = fmin(fmin(fmax(nn - target, 0.0), power), avail);
-    // soc + cc*k  ==  soc + (-(dd*k')) exactly for the discharge branch
-    const double dsoc = chg ? cc * in_per_bank : -(dd * out_per_bank);
+    // f: the battery's flow to the load (-cc charging, dd discharging).
+    // dsoc = -(f x k) is cc x k_in or -(dd x k_out) bit for bit (negation is
+    // exact); g2l = max(nn - f, 0) is 0 charging (cc <= -nn) and nn - dd >= 0
+    // discharging (dd <= nn) -- one select and one product fewer per hour
+    const double f = chg ? -cc : dd;
+    const double dsoc = -(f * (chg ? in_per_bank : out_per_bank));
     soc = soc + dsoc;
     HourStep r;
-    r.sys = pv + (chg ? -cc : dd);
-    r.g2l = chg ? 0.0 : nn - dd;
+    r.sys = pv + f;
+    r.g2l = fmax(nn - f, 0.0);
     return r;
 }
 
@@ -822,18 +830,23 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     dv[hh] = fmax((double)r.s[hh] * ls - (double)r.c[hh] * cs6, 0.0);
                 sort24_desc(dv);
                 const double avail = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
-#if DGEN_PHASE_PROF
+#if DGEN_PHASE_PROF && DGEN_DAY_COUNTERS
                 int its = 0;
                 target = day_target_sorted(dv, power, avail, &its);
-                {   // 12: battery lane-days, 13: saturated lane-days, 14: wave-days with
-                    // a saturated lane, 15: sum over wave-days of the wave's bisection trips
-                    const unsigned long long act = __ballot(1), sat = __ballot(dv[0] > power);
-                    for (int o = 32; o > 0; o >>= 1) its = max(its, __shfl_xor(its, o));
+                {   // 12: battery lane-days, 13: lane-days whose whole need fits
+                    // (target 0), 14: wave-days where it fits for every lane,
+                    // 15: saturated lane-days (an hour above the power limit)
+                    double need = 0.0;
+                    for (int k = 0; k < 24; k++) need += fmin(dv[k], power);
+                    const bool fits = need <= avail;
+                    const unsigned long long act = __ballot(1), fit = __ballot(fits),
+                                             sat = __ballot(dv[0] > power);
                     const bool lead = (int)(threadIdx.x & 63u) == __ffsll((long long)act) - 1;
                     PH_CNT(12, __popcll(act), lead);
-                    PH_CNT(13, __popcll(sat), lead);
-                    PH_CNT(14, sat != 0ull, lead);
-                    PH_CNT(15, its, lead);
+                    PH_CNT(13, __popcll(fit), lead);
+                    PH_CNT(14, fit == act, lead);
+                    PH_CNT(15, __popcll(sat), lead);
+                    (void)its;
                 }
 #else
                 target = day_target_sorted(dv, power, avail);
@@ -2414,9 +2427,11 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
     // the 8760 TS sell rate applies under net billing option 2 only (ff:626-641)
     c.src.ts = (t.mo == 2) ? c.ts_row : nullptr;
     if (!net_hourly(t)) {
+        PH_T0(tn);
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);
+        PH_ADD(12, tn, c.g.sl == 0);        // NEM set_tariff (bins + no-system bill)
     } else if constexpr (NET) {
         // net billing: the no-system bill from the load bins, then the split
         // of the search's hours for this tariff's periods
@@ -2456,7 +2471,9 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double total = ((c.capex * kw + 0.0) * c.ccm) + 0.0 + otc;     // ff:263,280-282
     double wb;
     if (!net_hourly(t)) {
+        PH_T0(tn);
         wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
+        PH_ADD(13, tn, c.g.sl == 0);        // NEM evaluation bill
     } else if constexpr (NET) {
         c.src.gen_scale = kws;
         PH_T0(te);
@@ -2486,7 +2503,9 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double w = wb * c.r_y;
     double wo = c.wo1 * c.r_y;
     double ev = wo - w;
+    PH_T0(tc);
     YFlow f = yl_cashflow(c.loan, total, ev, c.y, c.g, c.active);
+    PH_ADD(14, tc, c.g.sl == 0);            // cash flow + NPV + payback
     c.last.total = total;
     c.last.ev = ev;
     c.last.w = w;
@@ -2511,6 +2530,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
+    PH_T0(t_pro);
     const int half = lds_half(T.max_periods);
     YCtx<LPA> c(lane);
     const int sl = c.g.sl;
@@ -2603,6 +2623,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         c.tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
         c.thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
     }
+    PH_ADD(15, t_pro, sl == 0);             // prologue: agent loads, loan, bracket
     PH_T0(t_all);
     yl_set_tariff<LPA, DC, NET>(c, t0);
     int nfev = 0;

@@ -30,6 +30,10 @@ VARIANTS = {
     "base": [],
     # per-phase shader-cycle counters (bench.py prints them with DGEN_PHASE_PROF=1)
     "phase": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1")],
+    # k_hourly_batt day-target counters in slots 12-15 (battery lane-days, lanes
+    # whose whole need fits, wave-days where it fits for all lanes, saturated)
+    "phase_day": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
+                  ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1")],
     "db_cf4": [("#define DGEN_NB_DB_CF 8", "#define DGEN_NB_DB_CF 4")],
     "db_cf12": [("#define DGEN_NB_DB_CF 8", "#define DGEN_NB_DB_CF 12")],
     "hb_w3": [(HB, occ(HB, 3))],
