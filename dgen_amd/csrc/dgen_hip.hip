@@ -425,6 +425,48 @@ __device__ unsigned long long g_phase[16];
 #define PH_CNT(k, n, lead) do {} while (0)
 #endif
 
+__device__ __forceinline__ double pow_seq(double b, int e) {   // 1 * b * b ... (e times)
+    double r = 1.0;
+    for (int k = 0; k < e; k++) r = r * b;
+    return r;
+}
+
+// Net-billing split records (see the net-billing split section below): per
+// scratch slot, per (month, period) four sums linear in the generation scale
+// and the month's mixed hours.
+constexpr int NB_CAPM = 192;
+// an M entry carries the hour's own inputs, so an evaluation reads one
+// contiguous record instead of gathering the shape / cf (or system-output) /
+// TS rows at scattered hours: load L, generation term g (cf / 1e6 per kW in
+// the search, the system output in the battery case), the float32 sell
+// weight w and the period
+struct NbEnt {
+    double L, g;
+    float w;
+    int p;
+};
+static_assert(sizeof(NbEnt) == 24, "24-B mixed-hour entries");
+constexpr size_t NB_SUMS_BYTES = (size_t)12 * MAXP * 4 * sizeof(double);
+constexpr size_t NB_BYTES = NB_SUMS_BYTES + 64 + (size_t)12 * NB_CAPM * sizeof(NbEnt);
+static_assert(NB_BYTES % 16 == 0, "per-slot net-billing records stay 16-B aligned");
+static_assert(NB_BYTES == DGEN_NB_BYTES, "include/dgen_hip.h DGEN_NB_BYTES");
+
+struct NbRec {
+    double* sums;        // [12][MAXP][4]: SA_L, SA_g, SX_gw, SX_Lw
+    int* cnt;            // [12] M hours per month
+    NbEnt* ent;          // [12][NB_CAPM]
+};
+// cnt[12]: 1 when k_hourly_batt built the battery case's split into the record
+__device__ __forceinline__ int& nbr_flag(char* p) { return reinterpret_cast<int*>(p + NB_SUMS_BYTES)[12]; }
+__device__ __forceinline__ NbRec nb_rec(char* p) {
+    NbRec r;
+    r.sums = reinterpret_cast<double*>(p);
+    r.cnt = reinterpret_cast<int*>(p + NB_SUMS_BYTES);
+    r.ent = reinterpret_cast<NbEnt*>(p + NB_SUMS_BYTES + 64);
+    return r;
+}
+
+
 // ---------------------------------------------------------------------------
 // k_hourly_batt: one sequential scan over the year per agent
 // ---------------------------------------------------------------------------
@@ -674,7 +716,11 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 
 // F64: the hourly planes as doubles (the reference's fp64 lists) instead of
 // floats: the same values the scan computes, 32 B per lane per hour quad.
-template <bool HOURLY, bool F64>
+// NB: the batch has net-billing scratch slots; the scan then also builds the
+// battery case's net-billing split (below) for the agents that bill net
+// without a TS sell rate, so k_batt_finance bills them without a pass over
+// the system-output plane.
+template <bool HOURLY, bool F64, bool NB>
 __global__ void __launch_bounds__(BLOCK, 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on) {
@@ -728,6 +774,29 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const bool put_sys = need_sys && slot >= 0 && batt_on;
     int status = O.status[i] | t.flags;
     if (need_sys && slot < 0 && batt_on) status |= DGEN_ST_SCRATCH;
+    // The battery case's net-billing split over the agent's degradation range
+    // [s_lo, s_hi] (what k_batt_finance's yl_nb_build<true> builds from the
+    // plane), classified hour by hour as the scan produces the system output:
+    // import at both ends (import load / generation sums), export at both
+    // ends (export generation / load sums, sell weight 1: no TS rate), else a
+    // mixed entry in hour order.  Sums per (month, period) in the LDS bins
+    // (import) and bins2 (export), the current period's in registers.
+    bool put_nb = false;
+    double nb_lo = 0.0, nb_hi = 0.0;
+    NbRec nbr{nullptr, nullptr, nullptr};
+    if constexpr (NB) {
+        const bool is_ca = (A.flags[i] & 2) != 0;
+        const bool ts_on = t.mo == 2 && !is_ca && A.wholesale_row[i] >= 0 && T.wholesale != nullptr;
+        put_nb = put_sys && mo2 && !ts_on;
+        if (put_nb) {
+            const int N = A.econ_life[i];
+            const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+            const double sN = pow_seq(sys_base, (N >= 1 && N <= MAXY) ? N - 1 : 0);
+            nb_lo = sN < 1.0 ? sN : 1.0;
+            nb_hi = sN > 1.0 ? sN : 1.0;
+            nbr = nb_rec(ws_nb(ws, n, n_scratch) + (size_t)slot * NB_BYTES);
+        }
+    }
 
     const double inv_eta_in = 1.0 / cfg.batt_eta_in;
     const double in_per_bank = bank > 0.0 ? cfg.batt_eta_in / bank : 0.0;
@@ -778,7 +847,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // access of the kernel (the bins) behind a vmcnt(0).  Per wave: 12 chunks
     // x 64 lanes x 16 B = HB_DAY_BYTES.  (ISA check: DESIGN.md section 5.)
     const uint32_t dbase = (uint32_t)(size_t)(lds_ptr_t)(reinterpret_cast<char*>(dyn_lds) +
-                           (size_t)16 * lds_half(T.max_periods) * BLOCK +
+                           (size_t)(NB ? 32 : 16) * lds_half(T.max_periods) * BLOCK +
                            (size_t)(threadIdx.x / 64) * HB_DAY_BYTES);
     const uint32_t dbase_s = __builtin_amdgcn_readfirstlane(dbase);
     const uint32_t dlane = dbase_s + (threadIdx.x & 63u) * 16u;
@@ -796,8 +865,14 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     day_dma(d_lo);
     const int d_last = c_month_start_day[m_hi] - 1;
     DayRaw r;
+    double2* const bins2 = bins + (size_t)lds_half(T.max_periods) * BLOCK;   // NB: export sums
     for (int m = m_lo; m < m_hi; m++) {
         for (int p = 0; p < P; p++) bins[p * BLOCK] = make_double2(0.0, 0.0);
+        if (NB && put_nb)
+            for (int p = 0; p < P; p++) bins2[p * BLOCK] = make_double2(0.0, 0.0);
+        double2 xacc = make_double2(0.0, 0.0);
+        int n_m = 0;
+        NbEnt* const nb_ent = (NB && put_nb) ? nbr.ent + m * NB_CAPM : nullptr;
         // the current period's bin in registers (the same additions in the same
         // order as a per-hour LDS read-modify-write), written back when the
         // period changes and at the month's end
@@ -895,8 +970,47 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     }
                     bacc.x += ld;
                     bacc.y += st.sys;
+                } else if (NB && put_nb) {   // battery-case net-billing split
+                    const int p = (int)((sched[hh >> 3] >> (8 * (hh & 7))) & 0xffu);
+                    if (p != bcur) {
+                        bins[bcur * BLOCK] = bacc;
+                        bins2[bcur * BLOCK] = xacc;
+                        bcur = p;
+                        bacc = bins[p * BLOCK];
+                        xacc = bins2[p * BLOCK];
+                    }
+                    const double gk = st.sys;
+                    const double vlo = ld - gk * nb_lo, vhi = ld - gk * nb_hi;
+                    const double slack = 1e-10 * (fabs(ld) + fabs(gk) * nb_hi);
+                    const bool imp = fmin(vlo, vhi) > slack;               // imports at every s
+                    const bool exq = !imp && fmax(vlo, vhi) < -slack;      // exports at every s
+                    bacc.x += imp ? ld : 0.0;
+                    bacc.y += imp ? gk : 0.0;
+                    xacc.x += exq ? gk : 0.0;
+                    xacc.y += exq ? ld : 0.0;
+                    if (!imp && !exq) {
+                        if (n_m < NB_CAPM) {
+                            NbEnt e;
+                            e.L = ld;
+                            e.g = gk;
+                            e.w = 1.0f;
+                            e.p = p;
+                            nb_ent[n_m] = e;
+                        }
+                        n_m++;
+                    }
                 }
             }
+        }
+        if (NB && put_nb) {
+            bins[bcur * BLOCK] = bacc;
+            bins2[bcur * BLOCK] = xacc;
+            for (int p = 0; p < P; p++) {
+                const double2 a = bins[p * BLOCK], x = bins2[p * BLOCK];
+                double* q = nbr.sums + (m * MAXP + p) * 4;
+                q[0] = a.x; q[1] = a.y; q[2] = x.x; q[3] = x.y;
+            }
+            nbr.cnt[m] = n_m;
         }
         if (!mo2) bins[bcur * BLOCK] = bacc;
         if (!mo2) {
@@ -911,6 +1025,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
         W.carry[n + i] = annual;
         return;
     }
+    // the record holds this scan's battery-case split (k_batt_finance skips its build)
+    if (NB && mo2 && slot >= 0) nbr_flag(ws_nb(ws, n, n_scratch) + (size_t)slot * NB_BYTES) = put_nb ? 1 : 0;
     O.annual_kwh[i] = annual;
     double den = kw_star > 1e-9 ? kw_star : 1e-9;
     double naep = annual / den;
@@ -982,11 +1098,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ double pow_seq(double b, int e) {   // 1 * b * b ... (e times)
-    double r = 1.0;
-    for (int k = 0; k < e; k++) r = r * b;
-    return r;
-}
 
 // Per-block LDS (one wave):
 //   tariff [WAVE / LPA][dgen_tariff]                 (LPA < WAVE: staged copy, see stage_tariff)
@@ -1813,36 +1924,6 @@ __device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& 
 // agent back to the hourly pass.  Storage per scratch slot: NB_BYTES in the
 // caller's workspace.
 // ---------------------------------------------------------------------------
-constexpr int NB_CAPM = 192;
-// an M entry carries the hour's own inputs, so an evaluation reads one
-// contiguous record instead of gathering the shape / cf (or system-output) /
-// TS rows at scattered hours: load L, generation term g (cf / 1e6 per kW in
-// the search, the system output in the battery case), the float32 sell
-// weight w and the period
-struct NbEnt {
-    double L, g;
-    float w;
-    int p;
-};
-static_assert(sizeof(NbEnt) == 24, "24-B mixed-hour entries");
-constexpr size_t NB_SUMS_BYTES = (size_t)12 * MAXP * 4 * sizeof(double);
-constexpr size_t NB_BYTES = NB_SUMS_BYTES + 64 + (size_t)12 * NB_CAPM * sizeof(NbEnt);
-static_assert(NB_BYTES % 16 == 0, "per-slot net-billing records stay 16-B aligned");
-static_assert(NB_BYTES == DGEN_NB_BYTES, "include/dgen_hip.h DGEN_NB_BYTES");
-
-struct NbRec {
-    double* sums;        // [12][MAXP][4]: SA_L, SA_g, SX_gw, SX_Lw
-    int* cnt;            // [12] M hours per month
-    NbEnt* ent;          // [12][NB_CAPM]
-};
-__device__ __forceinline__ NbRec nb_rec(char* p) {
-    NbRec r;
-    r.sums = reinterpret_cast<double*>(p);
-    r.cnt = reinterpret_cast<int*>(p + NB_SUMS_BYTES);
-    r.ent = reinterpret_cast<NbEnt*>(p + NB_SUMS_BYTES + 64);
-    return r;
-}
-
 // The sell weight of an exported kWh: the float32-rounded TS sell rate
 // (ff:756) when the reference enables it, else 1 (the period's sell column is
 // applied per month).
@@ -1936,9 +2017,12 @@ __device__ bool yl_nb_build_serial(const dgen_tariff& t, const YSrc& src, double
 }
 
 // days per load batch: the battery case's f64 system output takes twice the
-// registers of the cf row, and k_batt_finance stays at 3 waves with 4
+// registers of the cf row, and k_batt_finance stays at 3 waves with 4; the
+// search's cf build measured 2 / 3 / 4 / 6 / 8 / 12 days: 21.2 / 20.3 / 20.0 /
+// 19.8 / 20.6 / 29.4 ms of C2 k_size at 200k (12 spills); sys 2 / 3 / 4 / 8:
+// 16.5 / 15.6 / 15.2 / 18.1 ms of k_batt_finance
 #ifndef DGEN_NB_DB_CF
-#define DGEN_NB_DB_CF 8
+#define DGEN_NB_DB_CF 6
 #endif
 #ifndef DGEN_NB_DB_SYS
 #define DGEN_NB_DB_SYS 4
@@ -2672,7 +2756,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
 template <int LPA, bool DC, bool NET>
 __global__ void __launch_bounds__(WAVE)
 k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-                 int64_t n_scratch, int64_t i0, int64_t i1, char* nbws) {
+                 int64_t n_scratch, int64_t i0, int64_t i1, char* nbws, int nb_scan) {
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -2750,8 +2834,13 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             src.gen_scale = 1.0;
             char* nbp = nbws + (size_t)slot * NB_BYTES;
             PH_T0(tb);
-            nb_ok = DGEN_NB_SERIAL ? yl_nb_build_serial(t, src, s_lo, s_hi, nbp, S, g)
-                                   : yl_nb_build<true>(t, src, s_lo, s_hi, nbp, S, g);
+            if (nb_scan && nbr_flag(nbp) == 1) {    // this step's k_hourly_batt built it in its scan
+                const NbRec R = nb_rec(nbp);
+                nb_ok = g.first(g.sl < 12 && R.cnt[g.sl] > NB_CAPM) < 0;
+            } else {
+                nb_ok = DGEN_NB_SERIAL ? yl_nb_build_serial(t, src, s_lo, s_hi, nbp, S, g)
+                                       : yl_nb_build<true>(t, src, s_lo, s_hi, nbp, S, g);
+            }
             PH_ADD(5, tb, g.sl == 0);
             PH_T0(te);
             if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S, g);
@@ -3311,6 +3400,7 @@ struct dgen_ctx {
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
     int battery;       // PV+battery forward run (dgen_set_battery)
+    int nb_scan;       // battery-case net-billing split in the hourly scan (dgen_set_nb_scan)
     int head;          // next ring slot to record
     int pending;       // recorded, not yet folded
     double sum_ms[3];
@@ -3378,6 +3468,7 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     c->chunks = DGEN_DEFAULT_CHUNKS;
     c->hb_months = DGEN_DEFAULT_HOURLY_MONTHS;
     c->battery = 1;
+    c->nb_scan = 1;
     c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
@@ -3534,7 +3625,10 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->head = (c->head + 1) % dgen_ctx::RING;
     c->pending++;
     c->nch[slot] = nch;
-    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK +
+    // k_hourly_batt: per-period bins [P][BLOCK] double2 (x2 with the net-billing
+    // split: import and export sums) + the waves' day buffers
+    const bool nb_scan = n_scratch > 0 && c->nb_scan && c->battery;
+    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK * (nb_scan ? 2 : 1) +
                        (size_t)(BLOCK / 64) * HB_DAY_BYTES;
     // two agents per wave when every analysis period fits 32 lanes, unless the
     // build guard withdrew that kernel's 32-lane instantiation (DGEN_NO2_*)
@@ -3590,15 +3684,19 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         dim3 grid((unsigned)((m + BLOCK - 1) / BLOCK)), block(BLOCK);
         for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
-            if (hourly && O->hourly_f64)
-                hipLaunchKernelGGL((k_hourly_batt<true, true>), grid, block, lds, s2, *T, *A, *O, c->cfg, n,
-                                   ws, n_scratch, i0, i1, m0, m1, c->battery);
-            else if (hourly)
-                hipLaunchKernelGGL((k_hourly_batt<true, false>), grid, block, lds, s2, *T, *A, *O, c->cfg, n,
-                                   ws, n_scratch, i0, i1, m0, m1, c->battery);
-            else
-                hipLaunchKernelGGL((k_hourly_batt<false, false>), grid, block, lds, s2, *T, *A, *O, c->cfg, n,
-                                   ws, n_scratch, i0, i1, m0, m1, c->battery);
+#define DGEN_HB_LAUNCH(H, F)                                                                      \
+    do {                                                                                          \
+        if (nb_scan)                                                                              \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, true>), grid, block, lds, s2, *T, *A, *O, c->cfg, n, \
+                               ws, n_scratch, i0, i1, m0, m1, c->battery);                        \
+        else                                                                                      \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false>), grid, block, lds, s2, *T, *A, *O, c->cfg,   \
+                               n, ws, n_scratch, i0, i1, m0, m1, c->battery);                     \
+    } while (0)
+            if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true);
+            else if (hourly) DGEN_HB_LAUNCH(true, false);
+            else DGEN_HB_LAUNCH(false, false);
+#undef DGEN_HB_LAUNCH
         }
         HIP_TRY(hipEventRecord(e[3], s2));
         if (!c->battery) {
@@ -3607,26 +3705,26 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
 #if !DGEN_NO2_FIN
             if (net)
                 hipLaunchKernelGGL((k_batt_finance_w<32, false, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws);
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
             else
                 hipLaunchKernelGGL((k_batt_finance_w<32, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws);
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
 #endif
         } else if (lpa_f == 32) {
 #if !DGEN_NO2_FIN_DC
             hipLaunchKernelGGL((k_batt_finance_w<32, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
-                               c->cfg, n, ws, n_scratch, i0, i1, nbws);
+                               c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
 #endif
         } else if (!dc) {
             if (net)
                 hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws);
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
             else
                 hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
-                                   *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws);
+                                   *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
         } else {
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
-                               c->cfg, n, ws, n_scratch, i0, i1, nbws);
+                               c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
         }
         HIP_TRY(hipEventRecord(e[4], s2));
     }
@@ -3651,6 +3749,15 @@ int32_t dgen_set_battery(dgen_ctx* c, int32_t on) {
         return DGEN_E_ARG;
     }
     c->battery = on;
+    return DGEN_OK;
+}
+
+int32_t dgen_set_nb_scan(dgen_ctx* c, int32_t on) {
+    if (!c || (on != 0 && on != 1)) {
+        set_err("dgen_set_nb_scan: on must be 0 or 1");
+        return DGEN_E_ARG;
+    }
+    c->nb_scan = on;
     return DGEN_OK;
 }
 

@@ -37,6 +37,8 @@ class AgentBatch:
     c_agents: _lib.Agents = field(default=None)
     # device row j holds caller agent perm[j] (None: caller order)
     perm: Optional[np.ndarray] = None
+    # build the battery case's net-billing split in the hourly scan (dgen_set_nb_scan)
+    nb_scan: bool = True
 
 
 def profile_order(cols: Dict[str, np.ndarray], major: str = "load",
@@ -146,6 +148,7 @@ class Engine:
         recs = np.ascontiguousarray(records, dtype=TARIFF_DTYPE)
         if recs.size == 0:
             raise ValueError("empty tariff table")
+        self._tariff_mo = recs["mo"].copy()
         dem = np.zeros(0, DEMAND_DTYPE) if demand is None else np.ascontiguousarray(demand, DEMAND_DTYPE)
         if int(recs["dc"].max()) > dem.size or int(recs["dc"].min()) < 0:
             raise ValueError("tariff dc index outside the demand table")
@@ -218,7 +221,27 @@ class Engine:
         ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
         ca = _lib.Agents(**{name: _ptr(dev[name]) for name, _ in _lib.AGENT_COLUMNS})
         ca.max_years = int(dev["econ_life"].max().item()) if n else 0
-        return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order)
+        return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order,
+                          nb_scan=self._nb_scan_pays(cols, n, n_scratch))
+
+    NB_SCAN_MIN_SHARE = 0.25
+
+    def _nb_scan_pays(self, cols, n: int, n_scratch: int) -> bool:
+        """dgen_set_nb_scan per batch: the scan-side split pays off when a large
+        share of the batch bills net without a TS sell rate (initial tariff;
+        the share is a cost heuristic only -- results do not depend on it)."""
+        mo_t = getattr(self, "_tariff_mo", None)
+        if n == 0 or n_scratch == 0 or mo_t is None:
+            return True
+        try:
+            sl = np.asarray(cols["scratch_slot"])
+            mo = mo_t[np.asarray(cols["tariff0"], np.int64)]
+            ts = (mo == 2) & ((np.asarray(cols["flags"]) & 2) == 0) & (np.asarray(cols["wholesale_row"]) >= 0)
+        except Exception:          # device-tensor columns: keep the default
+            return True
+        if not self.tables.wholesale:
+            ts[:] = False
+        return bool(((sl >= 0) & ((mo == 2) | (mo == 3)) & ~ts).mean() >= self.NB_SCAN_MIN_SHARE)
 
     def validate_agents(self, dev, n):
         """Host-side bounds checks before any kernel indexes a table."""
@@ -272,6 +295,9 @@ class Engine:
     def size(self, batch: AgentBatch, out: Dict[str, object], c_out: Optional[_lib.Outputs] = None):
         """Launch the sizing kernels for `batch` on the current stream (async)."""
         co = c_out if c_out is not None else self.c_outputs(out)
+        if batch.nb_scan != getattr(self, "_nb_scan", True):
+            _lib.check(self.lib.dgen_set_nb_scan(self.ctx, int(batch.nb_scan)), "dgen_set_nb_scan")
+            self._nb_scan = batch.nb_scan
         _lib.check(self.lib.dgen_size_agents(self.ctx, ctypes.byref(self.tables),
                                              ctypes.byref(batch.c_agents), ctypes.byref(co),
                                              batch.n, _ptr(batch.workspace),

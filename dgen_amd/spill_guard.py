@@ -97,42 +97,109 @@ def report(hits) -> str:
     return "\n".join(out)
 
 
-if __name__ == "__main__":
-    h = scan(sys.argv[1])
-    print(report(h) or "no spill ahead of an exec restore")
-    sys.exit(1 if h else 0)
+def _blocks(body):
+    """Basic blocks of a function body (stripped lines): split at labels and
+    after every branch.  Returns [(label or None, [instructions], [successor
+    block indices])]."""
+    blocks, cur = [], [None, []]
+    for l in body:
+        if not l or l.startswith((";", ".")) and not l.startswith(".LBB"):
+            continue
+        m = re.match(r"^(\.LBB\w+):", l)
+        if m:
+            blocks.append(cur)
+            cur = [m.group(1), []]
+            continue
+        cur[1].append(l)
+        if l.startswith(("s_branch", "s_cbranch", "s_endpgm", "s_setpc")):
+            blocks.append(cur)
+            cur = [None, []]
+    blocks.append(cur)
+    blocks = [b for b in blocks if b[0] is not None or b[1]]
+    index = {b[0]: k for k, b in enumerate(blocks) if b[0]}
+    out = []
+    for k, (lab, ins) in enumerate(blocks):
+        succ = []
+        last = ins[-1] if ins else ""
+        tgt = last.split()[1] if last.startswith(("s_branch", "s_cbranch")) and len(last.split()) > 1 else None
+        if last.startswith("s_branch"):
+            succ = [index[tgt]] if tgt in index else []
+        elif last.startswith(("s_endpgm", "s_setpc")):
+            succ = []
+        else:
+            if last.startswith("s_cbranch") and tgt in index:
+                succ.append(index[tgt])
+            if k + 1 < len(blocks):
+                succ.append(k + 1)
+        out.append((lab, ins, succ))
+    return out
+
+
+VMEM = re.compile(r"^(global_|buffer_|scratch_)")
+DMA = "global_load_lds_dwordx4"
 
 
 def day_dma_wait(path, kernel="k_hourly_battILb1E"):
     """ISA check of k_hourly_batt's next-day LDS DMA:
-    the day loop's read-back waits `s_waitcnt vmcnt(K)`; vmcnt retires in issue
-    order, so the 12 global_load_lds_dwordx4 of the previous day have landed if
-    at least K vector-memory ops are issued after the last of them on every
-    path to the wait.  Counts the ops between the last DMA and the loop's back
-    edge outside blocks an `s_cbranch_execz` can skip.  Every instantiation
-    whose symbol contains `kernel` is checked; returns the (K, issued) pair
-    with the smallest margin."""
+    the day loop's read-back waits `s_waitcnt vmcnt(K)` (directly ahead of its
+    ds_read_b128s); vmcnt retires in issue order, so the previous day's 12
+    global_load_lds_dwordx4 have landed if at least K vector-memory ops are
+    issued after the last of them on EVERY path to the wait.  The count is the
+    shortest path over the control-flow graph from each DMA group's last
+    instruction to each wait (a block an s_cbranch_execz skips counts nothing
+    on the path that skips it; a path through another DMA group or a full
+    drain, s_waitcnt vmcnt(0), ends there).
+    Every instantiation whose symbol contains `kernel` is checked; returns the
+    (K, issued) pair with the smallest margin."""
+    import heapq
     lines = open(path).read().split("\n")
     starts = [i for i, l in enumerate(lines) if re.match(r"_Z\S*" + kernel + r"\S*:", l)]
     worst = None
     for st in starts:
         en = next(i for i in range(st, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
-        body = [l.strip() for l in lines[st:en]]
-        waits = [int(re.search(r"vmcnt\((\d+)\)", body[i]).group(1)) for i in range(len(body) - 1)
-                 if body[i].startswith("s_waitcnt") and "vmcnt(" in body[i]
-                 and body[i + 1].startswith("ds_read_b128")]
-        k = max(waits)
-        last = max(i for i, l in enumerate(body) if l.startswith("global_load_lds_dwordx4"))
-        issued, cond = 0, False
-        for l in body[last + 1:]:
-            if l.startswith(".LBB"):
-                cond = False
-            elif l.startswith("s_cbranch_execz"):
-                cond = True
-            elif l.startswith("s_branch"):
-                break
-            elif re.match(r"(global_|buffer_|scratch_)", l) and not cond:
-                issued += 1
-        if worst is None or issued - k < worst[1] - worst[0]:
-            worst = (k, issued)
+        B = _blocks([l.strip() for l in lines[st + 1:en]])
+        # wait sites: (block, position, K)
+        waits = [(k, j, int(re.search(r"vmcnt\((\d+)\)", ins[j]).group(1)))
+                 for k, (_, ins, _) in enumerate(B) for j in range(len(ins) - 1)
+                 if ins[j].startswith("s_waitcnt") and "vmcnt(" in ins[j] and ins[j + 1].startswith("ds_read_b128")]
+        srcs = [(k, max(j for j, l in enumerate(ins) if l.startswith(DMA)))
+                for k, (_, ins, _) in enumerate(B) if any(l.startswith(DMA) for l in ins)]
+        for kb, jd in srcs:
+            # cost of entering block b from its top, up to a DMA or a full
+            # drain s_waitcnt vmcnt(0) (either ends the path) or its end
+            def head(b):
+                c = 0
+                for l in B[b][1]:
+                    if l.startswith(DMA) or (l.startswith("s_waitcnt") and "vmcnt(0)" in l):
+                        return c, True
+                    c += bool(VMEM.match(l))
+                return c, False
+            tail = sum(bool(VMEM.match(l)) for l in B[kb][1][jd + 1:])
+            dist = {}
+            pq = [(tail, s) for s in B[kb][2]]
+            while pq:
+                d, b = heapq.heappop(pq)
+                if b in dist:
+                    continue
+                dist[b] = d
+                c, stop = head(b)
+                if not stop:
+                    for s2 in B[b][2]:
+                        if s2 not in dist:
+                            heapq.heappush(pq, (d + c, s2))
+            for wb, wj, K in waits:
+                if wb not in dist or K == 0:
+                    continue
+                pre = B[wb][1][:wj]
+                if any(l.startswith(DMA) or (l.startswith("s_waitcnt") and "vmcnt(0)" in l) for l in pre):
+                    continue
+                issued = dist[wb] + sum(bool(VMEM.match(l)) for l in pre)
+                if worst is None or issued - K < worst[1] - worst[0]:
+                    worst = (K, issued)
     return worst
+
+
+if __name__ == "__main__":
+    h = scan(sys.argv[1])
+    print(report(h) or "no spill ahead of an exec restore")
+    sys.exit(1 if h else 0)

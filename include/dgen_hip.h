@@ -514,6 +514,16 @@ int32_t dgen_set_hourly_segment(dgen_ctx* ctx, int32_t months);
  * left untouched.                                                          */
 int32_t dgen_set_battery(dgen_ctx* ctx, int32_t on);
 
+/* Where the battery case's net-billing split is built for agents that bill
+ * net without a TS sell rate: 1 (default) in k_hourly_batt's scan, as the
+ * system output is produced (k_batt_finance then bills from the record), or
+ * 0 in k_batt_finance from the system-output plane.  Results are equal up to
+ * the rounding of the re-associated sums.  The scan form pays its
+ * classification in every wave that holds such an agent, so a batch where
+ * few agents qualify is faster with 0 (the Python engine decides per batch:
+ * Engine.upload_agents).  Replaces nothing in the reference.               */
+int32_t dgen_set_nb_scan(dgen_ctx* ctx, int32_t on);
+
 #ifdef __cplusplus
 }
 #endif

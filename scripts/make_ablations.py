@@ -34,8 +34,8 @@ VARIANTS = {
     # whose whole need fits, wave-days where it fits for all lanes, saturated)
     "phase_day": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
                   ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1")],
-    "db_cf4": [("#define DGEN_NB_DB_CF 8", "#define DGEN_NB_DB_CF 4")],
-    "db_cf12": [("#define DGEN_NB_DB_CF 8", "#define DGEN_NB_DB_CF 12")],
+    "db_cf4": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 4")],
+    "db_cf12": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 12")],
     "hb_w3": [(HB, occ(HB, 3))],
     "hb_w4": [(HB, occ(HB, 4))],
     "ks_w3": [(KS, occ(KS, 3))],
@@ -120,6 +120,26 @@ VARIANTS = {
                 "            c.dem_wo_pending = false;\n            c.dbg_e++;\n        }\n    }"),
                ('extern "C" {', 'extern "C" {\nint32_t dgen_debug_dcdbg(void* dst) { return (int32_t)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dcdbg), sizeof(g_dcdbg)); }')],
     # two-agent demand-charge k_size at 1 wave per SIMD (round 1's no-spill build; now 2 waves)
+    # net-billing k_size (C2) at 2 waves per SIMD (no spills) instead of 3
+    "ks_net_occ2": [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC || NET ? 2 : 3)")],
+    # k_batt_finance at 2 / 4 waves per SIMD
+    "kf_occ2": [("__global__ void __launch_bounds__(WAVE)\nk_batt_finance_w(",
+                 "__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(2, 2)))\nk_batt_finance_w(")],
+    "kf_occ4": [("__global__ void __launch_bounds__(WAVE)\nk_batt_finance_w(",
+                 "__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4)))\nk_batt_finance_w(")],
+    # days per load batch of the cooperative net-billing build
+    "nb_db_cf4": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 4")],
+    "nb_db_cf12": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 12")],
+    "nb_db_cf2": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 2")],
+    "nb_db_cf3": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 3")],
+    "nb_db_cf6": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 6")],
+    "nb_db_sys2": [("#define DGEN_NB_DB_SYS 4", "#define DGEN_NB_DB_SYS 2")],
+    "nb_db_sys3": [("#define DGEN_NB_DB_SYS 4", "#define DGEN_NB_DB_SYS 3")],
+    "nb_db_sys8": [("#define DGEN_NB_DB_SYS 4", "#define DGEN_NB_DB_SYS 8")],
+    # k_hourly_batt's battery-case split (NB instantiation): off (LDS still
+    # doubled: the occupancy cost alone) / without its mixed-entry stores
+    "hb_nb_off": [("        put_nb = put_sys && mo2 && !ts_on;", "        put_nb = false && put_sys && mo2 && !ts_on;")],
+    "hb_nb_nostore": [("                            nb_ent[n_m] = e;", "                            (void)e;")],
     "ks_dc_occ1": [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)")],
     # k_batt_finance without its battery-case demand pass (what the rest costs)
     "kf_no_dem": [("            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);",

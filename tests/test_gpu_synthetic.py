@@ -221,3 +221,32 @@ def test_hourly_f64_planes(engine):
     s32 = state_hourly(engine, (o32["baseline"], o32["net_pvonly"], o32["net_with_batt"]), w, None, seg)
     s64 = state_hourly(engine, (o64["baseline"], o64["net_pvonly"], o64["net_with_batt"]), w, None, seg)
     assert torch.allclose(s32, s64, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("cfg", ["ca_res_storage", "metering_mix"])
+def test_nb_scan_split_equals_finance_build(engine, cfg):
+    """The battery case's net-billing split built in k_hourly_batt's scan
+    (dgen_set_nb_scan(1)) bills like the split k_batt_finance builds from the
+    system-output plane (0): the same hours, sums re-associated (1e-9), and
+    every PV-only / hourly output bit-identical."""
+    pop = _small_pop(cfg, 600)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    assert batch.n_scratch > 0
+    res = []
+    try:
+        for on in (True, False):
+            batch.nb_scan = on
+            out = engine.alloc_outputs(batch.n, hourly=True)
+            engine.size(batch, out)
+            torch.cuda.synchronize()
+            res.append(outputs_to_host(out))
+    finally:
+        batch.nb_scan = True
+    a, b = res
+    for k in ("system_kw", "npv", "nfev", "baseline", "net_pvonly", "net_with_batt", "batt_kwh"):
+        assert np.array_equal(a[k], b[k], equal_nan=True), k
+    for k in ("npv_pv_batt", "bill_w_batt", "bill_wo_batt", "cfev_batt"):
+        assert np.allclose(a[k], b[k], rtol=1e-9, atol=1e-9, equal_nan=True), k

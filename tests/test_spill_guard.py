@@ -88,7 +88,7 @@ DMA = """_ZN12_GLOBAL__N_113k_hourly_battILb1EEEv11dgen_tables:   ; @k
 \tglobal_store_dwordx4 v[0:1], v[4:7], off
 .LBB16_69:
 \tglobal_store_dwordx4 v[0:1], v[4:7], off nt
-STORES\ts_branch .LBB16_40
+STORES\ts_branch .LBB16_41
 .Lfunc_end16:
 """
 
@@ -99,3 +99,6 @@ def test_day_dma_wait_counts_unconditional_ops(tmp_path):
     assert G.day_dma_wait(str(p)) == (4, 3)       # the two skippable stores do not count
     p.write_text(DMA.replace("STORES", "\tglobal_store_dwordx4 v[0:1], v[4:7], off nt\n"))
     assert G.day_dma_wait(str(p)) == (4, 4)
+    # a full drain on the way (s_waitcnt vmcnt(0)) covers the wait by itself
+    p.write_text(DMA.replace("STORES", "\ts_waitcnt vmcnt(0)\n"))
+    assert G.day_dma_wait(str(p)) is None
