@@ -446,6 +446,17 @@ struct NbEnt {
     int p;
 };
 static_assert(sizeof(NbEnt) == 24, "24-B mixed-hour entries");
+// The scan's compact form (k_hourly_batt, battery case, sell weight 1): the
+// generation term, the hour's float32 shape value (the load is that x the
+// load scale, exactly as the scan formed it, re-derived when the entry is
+// fetched) and the period -- one 16-B store per mixed hour instead of 24 B in
+// two stores.
+struct NbEntC {
+    double g;
+    float sh;
+    int p;
+};
+static_assert(sizeof(NbEntC) == 16, "16-B compact mixed-hour entries");
 constexpr size_t NB_SUMS_BYTES = (size_t)12 * MAXP * 4 * sizeof(double);
 constexpr size_t NB_BYTES = NB_SUMS_BYTES + 64 + (size_t)12 * NB_CAPM * sizeof(NbEnt);
 static_assert(NB_BYTES % 16 == 0, "per-slot net-billing records stay 16-B aligned");
@@ -872,7 +883,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             for (int p = 0; p < P; p++) bins2[p * BLOCK] = make_double2(0.0, 0.0);
         double2 xacc = make_double2(0.0, 0.0);
         int n_m = 0;
-        NbEnt* const nb_ent = (NB && put_nb) ? nbr.ent + m * NB_CAPM : nullptr;
+        NbEntC* const nb_ent = (NB && put_nb) ? reinterpret_cast<NbEntC*>(nbr.ent) + m * NB_CAPM : nullptr;
         // the current period's bin in registers (the same additions in the same
         // order as a per-hour LDS read-modify-write), written back when the
         // period changes and at the month's end
@@ -990,10 +1001,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     xacc.y += exq ? ld : 0.0;
                     if (!imp && !exq) {
                         if (n_m < NB_CAPM) {
-                            NbEnt e;
-                            e.L = ld;
+                            NbEntC e;
                             e.g = gk;
-                            e.w = 1.0f;
+                            e.sh = r.s[hh];
                             e.p = p;
                             nb_ent[n_m] = e;
                         }
@@ -2190,7 +2200,7 @@ __device__ __forceinline__ int nb_wave_max(int v) {
 // order as the hourly pass on the M hours.
 template <int LPA>
 __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& src, double s, char* nbp,
-                                             const YLds& S, const Seg<LPA>& g) {
+                                             const YLds& S, const Seg<LPA>& g, bool compact = false) {
     const NbRec R = nb_rec(nbp);
     const int P = t.P, half = S.half;
     const double kws = src.gen_scale;
@@ -2206,7 +2216,14 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
     int fm = -1, fj = 0;                         // which chunk the registers hold
     auto fetch = [&](int m, int j0, int n) __attribute__((always_inline)) {
         const int j = j0 + g.sl;
-        if (j < n) {
+        if (j < n && compact) {   // NbEntC: the load re-derived from the hour's shape value
+            const NbEntC* e = reinterpret_cast<const NbEntC*>(R.ent) + m * NB_CAPM + j;
+            const double2 v = *reinterpret_cast<const double2*>(e);
+            const long long sp = __double_as_longlong(v.y);
+            xg = v.x;
+            xL = (double)__int_as_float((int)(sp & 0xffffffffll)) * src.load_scale;
+            xwp = __longlong_as_double((sp & ~0xffffffffll) | (long long)(unsigned)__float_as_int(1.0f));
+        } else if (j < n) {
             const double* e = reinterpret_cast<const double*>(R.ent + m * NB_CAPM + j);
             xL = e[0];
             xg = e[1];
@@ -2834,7 +2851,8 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             src.gen_scale = 1.0;
             char* nbp = nbws + (size_t)slot * NB_BYTES;
             PH_T0(tb);
-            if (nb_scan && nbr_flag(nbp) == 1) {    // this step's k_hourly_batt built it in its scan
+            const bool scan_rec = nb_scan && nbr_flag(nbp) == 1;
+            if (scan_rec) {    // this step's k_hourly_batt built it in its scan (compact entries)
                 const NbRec R = nb_rec(nbp);
                 nb_ok = g.first(g.sl < 12 && R.cnt[g.sl] > NB_CAPM) < 0;
             } else {
@@ -2843,7 +2861,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             }
             PH_ADD(5, tb, g.sl == 0);
             PH_T0(te);
-            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S, g);
+            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S, g, scan_rec);
             PH_ADD(6, te, g.sl == 0);
         }
         if (!nb_ok) wb = yl_bill_net(t, src, s_y, true, S);

@@ -230,6 +230,10 @@ class Engine:
         """dgen_set_nb_scan per batch: the scan-side split pays off when a large
         share of the batch bills net without a TS sell rate (initial tariff;
         the share is a cost heuristic only -- results do not depend on it)."""
+        import os
+        force = os.environ.get("DGEN_NB_SCAN")          # "0" / "1" override the heuristic
+        if force in ("0", "1"):
+            return force == "1"
         mo_t = getattr(self, "_tariff_mo", None)
         if n == 0 or n_scratch == 0 or mo_t is None:
             return True
