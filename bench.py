@@ -94,8 +94,8 @@ def pmc_traffic(pmc_dir: str, workload: str):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=120)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--agents", type=int, default=1_000_000, help="agents per GPU")
     ap.add_argument("--config", default="res_1m_nem_tou")
     ap.add_argument("--no-hourly", action="store_true", help="on-device reduction mode")
@@ -181,9 +181,16 @@ def main():
     ws, rank, local = dist_env()
     import torch
     import torch.distributed as dist
+    # one rank per GPU (RCCL); DGEN_DIST_BACKEND=gloo rehearses the N > 1 flow
+    # with several ranks on one GPU (device = LOCAL_RANK mod the visible GPUs)
+    backend = os.environ.get("DGEN_DIST_BACKEND", "nccl")
     if ws > 1:
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from dgen_amd.config import EngineConfig
     from dgen_amd.engine import Engine, profile_order
     from dgen_amd.synth import make_population
@@ -213,7 +220,7 @@ def main():
     eng.kernel_times()                      # drop warmup events
 
     el = timed_region(lambda: eng.size(batch, out, c_out), args.steps, torch.cuda.synchronize,
-                      dist if ws > 1 else None, eng.dev)
+                      dist if ws > 1 else None, eng.dev if backend == "nccl" else "cpu")
     ms_size, ms_hourly, ms_fin, cnt = eng.kernel_times()
     if os.environ.get("DGEN_PHASE_PROF") and hasattr(eng.lib, "dgen_phase_read"):   # ablation builds only
         import ctypes
