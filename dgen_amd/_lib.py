@@ -17,6 +17,7 @@ NSLOT = 576
 MAXP = 12
 MAXT = 6
 MAXY = 50
+NB_CAPM = 192   # include/dgen_hip.h DGEN_NB_CAPM (mixed hours per month of a net-billing record)
 
 ST_BOUNDS = 0x01
 ST_TARIFF = 0x02

@@ -434,7 +434,14 @@ __device__ __forceinline__ double pow_seq(double b, int e) {   // 1 * b * b ... 
 // Net-billing split records (see the net-billing split section below): per
 // scratch slot, per (month, period) four sums linear in the generation scale
 // and the month's mixed hours.
-constexpr int NB_CAPM = 192;
+// NB_SYS_ZERO_IMPORT: in the battery case the hours where the battery takes
+// the whole PV surplus have system output = load up to an ulp, i.e. an import
+// of ~0 at s = 1 and a small one below; counted as mixed they overflowed the
+// record for a third of the CA-like agents.  The battery-case splits (scan and
+// plane build alike) put an hour whose import is above -slack at both ends of
+// [s_lo, s_hi] on the import side: its linear term then bills at most the
+// slack (1e-10 of the hour's load + generation) of export as negative import.
+constexpr int NB_CAPM = DGEN_NB_CAPM;
 // an M entry carries the hour's own inputs, so an evaluation reads one
 // contiguous record instead of gathering the shape / cf (or system-output) /
 // TS rows at scattered hours: load L, generation term g (cf / 1e6 per kW in
@@ -734,7 +741,8 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 template <bool HOURLY, bool F64, bool NB>
 __global__ void __launch_bounds__(BLOCK, 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-              int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on) {
+              int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
+              int repair) {
     // agents [i0, i1) of a batch of n (row stride of every plane stays n),
     // months [m_lo, m_hi) of the year: the year is swept in month segments,
     // one launch each, so that every resident wave works on the same weeks
@@ -743,6 +751,11 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     int64_t i = i0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= i1) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
+    // repair pass: only the agents whose scan-built split overflowed and whose
+    // system-output plane was therefore not written (flag 2) run again, with
+    // the plane; every other output it writes is the same value again
+    if (repair && !(A.scratch_slot[i] >= 0 &&
+                    nbr_flag(ws_nb(ws, n, n_scratch) + (size_t)A.scratch_slot[i] * NB_BYTES) == 2)) return;
     WsLayout W = ws_layout(ws, n);
     // battery-case bins: (load, system output) pairs per period, [p][BLOCK]
     double2* bins = reinterpret_cast<double2*>(dyn_lds) + threadIdx.x;
@@ -781,7 +794,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const int slot = A.scratch_slot[i];
     // the battery-case bill reads the hourly system output for net billing and
     // for demand charges (both need hourly imports, not bins)
-    const bool need_sys = mo2 || tariff_demand(T, cfg, t) != nullptr;
+    const bool has_dc = tariff_demand(T, cfg, t) != nullptr;
+    const bool need_sys = mo2 || has_dc;
     const bool put_sys = need_sys && slot >= 0 && batt_on;
     int status = O.status[i] | t.flags;
     if (need_sys && slot < 0 && batt_on) status |= DGEN_ST_SCRATCH;
@@ -793,12 +807,13 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // mixed entry in hour order.  Sums per (month, period) in the LDS bins
     // (import) and bins2 (export), the current period's in registers.
     bool put_nb = false;
+    bool nb_over = false;        // a month's mixed hours exceeded nb_cap
     double nb_lo = 0.0, nb_hi = 0.0;
     NbRec nbr{nullptr, nullptr, nullptr};
     if constexpr (NB) {
         const bool is_ca = (A.flags[i] & 2) != 0;
         const bool ts_on = t.mo == 2 && !is_ca && A.wholesale_row[i] >= 0 && T.wholesale != nullptr;
-        put_nb = put_sys && mo2 && !ts_on;
+        put_nb = put_sys && mo2 && !ts_on && nb_cap > 0;
         if (put_nb) {
             const int N = A.econ_life[i];
             const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
@@ -808,6 +823,10 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             nbr = nb_rec(ws_nb(ws, n, n_scratch) + (size_t)slot * NB_BYTES);
         }
     }
+    // the split replaces the system-output plane for the energy bill; demand
+    // charges still read the plane, and an overflowing split gets it from the
+    // repair pass
+    const bool skip_plane = put_nb && !has_dc;
 
     const double inv_eta_in = 1.0 / cfg.batt_eta_in;
     const double in_per_bank = bank > 0.0 ? cfg.batt_eta_in / bank : 0.0;
@@ -965,7 +984,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 }
                 qs[hh & 3] = st.sys;
                 if ((hh & 3) == 3) {
-                    if (put_sys) {                              // tile [h / 4][slot][4]
+                    if (put_sys && !skip_plane) {               // tile [h / 4][slot][4]
                         double2* q = reinterpret_cast<double2*>(osc + hq32 + off32);
                         q[0] = make_double2(qs[0], qs[1]);
                         q[1] = make_double2(qs[2], qs[3]);
@@ -993,14 +1012,14 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     const double gk = st.sys;
                     const double vlo = ld - gk * nb_lo, vhi = ld - gk * nb_hi;
                     const double slack = 1e-10 * (fabs(ld) + fabs(gk) * nb_hi);
-                    const bool imp = fmin(vlo, vhi) > slack;               // imports at every s
+                    const bool imp = fmin(vlo, vhi) > -slack;              // imports (or ~0) at every s
                     const bool exq = !imp && fmax(vlo, vhi) < -slack;      // exports at every s
                     bacc.x += imp ? ld : 0.0;
                     bacc.y += imp ? gk : 0.0;
                     xacc.x += exq ? gk : 0.0;
                     xacc.y += exq ? ld : 0.0;
                     if (!imp && !exq) {
-                        if (n_m < NB_CAPM) {
+                        if (n_m < nb_cap) {
                             NbEntC e;
                             e.g = gk;
                             e.sh = r.s[hh];
@@ -1020,7 +1039,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 double* q = nbr.sums + (m * MAXP + p) * 4;
                 q[0] = a.x; q[1] = a.y; q[2] = x.x; q[3] = x.y;
             }
-            nbr.cnt[m] = n_m;
+            nbr.cnt[m] = n_m <= nb_cap ? n_m : NB_CAPM + 1;     // > NB_CAPM: overflow
         }
         if (!mo2) bins[bcur * BLOCK] = bacc;
         if (!mo2) {
@@ -1035,8 +1054,17 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
         W.carry[n + i] = annual;
         return;
     }
-    // the record holds this scan's battery-case split (k_batt_finance skips its build)
-    if (NB && mo2 && slot >= 0) nbr_flag(ws_nb(ws, n, n_scratch) + (size_t)slot * NB_BYTES) = put_nb ? 1 : 0;
+    // the record holds this scan's battery-case split (1: k_batt_finance skips
+    // its build), or it overflowed without a plane (2: the repair pass writes
+    // the plane, k_batt_finance builds from it), or neither (0)
+    if (NB && mo2 && slot >= 0) {
+        int fl = 0;
+        if (put_nb) {
+            for (int k = 0; k < 12; k++) nb_over = nb_over || nbr.cnt[k] > NB_CAPM;
+            fl = !nb_over ? 1 : (skip_plane ? 2 : 0);
+        }
+        nbr_flag(ws_nb(ws, n, n_scratch) + (size_t)slot * NB_BYTES) = fl;
+    }
     O.annual_kwh[i] = annual;
     double den = kw_star > 1e-9 ? kw_star : 1e-9;
     double naep = annual / den;
@@ -1047,9 +1075,11 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     if (!batt_on || unsized) O.npv_pv_batt[i] = NAN;   // k_batt_finance does not run
     // battery run on the PV run's tariff: k_batt_finance reuses its no-system
     // bill (same load, same tariff -> the same bill, as in the oracle)
-    W.aux[i] = (tariff != O.tariff_final[i]) ? 1.0 : 0.0;
-    O.tariff_final[i] = tariff;
-    O.switched[i] = switched;
+    if (!repair) {   // the repair pass starts from the already switched tariff
+        W.aux[i] = (tariff != O.tariff_final[i]) ? 1.0 : 0.0;
+        O.tariff_final[i] = tariff;
+        O.switched[i] = switched;
+    }
     O.status[i] = status;
     W.otc_b[i] = otc;
 }
@@ -2104,7 +2134,9 @@ __device__ __forceinline__ bool yl_nb_build(const dgen_tariff& t, const YSrc& sr
                 const float w = cur.w[k];
                 const double vlo = L - gk * tlo, vhi = L - gk * thi;
                 const double slack = 1e-10 * (fabs(L) + fabs(gk) * thi);
-                const bool imp = act && fmin(vlo, vhi) > slack;            // imports at every t
+                // battery case (SYS): an hour within the slack of zero joins the
+                // import side (NB_SYS_ZERO_IMPORT below)
+                const bool imp = act && fmin(vlo, vhi) > (SYS ? -slack : slack);   // imports at every t
                 const bool exq = act && !imp && fmax(vlo, vhi) < -slack;   // exports at every t
                 const double wd = (double)w;
                 const double i0 = imp ? L : 0.0, i1 = imp ? gk : 0.0;
@@ -3418,7 +3450,7 @@ struct dgen_ctx {
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
     int battery;       // PV+battery forward run (dgen_set_battery)
-    int nb_scan;       // battery-case net-billing split in the hourly scan (dgen_set_nb_scan)
+    int nb_scan;       // battery-case split in the hourly scan: its per-month entry capacity, 0 = off (dgen_set_nb_scan)
     int head;          // next ring slot to record
     int pending;       // recorded, not yet folded
     double sum_ms[3];
@@ -3486,7 +3518,7 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     c->chunks = DGEN_DEFAULT_CHUNKS;
     c->hb_months = DGEN_DEFAULT_HOURLY_MONTHS;
     c->battery = 1;
-    c->nb_scan = 1;
+    c->nb_scan = DGEN_NB_CAPM;
     c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
@@ -3702,18 +3734,25 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         dim3 grid((unsigned)((m + BLOCK - 1) / BLOCK)), block(BLOCK);
         for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
-#define DGEN_HB_LAUNCH(H, F)                                                                      \
+#define DGEN_HB_LAUNCH(H, F, REP)                                                                 \
     do {                                                                                          \
-        if (nb_scan)                                                                              \
+        if (nb_scan && !(REP))                                                                    \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true>), grid, block, lds, s2, *T, *A, *O, c->cfg, n, \
-                               ws, n_scratch, i0, i1, m0, m1, c->battery);                        \
+                               ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0);         \
         else                                                                                      \
             hipLaunchKernelGGL((k_hourly_batt<H, F, false>), grid, block, lds, s2, *T, *A, *O, c->cfg,   \
-                               n, ws, n_scratch, i0, i1, m0, m1, c->battery);                     \
+                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? 1 : 0);   \
     } while (0)
-            if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true);
-            else if (hourly) DGEN_HB_LAUNCH(true, false);
-            else DGEN_HB_LAUNCH(false, false);
+            if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, false);
+            else if (hourly) DGEN_HB_LAUNCH(true, false, false);
+            else DGEN_HB_LAUNCH(false, false, false);
+        }
+        // repair pass (agents whose scan-built split overflowed: their plane)
+        for (int m0 = 0; nb_scan && m0 < 12; m0 += c->hb_months) {
+            const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
+            if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, true);
+            else if (hourly) DGEN_HB_LAUNCH(true, false, true);
+            else DGEN_HB_LAUNCH(false, false, true);
 #undef DGEN_HB_LAUNCH
         }
         HIP_TRY(hipEventRecord(e[3], s2));
@@ -3770,12 +3809,12 @@ int32_t dgen_set_battery(dgen_ctx* c, int32_t on) {
     return DGEN_OK;
 }
 
-int32_t dgen_set_nb_scan(dgen_ctx* c, int32_t on) {
-    if (!c || (on != 0 && on != 1)) {
-        set_err("dgen_set_nb_scan: on must be 0 or 1");
+int32_t dgen_set_nb_scan(dgen_ctx* c, int32_t cap) {
+    if (!c || cap < 0 || cap > DGEN_NB_CAPM) {
+        set_err("dgen_set_nb_scan: cap must be in [0, %d]", DGEN_NB_CAPM);
         return DGEN_E_ARG;
     }
-    c->nb_scan = on;
+    c->nb_scan = cap;
     return DGEN_OK;
 }
 

@@ -300,7 +300,8 @@ class Engine:
         """Launch the sizing kernels for `batch` on the current stream (async)."""
         co = c_out if c_out is not None else self.c_outputs(out)
         if batch.nb_scan != getattr(self, "_nb_scan", True):
-            _lib.check(self.lib.dgen_set_nb_scan(self.ctx, int(batch.nb_scan)), "dgen_set_nb_scan")
+            _lib.check(self.lib.dgen_set_nb_scan(self.ctx, _lib.NB_CAPM if batch.nb_scan else 0),
+                       "dgen_set_nb_scan")
             self._nb_scan = batch.nb_scan
         _lib.check(self.lib.dgen_size_agents(self.ctx, ctypes.byref(self.tables),
                                              ctypes.byref(batch.c_agents), ctypes.byref(co),

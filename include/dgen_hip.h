@@ -256,6 +256,7 @@ int32_t dgen_prep_cfs(dgen_ctx* ctx, const int32_t* cfs, int64_t n_rows, double*
  *                                           4 f64 sums, 12 counts, 12 x 192
  *                                           mixed-hour entries of 24 B       */
 #define DGEN_NB_BYTES 59968
+#define DGEN_NB_CAPM 192     /* mixed hours per month a net-billing split record holds */
 size_t dgen_workspace_bytes(int64_t n, int64_t n_scratch);
 
 /* Size a batch: Brent over PV kW with 25-year bills + cash flow per
@@ -515,14 +516,18 @@ int32_t dgen_set_hourly_segment(dgen_ctx* ctx, int32_t months);
 int32_t dgen_set_battery(dgen_ctx* ctx, int32_t on);
 
 /* Where the battery case's net-billing split is built for agents that bill
- * net without a TS sell rate: 1 (default) in k_hourly_batt's scan, as the
- * system output is produced (k_batt_finance then bills from the record), or
- * 0 in k_batt_finance from the system-output plane.  Results are equal up to
- * the rounding of the re-associated sums.  The scan form pays its
- * classification in every wave that holds such an agent, so a batch where
- * few agents qualify is faster with 0 (the Python engine decides per batch:
- * Engine.upload_agents).  Replaces nothing in the reference.               */
-int32_t dgen_set_nb_scan(dgen_ctx* ctx, int32_t on);
+ * net without a TS sell rate: cap > 0 (default DGEN_NB_CAPM) in
+ * k_hourly_batt's scan, as the system output is produced, holding at most cap
+ * mixed hours per month -- k_batt_finance then bills from the record and the
+ * system-output plane is not written for agents without demand charges; an
+ * agent whose split overflows gets its plane from a repair pass and is billed
+ * as with 0 -- or 0: in k_batt_finance from the plane.  Results are equal up
+ * to the rounding of the re-associated sums (bit-identical for an overflowing
+ * agent).  The scan form pays its classification in every wave that holds
+ * such an agent, so a batch where few agents qualify is faster with 0 (the
+ * Python engine decides per batch: Engine.upload_agents).  Range
+ * [0, DGEN_NB_CAPM].  Replaces nothing in the reference.                   */
+int32_t dgen_set_nb_scan(dgen_ctx* ctx, int32_t cap);
 
 #ifdef __cplusplus
 }

@@ -250,3 +250,34 @@ def test_nb_scan_split_equals_finance_build(engine, cfg):
         assert np.array_equal(a[k], b[k], equal_nan=True), k
     for k in ("npv_pv_batt", "bill_w_batt", "bill_wo_batt", "cfev_batt"):
         assert np.allclose(a[k], b[k], rtol=1e-9, atol=1e-9, equal_nan=True), k
+
+
+def test_nb_scan_overflow_repair_pass(engine):
+    """A scan-built split that overflows its per-month capacity (forced here
+    with a capacity of 2 mixed hours) leaves no system-output plane behind;
+    the repair pass writes it and k_batt_finance bills exactly as with the
+    split built from the plane (bit-identical), every other output unchanged."""
+    from dgen_amd import _lib
+    pop = _small_pop("ca_res_storage", 400)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    res = []
+    try:
+        for on, cap in ((False, 0), (True, 2)):
+            batch.nb_scan = on
+            out = engine.alloc_outputs(batch.n, hourly=True)
+            engine.size(batch, out)                    # sets the engine's nb_scan state
+            _lib.check(engine.lib.dgen_set_nb_scan(engine.ctx, cap), "dgen_set_nb_scan")
+            engine.size(batch, out)
+            torch.cuda.synchronize()
+            res.append(outputs_to_host(out))
+    finally:
+        _lib.check(engine.lib.dgen_set_nb_scan(engine.ctx, _lib.NB_CAPM), "dgen_set_nb_scan")
+        engine._nb_scan = True
+        batch.nb_scan = True
+    a, b = res
+    for k, v in a.items():
+        if v is not None:
+            assert np.array_equal(v, b[k], equal_nan=True), k
