@@ -2321,7 +2321,10 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
             const double pad = __longlong_as_double((long long)lastp << 32);
             wave_lds_sync();
             col0[E * WAVE + dst] = g.sl < kn ? xL : 0.0;
-            col0[(E + 1) * WAVE + dst] = g.sl < kn ? xg : 0.0;
+            // the generation term at this evaluation's kW' (cf / 1e6 x kW', the
+            // same product every lane formed per entry; the battery case's system
+            // output as is), formed once by the staging lane
+            col0[(E + 1) * WAVE + dst] = g.sl < kn ? (sysg ? xg : xg * kws) : 0.0;
             col0[(E + 2) * WAVE + dst] = g.sl < kn ? xwp : pad;
             wave_lds_sync();
             if (j0 + LPA < n_m) fetch(m, j0 + LPA, n_m);
@@ -2347,8 +2350,7 @@ __device__ __forceinline__ double yl_bill_nb(const dgen_tariff& t, const YSrc& s
                         ci = S.at(p);
                         ce = S.at(half + p);
                     }
-                    const double gg = sysg ? eg : eg * kws;
-                    const double dd = eL - gg * s;
+                    const double dd = eL - eg * s;
                     ci += fmax(dd, 0.0);
                     double e = fmax(-dd, 0.0);
                     if constexpr (TSW) e *= (double)__int_as_float((int)(wpb & 0xffffffff));
