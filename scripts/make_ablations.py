@@ -140,6 +140,11 @@ VARIANTS = {
     # doubled: the occupancy cost alone) / without its mixed-entry stores
     "hb_nb_off": [("        put_nb = put_sys && mo2 && !ts_on;", "        put_nb = false && put_sys && mo2 && !ts_on;")],
     "hb_nb_nostore": [("                            nb_ent[n_m] = e;", "                            (void)e;")],
+    # per-agent kernels' block size (k_hourly_batt: waves per block)
+    "block64": [("constexpr int BLOCK = 128;", "constexpr int BLOCK = 64;"),
+                 ("__launch_bounds__(BLOCK, 2)\nk_hourly_batt(", "__launch_bounds__(BLOCK, 8)\nk_hourly_batt(")],
+    "block256": [("constexpr int BLOCK = 128;", "constexpr int BLOCK = 256;"),
+                 ("__launch_bounds__(BLOCK, 2)\nk_hourly_batt(", "__launch_bounds__(BLOCK, 1)\nk_hourly_batt(")],
     "ks_dc_occ1": [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)")],
     # k_batt_finance without its battery-case demand pass (what the rest costs)
     "kf_no_dem": [("            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);",
