@@ -97,15 +97,21 @@ def test_profile_order_is_invisible(engine, cfg, n):
         assert np.array_equal(a[k], b[k], equal_nan=True), k
 
 
-def test_pipeline_depth_is_invisible(engine):
+@pytest.mark.parametrize("cfg,nb_scan", [("national_mixed", None), ("national_mixed", True),
+                                         ("ca_res_storage", None)])
+def test_pipeline_depth_is_invisible(engine, cfg, nb_scan):
     """Chunking the batch across the two-stream pipeline (k_size of chunk j+1
     beside k_hourly_batt / k_batt_finance of chunk j) changes no output bit,
-    including a batch size that is not a multiple of the block size."""
-    pop = _small_pop("national_mixed", 3001)
+    including a batch size that is not a multiple of the block size; with the
+    battery-case split in k_batt_finance (national: few qualify) and in the
+    hourly scan (forced, and CA-like: all qualify)."""
+    pop = _small_pop(cfg, 3001)
     engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     engine.set_tariffs(pop.tariffs)
     engine.set_switches(pop.switches)
     batch = engine.upload_agents(pop.cols, pop.n_scratch)
+    if nb_scan is not None:
+        batch.nb_scan = nb_scan
     res = []
     engine.kernel_times()            # drain calls made by earlier tests
     try:
@@ -126,12 +132,14 @@ def test_pipeline_depth_is_invisible(engine):
                 assert np.array_equal(res[0][k], r[k], equal_nan=True), k
 
 
-def test_hourly_segment_is_invisible(engine):
+@pytest.mark.parametrize("cfg", ["national_mixed", "ca_res_storage"])
+def test_hourly_segment_is_invisible(engine, cfg):
     """Sweeping the year in month-segment launches of k_hourly_batt (SOC and
     the annual PV sum carried in the workspace) changes no output bit; mixed
-    population with net-billing (mo 2) agents and storage switches."""
+    population with net-billing (mo 2) agents and storage switches, and the
+    CA-like one whose battery-case split is built in the scan."""
     from dgen_amd import _lib
-    pop = _small_pop("national_mixed", 3001)
+    pop = _small_pop(cfg, 3001)
     engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     engine.set_tariffs(pop.tariffs)
     engine.set_switches(pop.switches)
