@@ -412,6 +412,12 @@ __host__ __device__ inline char* ws_nb(void* base, int64_t n, int64_t n_scratch)
 #ifndef DGEN_DAY_COUNTERS          // k_hourly_batt day-target counters (slots 12-15)
 #define DGEN_DAY_COUNTERS 0
 #endif
+// k_size's NEM phase timers use slots 12-15 unless the day counters do
+#if DGEN_DAY_COUNTERS
+#define PH_ADD_KS(k, v, lead) do {} while (0)
+#else
+#define PH_ADD_KS(k, v, lead) PH_ADD(k, v, lead)
+#endif
 #if DGEN_PHASE_PROF
 __device__ unsigned long long g_phase[16];
 #define PH_T0(v) const unsigned long long v = __builtin_readcyclecounter()
@@ -2566,7 +2572,7 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);
-        PH_ADD(12, tn, c.g.sl == 0);        // NEM set_tariff (bins + no-system bill)
+        PH_ADD_KS(12, tn, c.g.sl == 0);        // NEM set_tariff (bins + no-system bill)
     } else if constexpr (NET) {
         // net billing: the no-system bill from the load bins, then the split
         // of the search's hours for this tariff's periods
@@ -2608,7 +2614,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     if (!net_hourly(t)) {
         PH_T0(tn);
         wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
-        PH_ADD(13, tn, c.g.sl == 0);        // NEM evaluation bill
+        PH_ADD_KS(13, tn, c.g.sl == 0);        // NEM evaluation bill
     } else if constexpr (NET) {
         c.src.gen_scale = kws;
         PH_T0(te);
@@ -2640,7 +2646,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double ev = wo - w;
     PH_T0(tc);
     YFlow f = yl_cashflow(c.loan, total, ev, c.y, c.g, c.active);
-    PH_ADD(14, tc, c.g.sl == 0);            // cash flow + NPV + payback
+    PH_ADD_KS(14, tc, c.g.sl == 0);            // cash flow + NPV + payback
     c.last.total = total;
     c.last.ev = ev;
     c.last.w = w;
@@ -2758,7 +2764,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         c.tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
         c.thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
     }
-    PH_ADD(15, t_pro, sl == 0);             // prologue: agent loads, loan, bracket
+    PH_ADD_KS(15, t_pro, sl == 0);             // prologue: agent loads, loan, bracket
     PH_T0(t_all);
     yl_set_tariff<LPA, DC, NET>(c, t0);
     int nfev = 0;
