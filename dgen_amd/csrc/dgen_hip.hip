@@ -1741,6 +1741,17 @@ __device__ double yl_demand_staged(const dgen_demand* D, const YSrc& src, double
     const uint64_t segmask = LPA == WAVE ? ~0ull : (((1ull << LPA) - 1ull) << g.base);
     const uint64_t below = ((1ull << g.lane) - 1ull) & segmask;   // segment lanes before this one
     const int k0 = g.sl * HPL;
+    // Filter: an hour whose import cannot exceed the lowest running peak of
+    // its period among the segment's lanes changes no lane's peak, so it is
+    // not staged.  Its largest import over the lanes' factors is at the
+    // smallest or largest s of the segment (a line in s).
+    double s_mn = s, s_mx = s;
+#pragma unroll
+    for (int o = LPA / 2; o > 0; o >>= 1) {
+        const double a = __shfl_xor(s_mn, o, WAVE), b = __shfl_xor(s_mx, o, WAVE);
+        s_mn = a < s_mn ? a : s_mn;
+        s_mx = b > s_mx ? b : s_mx;
+    }
     double total = 0.0;
     for (int m = 0; m < 12; m++) {
         double flat = 0.0;
@@ -1760,6 +1771,28 @@ __device__ double yl_demand_staged(const dgen_demand* D, const YSrc& src, double
                 pv[u] = valid ? (pp < DCP ? pp : 0) : -1;
                 Lv[u] = (double)src.shape[hu] * src.load_scale;
                 gv[u] = with_gen ? src.sysgen[(int64_t)(hu >> 2) * src.sys_stride * 4 + (hu & 3)] : 0.0;
+            }
+            // the segment's lowest running peak per period; drop hours below it
+            double thr[DCP];
+#pragma unroll
+            for (int q = 0; q < DCP; q++) {
+                double v = S.at(q);
+#pragma unroll
+                for (int o = LPA / 2; o > 0; o >>= 1) {
+                    const double w = __shfl_xor(v, o, WAVE);
+                    v = w < v ? w : v;
+                }
+                thr[q] = v;
+            }
+#pragma unroll
+            for (int u = 0; u < HPL; u++) {
+                if (pv[u] >= 0) {
+                    double t_u = thr[0];
+#pragma unroll
+                    for (int q = 1; q < DCP; q++) t_u = pv[u] == q ? thr[q] : t_u;
+                    const double a = Lv[u] - gv[u] * s_mn, b = Lv[u] - gv[u] * s_mx;
+                    if (!((a > b ? a : b) > t_u)) pv[u] = -1;
+                }
             }
             wave_lds_sync();                          // previous batch fully read
             int base_q = 0;
