@@ -1757,21 +1757,36 @@ __device__ double yl_demand_staged(const dgen_demand* D, const YSrc& src, double
         double flat = 0.0;
         for (int q = 0; q < DCP; q++) S.at(q) = 0.0;
         const int h_lo = c_month_start_day[m] * 24, h_hi = c_month_start_day[m + 1] * 24;
+        // the batch's hours (load, system output, period), the next batch's
+        // loads issued before the current batch is processed
+        auto fetch = [&](int hb, double (&Lq)[HPL], double (&gq)[HPL], int (&pq)[HPL])
+            __attribute__((always_inline)) {
+            const int nb = (h_hi - hb) < DEM_BATCH ? (h_hi - hb) : DEM_BATCH;
+#pragma unroll
+            for (int u = 0; u < HPL; u++) {
+                const bool valid = hb < h_hi && k0 + u < nb;
+                const int hu = valid ? hb + k0 + u : h_lo;
+                const int d = hu / 24, hod = hu - d * 24;
+                const int pp = ((d % 7) >= 5) ? D->wkend[m][hod] : D->wkday[m][hod];
+                pq[u] = valid ? (pp < DCP ? pp : 0) : -1;
+                Lq[u] = (double)src.shape[hu] * src.load_scale;
+                gq[u] = with_gen ? src.sysgen[(int64_t)(hu >> 2) * src.sys_stride * 4 + (hu & 3)] : 0.0;
+            }
+        };
+        double nL[HPL], ng[HPL];
+        int np[HPL];
+        fetch(h_lo, nL, ng, np);
 #pragma unroll 1
         for (int hb = h_lo; hb < h_hi; hb += DEM_BATCH) {
-            const int nb = (h_hi - hb) < DEM_BATCH ? (h_hi - hb) : DEM_BATCH;
             double Lv[HPL], gv[HPL];
             int pv[HPL];
 #pragma unroll
             for (int u = 0; u < HPL; u++) {
-                const bool valid = k0 + u < nb;
-                const int hu = hb + (valid ? k0 + u : 0);
-                const int d = hu / 24, hod = hu - d * 24;
-                const int pp = ((d % 7) >= 5) ? D->wkend[m][hod] : D->wkday[m][hod];
-                pv[u] = valid ? (pp < DCP ? pp : 0) : -1;
-                Lv[u] = (double)src.shape[hu] * src.load_scale;
-                gv[u] = with_gen ? src.sysgen[(int64_t)(hu >> 2) * src.sys_stride * 4 + (hu & 3)] : 0.0;
+                Lv[u] = nL[u];
+                gv[u] = ng[u];
+                pv[u] = np[u];
             }
+            fetch(hb + DEM_BATCH, nL, ng, np);
             // the segment's lowest running peak per period; drop hours below it
             double thr[DCP];
 #pragma unroll
