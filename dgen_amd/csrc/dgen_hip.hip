@@ -1398,6 +1398,77 @@ __device__ __forceinline__ double yl_bill_nem(const dgen_tariff& t, const YLds& 
     return (t.P <= PREG) ? yl_bill_mo0_reg(t, S, gscale, yearend) : yl_bill_mo0(t, S, gscale, yearend);
 }
 
+// The no-system NEM bill (gscale 0): every month nets its load (>= 0), so no
+// kWh credit ever accrues and the months are independent -- lane m < 12 of
+// the segment bills month m with yl_bill_mo0_reg's arithmetic (credit 0),
+// then the months are added in order, the serial loop's sum.  A negative
+// bin (months then depend on each other) or P > PREG takes the serial bill.
+template <int LPA>
+__device__ __forceinline__ double yl_bill_nem_nosys(const dgen_tariff& t, const YLds& S, double yearend,
+                                                    const Seg<LPA>& g) {
+    if (t.mo != 0 || t.P > PREG) return yl_bill_nem(t, S, 0.0, yearend);
+    const int P = t.P, T = t.T, half = S.half;
+    const int m = g.sl < 12 ? g.sl : 11;
+    double b0[PREG], u[PREG], credit[PREG];
+    bool neg = false;
+#pragma unroll
+    for (int p = 0; p < PREG; p++) {
+        b0[p] = p < P ? t.buy[p][0] : 0.0;
+        u[p] = 0.0;
+        credit[p] = 0.0;
+        if (p < P) {
+            const double nn = S.L[m * half + p] - 0.0 * S.G[m * half + p];
+            const double use = nn < 0.0 ? nn : 0.0;
+            const double un = nn - use;
+            const double cn = 0.0 - use;
+            const bool pos = nn >= 0.0;
+            u[p] = pos ? un : 0.0;
+            credit[p] = pos ? cn : 0.0 + -nn;
+            neg = neg || !pos;
+        }
+    }
+    if (g.first(neg) >= 0) return yl_bill_nem(t, S, 0.0, yearend);
+    double U = 0.0;
+#pragma unroll
+    for (int p = 0; p < PREG; p++)
+        if (p < P) U += u[p];
+    double charge = 0.0;
+    if (U > 0.0) {
+        if (T == 1) {
+#pragma unroll
+            for (int p = 0; p < PREG; p++)
+                if (p < P) charge += u[p] * b0[p];
+        } else {
+            double fr[PREG];
+#pragma unroll
+            for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
+            const double scale = t.unit == 2 ? (double)c_days_in_month[m] : 1.0;
+            double prev = 0.0;
+            for (int k = 0; k < T; k++) {
+                double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
+                double top = U < hi ? U : hi;
+                double amt = top - prev;
+                if (amt < 0.0) amt = 0.0;
+                if (hi > prev) prev = hi;
+#pragma unroll
+                for (int p = 0; p < PREG; p++)
+                    if (p < P) charge += fr[p] * amt * (k == 0 ? b0[p] : t.buy[p][k]);
+            }
+        }
+    }
+    double bill = t.fixed + charge;
+    if (m == 11) {
+        double cc = 0.0;
+#pragma unroll
+        for (int p = 0; p < PREG; p++)
+            if (p < P) cc += credit[p];
+        bill -= cc * yearend;
+    }
+    double total = 0.0;
+    for (int mm = 0; mm < 12; mm++) total += __shfl(bill, g.base + mm, WAVE);
+    return total;
+}
+
 // Wave-uniform hourly source for net billing.
 struct YSrc {
     const float* shape;
@@ -2619,7 +2690,7 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
         PH_T0(tn);
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
-        c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);
+        c.wo1 = yl_bill_nem_nosys(t, c.S, c.yearend, c.g);
         PH_ADD_KS(12, tn, c.g.sl == 0);        // NEM set_tariff (bins + no-system bill)
     } else if constexpr (NET) {
         // net billing: the no-system bill from the load bins, then the split
@@ -2916,7 +2987,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             S.G[m * half + p] = b.y;
         }
         wave_lds_sync();
-        wo1 = same_tariff ? O.first_without[i] : yl_bill_nem(t, S, 0.0, cfg.nm_yearend_sell_rate);
+        wo1 = same_tariff ? O.first_without[i] : yl_bill_nem_nosys(t, S, cfg.nm_yearend_sell_rate, g);
         wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
     } else if constexpr (NET) {
         if (same_tariff) {

@@ -145,6 +145,12 @@ VARIANTS = {
                  ("__launch_bounds__(BLOCK, 2)\nk_hourly_batt(", "__launch_bounds__(BLOCK, 8)\nk_hourly_batt(")],
     "block256": [("constexpr int BLOCK = 128;", "constexpr int BLOCK = 256;"),
                  ("__launch_bounds__(BLOCK, 2)\nk_hourly_batt(", "__launch_bounds__(BLOCK, 1)\nk_hourly_batt(")],
+    # C3 k_size attribution: the NEM bins build's slot-sum loads replaced by
+    # a constant / the no-system bill skipped (results wrong by construction)
+    "ks_bins_const": [("                    lv[k] = lm[dt * 24 + h0 + k];\n                    gv[k] = gm[dt * 24 + h0 + k];",
+                       "                    lv[k] = 1.0 + (double)(size_t)lm * 0.0;\n                    gv[k] = 0.5 + (double)(size_t)gm * 0.0;")],
+    "ks_wo1_skip": [("        c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);\n        PH_ADD_KS(12",
+                     "        c.wo1 = 1000.0;\n        PH_ADD_KS(12")],
     "ks_dc_occ1": [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)")],
     # k_batt_finance without its battery-case demand pass (what the rest costs)
     "kf_no_dem": [("            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);",
