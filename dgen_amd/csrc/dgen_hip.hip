@@ -2511,6 +2511,19 @@ __device__ __forceinline__ double yl_bill_mo2_nogen(const dgen_tariff& t, const 
     return total;
 }
 
+// The same no-system bill month-parallel (year-independent): lane m < 12 of
+// the segment bills month m in its own LDS column, the months added in order.
+template <int LPA>
+__device__ __forceinline__ double yl_bill_mo2_nogen_par(const dgen_tariff& t, const YLds& S, const Seg<LPA>& g) {
+    const int P = t.P, half = S.half;
+    const int m = g.sl < 12 ? g.sl : 11;
+    for (int p = 0; p < P; p++) S.at(p) = S.L[m * half + p];
+    const double b = t.fixed + yl_month_charge(t, m, S, 0);
+    double total = 0.0;
+    for (int mm = 0; mm < 12; mm++) total += __shfl(b, g.base + mm, WAVE);
+    return total;
+}
+
 // bins of a tariff from a row's slot sums, one (month, period) cell per lane
 template <int LPA>
 __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double* __restrict__ lslots,
@@ -2697,7 +2710,7 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
         // of the search's hours for this tariff's periods
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
-        c.wo1 = yl_bill_mo2_nogen(t, c.S);
+        c.wo1 = yl_bill_mo2_nogen_par(t, c.S, c.g);
         PH_T0(tb);
         c.nb_ok = c.nb && (DGEN_NB_SERIAL ? yl_nb_build_serial(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g) : yl_nb_build<false>(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g));
         PH_ADD(1, tb, c.g.sl == 0);
@@ -2996,7 +3009,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             const int lr = A.load_row[i], cr = A.cf_row[i];
             yl_build_bins(t, T.shape_slots + (int64_t)lr * NSLOT, T.cf_slots + (int64_t)cr * NSLOT,
                           src.load_scale, S, g);
-            wo1 = yl_bill_mo2_nogen(t, S);
+            wo1 = yl_bill_mo2_nogen_par(t, S, g);
         }
         // the split of the battery-case hours over the lanes' degradation
         // factors [s_lo, s_hi] (the agent's net-billing record is free: its
