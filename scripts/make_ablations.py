@@ -151,6 +151,11 @@ VARIANTS = {
                        "                    lv[k] = 1.0 + (double)(size_t)lm * 0.0;\n                    gv[k] = 0.5 + (double)(size_t)gm * 0.0;")],
     "ks_wo1_skip": [("        c.wo1 = yl_bill_nem(t, c.S, 0.0, c.yearend);\n        PH_ADD_KS(12",
                      "        c.wo1 = 1000.0;\n        PH_ADD_KS(12")],
+    # NEM evaluation bill: months unrolled (ILP across months' tier charges)
+    "bill_unroll2": [("    double total = 0.0;\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn",
+                      "    double total = 0.0;\n#pragma unroll 2\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn")],
+    "bill_unroll4": [("    double total = 0.0;\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn",
+                      "    double total = 0.0;\n#pragma unroll 4\n    for (int m = 0; m < 12; m++) {\n#pragma unroll\n        for (int p = 0; p < PREG; p++) {\n            if (p < P) {\n                double nn")],
     "ks_dc_occ1": [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? (LPA == WAVE ? 2 : 1) : 3)")],
     # k_batt_finance without its battery-case demand pass (what the rest costs)
     "kf_no_dem": [("            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);",
