@@ -3817,7 +3817,11 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->nch[slot] = nch;
     // k_hourly_batt: per-period bins [P][BLOCK] double2 (x2 with the net-billing
     // split: import and export sums) + the waves' day buffers
-    const bool nb_scan = n_scratch > 0 && c->nb_scan && c->battery;
+    // (the scan form doubles the bins; kept within 64 KB of dynamic LDS per
+    // block, i.e. batches whose tariffs have at most 10 periods)
+    const size_t lds_nb = sizeof(double) * 4 * (size_t)lds_half(T->max_periods) * BLOCK +
+                          (size_t)(BLOCK / 64) * HB_DAY_BYTES;
+    const bool nb_scan = n_scratch > 0 && c->nb_scan && c->battery && lds_nb <= 65536;
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK * (nb_scan ? 2 : 1) +
                        (size_t)(BLOCK / 64) * HB_DAY_BYTES;
     // two agents per wave when every analysis period fits 32 lanes, unless the

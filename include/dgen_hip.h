@@ -525,8 +525,10 @@ int32_t dgen_set_battery(dgen_ctx* ctx, int32_t on);
  * to the rounding of the re-associated sums (bit-identical for an overflowing
  * agent).  The scan form pays its classification in every wave that holds
  * such an agent, so a batch where few agents qualify is faster with 0 (the
- * Python engine decides per batch: Engine.upload_agents).  Range
- * [0, DGEN_NB_CAPM].  Replaces nothing in the reference.                   */
+ * Python engine decides per batch: Engine.upload_agents).  Applies to
+ * batches whose tariffs have at most 10 periods (the scan form's doubled
+ * bins then fit 64 KB of LDS per block); others build in k_batt_finance.
+ * Range [0, DGEN_NB_CAPM].  Replaces nothing in the reference.            */
 int32_t dgen_set_nb_scan(dgen_ctx* ctx, int32_t cap);
 
 #ifdef __cplusplus
