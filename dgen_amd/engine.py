@@ -429,14 +429,17 @@ def _staging(k: int, nbytes: int):
     return t
 
 
-def hourly_to_host(t, inv=None, chunk: int = 4096, threads: int = 8) -> np.ndarray:
+def hourly_to_host(t, inv=None, chunk: int = 4096, threads: Optional[int] = None) -> np.ndarray:
     """One hour-quad-tiled plane [NH/4][n][4] -> host [n][NH] (caller order when
     `inv` gathers it): per chunk of agents, a device gather into agent-major
     order, an async copy into one of two pinned staging buffers, and host
     threads copying the previous chunk out into the destination while the
     next chunk crosses PCIe."""
     torch = _torch()
+    import os
     from concurrent.futures import ThreadPoolExecutor
+    if threads is None:
+        threads = int(os.environ.get("DGEN_D2H_THREADS", "8"))
     q, n, four = t.shape
     ncol = q * four
     rowb = ncol * t.element_size()
@@ -444,9 +447,9 @@ def hourly_to_host(t, inv=None, chunk: int = 4096, threads: int = 8) -> np.ndarr
     if n == 0:
         return dst
     chunk = max(1, min(chunk, n))
-    pool = _POOL.get("copy")
+    pool = _POOL.get(("copy", threads))
     if pool is None:
-        pool = _POOL["copy"] = ThreadPoolExecutor(threads, thread_name_prefix="dgen-d2h")
+        pool = _POOL[("copy", threads)] = ThreadPoolExecutor(threads, thread_name_prefix="dgen-d2h")
     tp = t.permute(1, 0, 2)
     pend = [[], []]
     for k, c0 in enumerate(range(0, n, chunk)):
