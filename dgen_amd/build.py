@@ -86,7 +86,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
             if attempt == 0:
                 first = {k: [b for b, _ in v] for k, v in hits.items()}
             # k_hourly_batt's counted next-day DMA wait must cover the DMA
-            dma_k, dma_issued = spill_guard.day_dma_wait(asm) or (0, 0)   # None: every wait drained
+            dma = spill_guard.day_dma_wait(asm)
+            if dma is None:
+                raise RuntimeError("k_hourly_batt: no next-day DMA group or counted read-back wait found "
+                                   "in the device assembly (the DMA-coverage check cannot see the loop)")
+            dma_k, dma_issued = (0, 0) if dma == spill_guard.DRAINED else dma
             if dma_issued < dma_k:
                 raise RuntimeError(f"k_hourly_batt: the day read-back waits vmcnt({dma_k}) but only "
                                    f"{dma_issued} vector-memory ops follow the next-day DMA on every path")

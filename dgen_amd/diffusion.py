@@ -178,7 +178,8 @@ def anchor_to_observed(eng, df: pd.DataFrame, observed: pd.DataFrame) -> pd.Data
     import torch
     group_cols = ['state_abbr', 'sector_abbr', 'year']
     n = len(df)
-    gid = df.groupby(group_cols, sort=False, dropna=True).ngroup().to_numpy(np.int64)
+    # ngroup() gives NaN (pandas 2.x) for a row whose key has a NaN: -1 here
+    gid = df.groupby(group_cols, sort=False, dropna=True).ngroup().fillna(-1).to_numpy(np.int64)
     ok = gid >= 0
     G = int(gid.max()) + 1 if ok.any() else 0
     order = np.argsort(np.where(ok, gid, G), kind="stable")[:int(ok.sum())]

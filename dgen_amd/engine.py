@@ -228,8 +228,14 @@ class Engine:
 
     def _nb_scan_pays(self, cols, n: int, n_scratch: int) -> bool:
         """dgen_set_nb_scan per batch: the scan-side split pays off when a large
-        share of the batch bills net without a TS sell rate (initial tariff;
-        the share is a cost heuristic only -- results do not depend on it)."""
+        share of the batch bills net without a TS sell rate (initial tariff).
+        The share is a cost heuristic, but the two split builds re-associate
+        the battery case's net-billing sums differently: npv_pv_batt,
+        bill_w_batt, bill_wo_batt and cfev_batt of such agents can differ by
+        about 1e-9 relative between the forms (every other output and every
+        discrete decision is identical; test_nb_scan_split_equals_finance_build),
+        so these four outputs depend on the batch composition (and on the
+        at-most-10-periods LDS gate) at that level."""
         import os
         force = os.environ.get("DGEN_NB_SCAN")          # "0" / "1" override the heuristic
         if force in ("0", "1"):
@@ -440,6 +446,7 @@ def hourly_to_host(t, inv=None, chunk: int = 4096, threads: Optional[int] = None
     from concurrent.futures import ThreadPoolExecutor
     if threads is None:
         threads = int(os.environ.get("DGEN_D2H_THREADS", "8"))
+    threads = max(1, int(threads))
     q, n, four = t.shape
     ncol = q * four
     rowb = ncol * t.element_size()

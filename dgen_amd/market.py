@@ -228,6 +228,21 @@ class YearTables:
         return out
 
 
+def financing_max_years(by_sector: np.ndarray, k_sector, year: int) -> int:
+    """Largest economic lifetime the agents (sector keys `k_sector`) gather
+    from a compiled year's by_sector table; the lifetimes and loan terms they
+    use must lie in [1, MAXY] (a merge miss is NaN and is rejected, as the
+    upload-time checks would reject it)."""
+    used = np.unique(np.asarray(k_sector, np.int64))
+    if used.size == 0:
+        return 0
+    terms = np.asarray(by_sector)[used][:, [5, 6]]
+    if not np.all(np.isfinite(terms)) or terms.min() < 1 or terms.max() > _lib.MAXY:
+        raise ValueError(f"financing terms for {year}: economic lifetime / loan term outside "
+                         f"[1, {_lib.MAXY}] or missing (merge miss)")
+    return int(terms[:, 0].max())
+
+
 class YearInputs:
     """Device side of YearTables: key codes and initial columns resident on the
     GPU, per-year tables uploaded (cached) and gathered by dgen_year_inputs."""
@@ -261,8 +276,17 @@ class YearInputs:
                              n_state_sector=len(self.yt.state_sectors),
                              n_county=len(self.yt.counties) if "wholesale_row" in keep else 0,
                              inflation_rate=self.yt.inflation_rate)
-            hit = self._years[year] = (tc, keep)
+            # the financing lifetimes this shard's agents gather: the sizing
+            # kernels pick their lanes-per-agent form from the batch maximum,
+            # so it is refreshed every year (a merge miss is NaN -> rejected)
+            max_years = financing_max_years(c["by_sector"], self.yt.k_sector, year)
+            hit = self._years[year] = (tc, keep, max_years)
         return hit[0]
+
+    def max_years(self, year: int) -> int:
+        """Largest economic lifetime any agent of the shard gathers in `year`."""
+        self._tables(year)
+        return self._years[year][2]
 
     def apply(self, year: int, cols: Dict[str, object], loop: Dict[str, object]):
         """Write year `year`'s attributes into the device agent columns `cols`

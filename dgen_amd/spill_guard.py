@@ -29,11 +29,18 @@ import re
 import sys
 
 SPILL = re.compile(r"^\s*(v_accvgpr_write_b32|scratch_store_\w+|buffer_store_\w+)\b")
+# register-to-register copies of a live value (live-range splits, AGPR
+# reloads, selects) in a join prologue write only the branch's lanes as well:
+# the same stale-lane hazard as a spill.  The current build has
+# none; phi copies sit at the end of the predecessor blocks, not here.
+COPY = re.compile(r"^\s*(v_mov_b(32|64)\w*\s+[va]\S*,\s*[va][\[\d]|v_cndmask_b32\w*|v_accvgpr_read_b32|"
+                  r"v_accvgpr_mov_b32)")
 RESTORE = re.compile(r"^\s*s_or_b64\s+exec,\s*exec,")
 LABEL = re.compile(r"^(\.LBB\w+|[A-Za-z_]\w*):")
 # instructions that may sit between a join block's label and its exec restore
-# without ending the prologue: scalar ops, SGPR lane spills, plain moves
-PASS = ("s_", "v_writelane", "v_readlane", "v_mov", "v_accvgpr_read", "v_cndmask")
+# without ending the prologue: scalar ops, SGPR lane spills, moves (a
+# VGPR / AGPR-sourced copy or select among them is itself a hit, COPY above)
+PASS = ("s_", "v_writelane", "v_readlane", "v_mov", "v_accvgpr_read", "v_accvgpr_mov", "v_cndmask")
 
 # 32-lane instantiations with a one-agent-per-wave fallback (compile macro)
 REMEDY = {
@@ -65,7 +72,7 @@ def scan(path):
                 continue
             if LABEL.match(t):
                 break
-            if SPILL.match(t):
+            if SPILL.match(t) or COPY.match(t):
                 spills.append(s)
             elif RESTORE.match(t):
                 if spills:
@@ -150,11 +157,15 @@ def day_dma_wait(path, kernel="k_hourly_battILb1E"):
     on the path that skips it; a path through another DMA group or a full
     drain, s_waitcnt vmcnt(0), ends there).
     Every instantiation whose symbol contains `kernel` is checked; returns the
-    (K, issued) pair with the smallest margin."""
+    (K, issued) pair with the smallest margin, DRAINED when DMA groups and
+    counted wait sites exist but every path between them drains (vmcnt(0)), and
+    None when no DMA group or no counted wait site was found at all (a symbol
+    change or a reordering the check no longer sees: the build fails then)."""
     import heapq
     lines = open(path).read().split("\n")
     starts = [i for i, l in enumerate(lines) if re.match(r"_Z\S*" + kernel + r"\S*:", l)]
     worst = None
+    seen_src = seen_wait = False
     for st in starts:
         en = next(i for i in range(st, len(lines)) if lines[i].strip().startswith(".Lfunc_end"))
         B = _blocks([l.strip() for l in lines[st + 1:en]])
@@ -164,6 +175,8 @@ def day_dma_wait(path, kernel="k_hourly_battILb1E"):
                  if ins[j].startswith("s_waitcnt") and "vmcnt(" in ins[j] and ins[j + 1].startswith("ds_read_b128")]
         srcs = [(k, max(j for j, l in enumerate(ins) if l.startswith(DMA)))
                 for k, (_, ins, _) in enumerate(B) if any(l.startswith(DMA) for l in ins)]
+        seen_src |= bool(srcs)
+        seen_wait |= any(K > 0 for _, _, K in waits)
         for kb, jd in srcs:
             # cost of entering block b from its top, up to a DMA or a full
             # drain s_waitcnt vmcnt(0) (either ends the path) or its end
@@ -196,7 +209,12 @@ def day_dma_wait(path, kernel="k_hourly_battILb1E"):
                 issued = dist[wb] + sum(bool(VMEM.match(l)) for l in pre)
                 if worst is None or issued - K < worst[1] - worst[0]:
                     worst = (K, issued)
+    if worst is None:
+        return DRAINED if (seen_src and seen_wait) else None
     return worst
+
+
+DRAINED = "drained"
 
 
 if __name__ == "__main__":

@@ -336,6 +336,10 @@ class YearLoop:
         """This year's elec.apply_* merges as device gathers (dgen_year_inputs)
         into the resident SoA columns and the loop's customers / load in bin."""
         self.year_inputs.apply(year, self.batch.cols, self.loop_cols)
+        # the year's lifetimes pick the sizing kernels' lanes-per-agent form
+        # (k_size / k_batt_finance treat years <= 32 as active in the two-agent
+        # form); the chunked export's sub-batches copy it from here
+        self.batch.c_agents.max_years = self.year_inputs.max_years(year)
 
     def initial_market(self):
         """First model year: elec.estimate_initial_market_shares (elec.py:701-765)
@@ -428,7 +432,7 @@ class YearLoop:
             ca = _lib.Agents(**{name: cols[name].data_ptr() for name, _ in _lib.AGENT_COLUMNS})
             ca.max_years = B.c_agents.max_years
             sub = AgentBatch(n=m, n_scratch=B.n_scratch, cols=cols, workspace=B.workspace,
-                             c_agents=ca)
+                             c_agents=ca, nb_scan=B.nb_scan)
             # prefixes of the chunk buffers: [m] scalars, [m][26] yearly, and the
             # first 8760*m floats of each plane viewed as [2190][m][4] tiles
             out = {k: v[:m] for k, v in self._chunk_out.items()}

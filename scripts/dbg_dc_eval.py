@@ -4,7 +4,7 @@ dc_dbg variant (scripts/make_ablations.py), read back its per-evaluation
 capture of agents 0-3 (kW', degradation factor, demand charge and energy bill
 of every year lane) and compare each lane with the oracle's Utilityrate5
 restatement at the same kW' -- energy bill and demand charge separately.
-Usage: DGEN_LIB=dgen_amd/lib/ablate/libdgen_dc_dbg.so dbg_dc_eval.py"""
+Usage: DGEN_LIB=ablate/libdgen_dc_dbg.so dbg_dc_eval.py"""
 import ctypes
 import os
 import sys

@@ -1,16 +1,17 @@
 #!/usr/bin/env python3
-"""Build kernel variants for A/B timing into dgen_amd/lib/ablate/ (diagnostic
-only: occupancy variants compute the same results, the no_* variants are
+"""Build kernel variants for A/B timing into ablate/ (outside the product
+library directory; diagnostic only: occupancy variants compute the same results, the no_* variants are
 wrong by construction).  Each variant is a text edit of a temporary copy of
 the source; nothing here is part of the product build.  Run a variant with
-DGEN_LIB=dgen_amd/lib/ablate/libdgen_<name>.so python bench.py ..."""
+DGEN_LIB=ablate/libdgen_<name>.so python bench.py ..., or scripts/gpu.sh ab.
+Delete ablate/ after the A/B: everything in the tree ships with every gpurun call."""
 import os
 import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "dgen_amd", "csrc", "dgen_hip.hip")
-OUT = os.path.join(REPO, "dgen_amd", "lib", "ablate")
+OUT = os.path.join(REPO, "ablate")
 sys.path.insert(0, REPO)
 from dgen_amd.build import FLAGS, hipcc  # noqa: E402
 

@@ -160,3 +160,40 @@ def test_two_state_shards_reproduce_one_pool(engine):
     for j in range(len(years)):
         assert np.array_equal(tot[j], full[j].totals.cpu().numpy()), years[j]
         assert np.allclose(hrs[j], full[j].hourly.cpu().numpy(), rtol=0, atol=0), years[j]
+
+
+def test_lifetime_raised_by_year_table_reaches_the_kernels(engine):
+    """A financing table that raises the economic lifetime from 25 to 40 in a
+    later model year: the loop refreshes the batch's max_years from the year's
+    gather, so the sizing kernels switch to one agent per wave and every agent
+    sizes over 40 years -- bit for bit what a fresh upload of the same
+    gathered columns gives (max_years was computed once)."""
+    import copy
+    pop = make_population("national_mixed", N, seed=20269002, n_res_shapes=64, n_com_shapes=32,
+                          n_cf=32, n_counties=16, n_tariffs=48)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    ag = loop_agents(pop, agent_id0=7)
+    tabs = copy.deepcopy(LoopTables.synthetic())
+    fin = tabs.inputs["financing"]
+    fin.loc[fin["year"] == 2027, "economic_lifetime_yrs"] = 40
+    loop = YearLoop(engine, pop, ag, tabs, first_year=2026, hourly_export=False)
+    loop.run_year(2026)
+    assert loop.batch.c_agents.max_years == 25
+    loop.run_year(2027)
+    assert loop.batch.c_agents.max_years == 40
+    assert (loop.out["status"].cpu().numpy() == 0).all()
+    assert (loop.batch.cols["econ_life"].cpu().numpy() == 40).all()
+    # the same gathered columns uploaded fresh (device order, no permutation)
+    cols = {k: v.cpu().numpy() for k, v in loop.batch.cols.items()}
+    fresh = engine.upload_agents(cols, n_scratch=loop.batch.n_scratch)
+    assert fresh.c_agents.max_years == 40
+    out = engine.alloc_outputs(N, hourly=False)
+    engine.size(fresh, out)
+    torch.cuda.synchronize()
+    for k in ("system_kw", "npv", "payback_period", "npv_pv_batt"):
+        assert np.array_equal(loop.out[k].cpu().numpy(), out[k].cpu().numpy(), equal_nan=True), k
+    # year 40's cash flow is live, year 41's is not
+    cf = loop.out["cash_flow"].cpu().numpy()
+    assert np.abs(cf[:, 40]).max() > 0 and not cf[:, 41:].any()

@@ -75,3 +75,30 @@ def test_kahan_group_sum_is_pandas():
     for g, s in ref.items():
         got, _ = om.group_sum_kahan(df.loc[df.g == g, "v"].tolist())
         assert got == s, g
+
+
+def test_financing_max_years_follows_the_year_and_rejects_misses():
+    """The per-year lifetimes pick the sizing kernels' lanes-per-agent form, so
+    the loop refreshes the batch maximum every year and refuses a merge miss
+    (NaN) or a lifetime outside [1, MAXY]."""
+    from dgen_amd.market import financing_max_years
+    from dgen_amd.year_loop import LoopTables
+    tabs = LoopTables.synthetic()
+    fin = tabs.inputs["financing"].copy()
+    fin.loc[(fin["year"] == 2027) & (fin["sector_abbr"] == "com"), "economic_lifetime_yrs"] = 40
+    t = dict(tabs.inputs, financing=fin)
+    frame = pd.DataFrame({"state_abbr": ["DE", "DE", "CA"], "sector_abbr": ["res", "com", "com"],
+                          "county_id": [0, 1, 2]})
+    yt = YearTables(frame, t, 0.025)
+    assert financing_max_years(yt.compile(2026)["by_sector"], yt.k_sector, 2026) == 25
+    assert financing_max_years(yt.compile(2027)["by_sector"], yt.k_sector, 2027) == 40
+    res_only = [k for k, s in zip(yt.k_sector, frame["sector_abbr"]) if s == "res"]
+    assert financing_max_years(yt.compile(2027)["by_sector"], res_only, 2027) == 25
+    bs = yt.compile(2027)["by_sector"].copy()
+    bs[:, 5] = np.nan
+    with pytest.raises(ValueError, match="merge miss"):
+        financing_max_years(bs, yt.k_sector, 2027)
+    bs = yt.compile(2027)["by_sector"].copy()
+    bs[:, 5] = 51
+    with pytest.raises(ValueError, match="outside"):
+        financing_max_years(bs, yt.k_sector, 2027)

@@ -101,4 +101,26 @@ def test_day_dma_wait_counts_unconditional_ops(tmp_path):
     assert G.day_dma_wait(str(p)) == (4, 4)
     # a full drain on the way (s_waitcnt vmcnt(0)) covers the wait by itself
     p.write_text(DMA.replace("STORES", "\ts_waitcnt vmcnt(0)\n"))
+    assert G.day_dma_wait(str(p)) == G.DRAINED
+    # no DMA group (or no counted wait) at all is not "drained": the build fails
+    p.write_text(DMA.replace("STORES", "").replace("global_load_lds_dwordx4", "global_load_dwordx4"))
     assert G.day_dma_wait(str(p)) is None
+    p.write_text(DMA.replace("STORES", "").replace("vmcnt(4)", "vmcnt(0)"))
+    assert G.day_dma_wait(str(p)) is None
+
+
+COPY = BAD.replace("\tv_accvgpr_write_b32 a12, v244\n", "\tv_mov_b32_e32 v10, v244\n") \
+          .replace("\tv_accvgpr_write_b32 a10, v242\n", "")
+
+
+def test_flags_vgpr_copy_before_exec_restore(tmp_path):
+    # a live-range-split copy ahead of the restore fills only the branch's lanes
+    hits = _scan(tmp_path, COPY)
+    (fn, blocks), = hits.items()
+    assert blocks[0][1] == ["v_mov_b32_e32 v10, v244"]
+    for ins in ("v_cndmask_b32_e64 v10, v1, v2, s[4:5]", "v_accvgpr_read_b32 v10, a3",
+                "v_mov_b64_e32 v[10:11], v[244:245]"):
+        assert _scan(tmp_path, COPY.replace("v_mov_b32_e32 v10, v244", ins)), ins
+    # constants and SGPR sources are not copies of a live VGPR value
+    for ins in ("v_mov_b32_e32 v10, 0", "v_mov_b32_e32 v10, s4", "v_mov_b64_e32 v[6:7], s[68:69]"):
+        assert _scan(tmp_path, COPY.replace("v_mov_b32_e32 v10, v244", ins)) == {}, ins
