@@ -251,8 +251,20 @@ def main():
     dom = max(kms, key=lambda k: kms[k])
     d = per_kernel[dom]
     nl = max(launches[dom], 1)
-    roof = {"bound": "hbm", "kernel": dom, "achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": d["hbm_frac"],
+    # the roofline follows the dominant kernel's limiter: k_hourly_batt streams
+    # its rows and hourly planes (HBM); the year-lane kernels (k_size,
+    # k_batt_finance) re-bill per evaluation from LDS / registers and are
+    # bound by fp64 VALU issue, so their line reports the PMC VALU-busy share
+    # of this workload (profiles/pmc/<workload>.json) with the HBM fraction
+    # kept as a secondary field
+    valu_bound = dom != "k_hourly_batt" and valu_busy.get(dom) is not None
+    if valu_bound:
+        head = {"bound": "valu", "kernel": dom, "achieved": valu_busy[dom], "peak": 1.0,
+                "unit": "VALU-busy fraction", "frac": valu_busy[dom]}
+    else:
+        head = {"bound": "hbm", "kernel": dom, "achieved": d["achieved_gbs"], "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": d["hbm_frac"]}
+    roof = {**head, "hbm_frac": d["hbm_frac"], "hbm_achieved_gbs": d["achieved_gbs"],
             # per launch, like rocprof's per-dispatch durations (bytes / launches)
             "traffic": (d["traffic_per_step"] / nl) if d["traffic_per_step"] is not None else None,
             "algorithmic_bytes_per_launch": nbytes[dom] / nl, "launches_per_step": nl,
@@ -263,8 +275,9 @@ def main():
             "valu_busy_frac": valu_busy.get(dom),
             "note": ("k_hourly_batt streams its rows and planes (HBM roofline) and is co-limited by fp64 "
                      "VALU (valu_busy_frac)" if dom == "k_hourly_batt"
-                     else f"{dom} is fp64-VALU / latency bound (the year lanes re-bill per evaluation): "
-                          "valu_busy_frac is its bound; the HBM fraction is reported for completeness")}
+                     else (f"{dom} is fp64-VALU / latency bound (the year lanes re-bill per evaluation): "
+                           "bound/frac are its PMC VALU-busy share; hbm_frac is secondary") if valu_bound
+                     else f"{dom}: no PMC summary for this workload, HBM fraction only")}
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:

@@ -21,6 +21,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -47,25 +49,51 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # one rank per GPU (RCCL); DGEN_DIST_BACKEND=gloo rehearses the N > 1 flow
+    # with several ranks on one GPU (device = LOCAL_RANK mod the visible GPUs)
+    backend = os.environ.get("DGEN_DIST_BACKEND", "nccl")
     if ws > 1:
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     from dgen_amd.engine import Engine
-    from dgen_amd.synth import make_population
-    from dgen_amd.synth import STATES
-    from dgen_amd.year_loop import LoopTables, YearLoop, loop_agents, rank_states
+    from dgen_amd.synth import STATE_HOUSEHOLDS_M, STATES, make_population
+    from dgen_amd.year_loop import LoopTables, YearLoop, loop_agents, population_work, rank_states
 
     t_setup = time.perf_counter()
     cnum = 1 if args.config == "de_res" else 5
-    pool = [STATES.index("DE")] if args.config == "de_res" else rank_states(rank, ws)
-    pop = make_population(args.config, args.agents, seed=20260000 + cnum + 7919 * rank, state_pool=pool)
+    n_global = args.agents * ws
+    if args.config == "de_res":
+        pool, n_rank, mix = [STATES.index("DE")], args.agents, "uniform"
+    else:
+        # national population with census state sizes; whole states per rank,
+        # balanced by predicted work: every rank derives the same
+        # partition from the same census sample, then generates its own states'
+        # agents (its share of the global population by households)
+        sample = make_population(args.config, 50_000, seed=20260000 + cnum, n_res_shapes=256,
+                                 n_com_shapes=128, n_cf=256, n_counties=64, n_tariffs=32,
+                                 state_mix="census")
+        sw = np.bincount(sample.state_ix.astype(np.int64), weights=population_work(sample),
+                         minlength=len(STATES))
+        del sample
+        pool = rank_states(rank, ws, state_work=sw)
+        hh = STATE_HOUSEHOLDS_M
+        n_rank = int(round(n_global * hh[pool].sum() / hh.sum())) if ws > 1 else args.agents
+        mix = "census"
+        part = [rank_states(r, ws, state_work=sw) for r in range(ws)]
+        part_load = [float(sw[p_].sum()) for p_ in part]
+    pop = make_population(args.config, n_rank, seed=20260000 + cnum + 7919 * rank, state_pool=pool,
+                          state_mix=mix)
     eng = Engine(local if ws > 1 else 0)
     if args.no_batt:
         eng.set_battery(False)
     eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     eng.set_tariffs(pop.tariffs)
     eng.set_switches(pop.switches)
-    loop = YearLoop(eng, pop, loop_agents(pop, agent_id0=rank * args.agents), LoopTables.synthetic(),
+    loop = YearLoop(eng, pop, loop_agents(pop, agent_id0=rank * 2 * args.agents), LoopTables.synthetic(),
                     first_year=args.first_year, hourly_export=not args.no_export,
                     hourly_chunk=args.hourly_chunk)
     del pop
@@ -84,17 +112,22 @@ def main():
     if ws > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    n_total = n_rank
     if ws > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=eng.dev)
+        dev = eng.dev if backend == "nccl" else "cpu"
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+        c = torch.tensor([float(n_rank)], dtype=torch.float64, device=dev)
+        dist.all_reduce(c)
+        n_total = int(c.item())
     ms_size, ms_hourly, ms_fin, cnt = eng.kernel_times()
     last = res[-1].totals.cpu().numpy()
     if rank == 0:
         line = {
             "metric": "agent-years/sec (national diffusion loop: sizing + diffusion + attachment "
                       "+ state export + RCCL totals)",
-            "value": args.agents * ws * len(years) / el, "unit": "agent-years/s", "n_gpus": ws,
+            "value": n_total * len(years) / el, "unit": "agent-years/s", "n_gpus": ws,
             "steps": len(years), "warmup": args.warmup, "ms_per_step": el / len(years) * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic national population (numpy PCG64; synthetic Bass / max-market-share "
@@ -102,7 +135,12 @@ def main():
             "config": {"workload": "national_loop" if args.config == "national_mixed" else f"{args.config}_loop",
                        "population": args.config, "year_step": args.step, "battery_run": not args.no_batt,
                        "agents_per_gpu": args.agents,
-                       "global_agents": args.agents * ws, "years": [years[0], years[-1]],
+                       "global_agents": n_total, "years": [years[0], years[-1]],
+                       "state_mix": mix,
+                       "rank_partition": (None if args.config == "de_res" else
+                                          {"states_per_rank": [len(p_) for p_ in part],
+                                           "predicted_work_max_over_mean":
+                                               max(part_load) / (sum(part_load) / len(part_load))}),
                        "state_export": not args.no_export, "hourly_chunk": args.hourly_chunk,
                        "parallelism": f"dp{ws} (whole states per rank; one all-reduce per year)"},
             "sizing_kernel_ms_per_call": {"k_size": ms_size, "k_hourly_batt": ms_hourly,

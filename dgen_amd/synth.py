@@ -172,13 +172,27 @@ STATES = ["AL", "AZ", "AR", "CA", "CO", "CT", "DE", "FL", "GA", "ID", "IL", "IN"
           "WV", "WI", "WY", "DC", "AK", "HI"]
 
 
+# Approximate households per state (millions, 2020 census order of magnitude),
+# STATES order: the "census" state mix of a national population, so that state
+# sizes are as uneven as the real ones (CA and TX together ~18 %, WY ~0.2 %).
+STATE_HOUSEHOLDS_M = np.array([
+    1.93, 2.74, 1.17, 13.30, 2.23, 1.40, 0.38, 8.23, 3.83, 0.66, 4.91, 2.62, 1.27, 1.13, 1.74,
+    1.74, 0.57, 2.23, 2.62, 3.98, 2.21, 1.11, 2.43, 0.43, 0.77, 1.13, 0.53, 3.27, 0.80, 7.42,
+    4.01, 0.32, 4.68, 1.49, 1.64, 5.11, 0.41, 1.96, 0.35, 2.63, 10.00, 1.03, 0.26, 3.15, 2.90,
+    0.73, 2.37, 0.23, 0.29, 0.25, 0.46])
+
+
 def make_population(config: str, n_agents: int, seed: Optional[int] = None,
                     n_res_shapes: int = 4096, n_com_shapes: int = 2048, n_cf: int = 2048,
                     n_counties: int = 3100, n_tariffs: int = 256,
-                    state_pool: Optional[np.ndarray] = None) -> Population:
+                    state_pool: Optional[np.ndarray] = None,
+                    state_mix: str = "uniform") -> Population:
     """Synthetic population of `config`.  `state_pool` (indices into
     STATES) restricts the agents' states, e.g. to the states one rank of the
-    model-year loop owns (year_loop.rank_states); CA agents take the NEM3 path."""
+    model-year loop owns (year_loop.rank_states); CA agents take the NEM3 path.
+    state_mix (mixed configs): "uniform" (every state equally likely, the
+    default stream) or "census" (states drawn in proportion to
+    STATE_HOUSEHOLDS_M, renormalised over the pool)."""
     if config not in CONFIGS:
         raise KeyError(f"unknown config {config!r}; one of {sorted(CONFIGS)}")
     cnum, sector, metering, _ = CONFIGS[config]
@@ -208,7 +222,14 @@ def make_population(config: str, n_agents: int, seed: Optional[int] = None,
         pool = np.arange(len(STATES)) if state_pool is None else np.asarray(state_pool, np.int64)
         if len(pool) == 0:
             raise ValueError("empty state pool")
-        state_ix = pool[rng.integers(0, len(pool), n)]
+        if state_mix == "census":
+            w = STATE_HOUSEHOLDS_M[pool]
+            state_ix = pool[np.minimum(np.searchsorted(np.cumsum(w / w.sum()), rng.random(n), side="right"),
+                                       len(pool) - 1)]
+        elif state_mix == "uniform":
+            state_ix = pool[rng.integers(0, len(pool), n)]
+        else:
+            raise ValueError(f"unknown state_mix {state_mix!r}")
         is_ca = state_ix == STATES.index("CA")
     else:
         is_ca = np.zeros(n, dtype=bool)

@@ -69,11 +69,61 @@ TOTAL_COLS = ["system_kw_cum", "batt_kw_cum", "batt_kwh_cum", "number_of_adopter
 LOOP_YEARS = (2022, 2050)       # the years the synthetic input tables cover
 
 
-def rank_states(rank: int, world: int, n_states: int = len(STATES)) -> np.ndarray:
-    """States owned by `rank`: s % world == rank (every state on exactly one
-    rank; whole states keep the attachment groups and state sums local)."""
+# Brent depth bound E as a function of L = load / naep (kW) with the optimum at
+# the bracket's bound (scipy 1.15.3 probes): the sizing work
+# of an agent is one hourly scan plus E objective evaluations
+E_BOUND_L = np.array([3.0, 5.0, 7.5, 10.0, 20.0, 50.0, 100.0, 200.0, 500.0, 1000.0, 4444.0])
+E_BOUND_E = np.array([1.0, 2.0, 2.0, 3.0, 4.0, 6.0, 8.0, 9.0, 11.0, 13.0, 16.0])
+# device cost of one evaluation relative to the agent's hourly scan (C3 at 1M:
+# k_size 9.3 ms over ~2.5 evaluations per agent vs k_hourly_batt 25 ms)
+EVAL_COST = 0.15
+
+
+def predicted_work(load_kwh, naep) -> np.ndarray:
+    """Predicted device work per agent: 1 (the 8760-h scan) + EVAL_COST x the
+    Brent-depth bound E(L), L = load_kwh / naep, interpolated in log L."""
+    L = np.asarray(load_kwh, np.float64) / np.maximum(np.asarray(naep, np.float64), 1e-9)
+    E = np.interp(np.log(np.maximum(L, 1e-12)), np.log(E_BOUND_L), E_BOUND_E)
+    return 1.0 + EVAL_COST * E
+
+
+def population_work(pop) -> np.ndarray:
+    """predicted_work of a synth.Population's agents (naep from its cf rows)."""
+    naep = np.asarray(pop.cfs, np.float64).sum(axis=1) / 1e6
+    return predicted_work(pop.cols["load_kwh"], naep[np.asarray(pop.cols["cf_row"], np.int64)])
+
+
+def balanced_states(state_work, world: int) -> List[np.ndarray]:
+    """Whole states onto `world` ranks, largest predicted work first, each to
+    the rank with the least work so far (ties: the lowest rank); every rank
+    computes the same assignment from the same weights.  Returns each rank's
+    states, ascending."""
+    w = np.asarray(state_work, np.float64)
+    if world < 1:
+        raise ValueError("bad world")
+    load = np.zeros(world)
+    owner = np.empty(w.size, np.int64)
+    for s in np.argsort(-w, kind="stable"):
+        r = int(np.argmin(load))
+        owner[s] = r
+        load[r] += w[s]
+    return [np.nonzero(owner == r)[0].astype(np.int64) for r in range(world)]
+
+
+def rank_states(rank: int, world: int, n_states: int = len(STATES),
+                state_work=None) -> np.ndarray:
+    """States owned by `rank` (every state on exactly one rank; whole states
+    keep the attachment groups and state sums local).  With `state_work`
+    (predicted work per state, e.g. the bincount of population_work over the
+    agents' states) the states are balanced by it
+    (balanced_states); without, s % world == rank."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError("bad rank / world")
+    if state_work is not None:
+        w = np.asarray(state_work, np.float64)
+        if w.size != n_states:
+            raise ValueError("state_work must have one entry per state")
+        return balanced_states(w, world)[rank]
     return np.arange(rank, n_states, world, dtype=np.int64)
 
 

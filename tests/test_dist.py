@@ -196,3 +196,80 @@ def test_bench_timed_region_max_over_ranks_gloo_world2():
     assert c0 == c1 == 3                      # exactly `steps` timed calls per rank
     assert el0 == el1                         # every rank reports the same (max) time
     assert el0 >= 3 * 0.08 * 0.95             # ... the slower rank's (3 x 80 ms)
+
+
+# ---------------------------------------------------------------------------
+# work-balanced state partition (whole states, balanced by the
+# predicted Brent depth E(L) per agent)
+# ---------------------------------------------------------------------------
+def _census_state_work(n=30_000, seed=11):
+    from dgen_amd.synth import STATES, make_population
+    from dgen_amd.year_loop import population_work
+    pop = make_population("national_mixed", n, seed=seed, n_res_shapes=64, n_com_shapes=32, n_cf=64,
+                          n_counties=16, n_tariffs=16, state_mix="census")
+    w = population_work(pop)
+    return np.bincount(pop.state_ix.astype(np.int64), weights=w, minlength=len(STATES)), pop, w
+
+
+def test_predicted_work_follows_the_brent_depth_table():
+    from dgen_amd.year_loop import E_BOUND_E, E_BOUND_L, EVAL_COST, predicted_work
+    assert np.allclose(predicted_work(E_BOUND_L * 1000.0, np.full(E_BOUND_L.size, 1000.0)),
+                       1.0 + EVAL_COST * E_BOUND_E)
+    w = predicted_work([1e3, 1e4, 1e6, 1e9], [1500.0] * 4)
+    assert np.all(np.diff(w) >= 0) and w[0] == 1.0 + EVAL_COST and w[-1] == 1.0 + EVAL_COST * 16
+
+
+def test_balanced_partition_of_census_states():
+    """LPT over whole states by predicted work: every state on one rank, and
+    max/mean rank load <= 1.1 for 2-8 ranks on census-sized states (CA and TX
+    are ~18 % of the households), where s % world leaves ranks idle."""
+    from dgen_amd.synth import STATES
+    from dgen_amd.year_loop import balanced_states, rank_states
+    sw, _, _ = _census_state_work()
+    for world in (1, 2, 3, 4, 8):
+        parts = balanced_states(sw, world)
+        assert sorted(np.concatenate(parts).tolist()) == list(range(len(STATES)))
+        for r in range(world):
+            assert np.array_equal(rank_states(r, world, state_work=sw), parts[r])
+        load = np.array([sw[p].sum() for p in parts])
+        assert load.max() / load.mean() <= 1.1, (world, load)
+    rr = np.array([sw[rank_states(r, 8)].sum() for r in range(8)])
+    assert rr.max() / rr.mean() > 1.3            # the round-robin split is what this replaces
+    with pytest.raises(ValueError):
+        rank_states(0, 2, state_work=sw[:10])
+
+
+def _balance_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dgen_amd.year_loop import rank_states
+    sw, pop, w = _census_state_work()          # every rank derives the same weights
+    mine = rank_states(rank, world, state_work=sw)
+    mask = np.isin(pop.state_ix.astype(np.int64), mine)
+    t = torch.zeros(world, dtype=torch.float64)
+    t[rank] = float(w[mask].sum())
+    n = torch.tensor([float(mask.sum())], dtype=torch.float64)
+    allreduce_sum(t)
+    allreduce_sum(n)
+    q.put((rank, t.numpy().tolist(), float(n.item()), mine.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_balanced_partition_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_balance_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (t, n, m)) for r, t, n, m in (q.get(timeout=180) for _ in procs))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (t0, n0, m0), (t1, n1, m1) = res[0], res[1]
+    assert t0 == t1 and n0 == n1 == 30_000          # all agents on exactly one rank
+    assert not set(m0) & set(m1)
+    load = np.array(t0)
+    assert load.max() / load.mean() <= 1.1, load

@@ -125,22 +125,26 @@ def test_chunked_hourly_export_matches_in_place(engine):
         assert torch.allclose(a.hourly, b.hourly, rtol=1e-12, atol=1e-9), y
 
 
-def test_two_state_shards_reproduce_one_pool(engine):
-    """Multi-GPU by construction: the two ranks' state shards (rank_states(r, 2))
-    run one after the other on this GPU reproduce the single-pool loop --
-    per-agent results bit for bit, per-state totals and hourly rows as the
-    all-reduce would merge them (states are disjoint across ranks)."""
+@pytest.mark.parametrize("world,balanced", [(2, False), (3, True)])
+def test_state_shards_reproduce_one_pool(engine, world, balanced):
+    """Multi-GPU by construction: the ranks' state shards (rank_states(r, world),
+    round robin or balanced by predicted work) run one after the other on this
+    GPU reproduce the single-pool loop -- per-agent results bit for bit,
+    per-state totals and hourly rows as the all-reduce would merge them
+    (states are disjoint across ranks)."""
     from dgen_amd.synth import subset
-    from dgen_amd.year_loop import rank_states
+    from dgen_amd.year_loop import population_work, rank_states
     pop, ag, tabs, whole = _setup(engine)
+    sw = (np.bincount(ag["state"], weights=population_work(pop), minlength=len(STATES))
+          if balanced else None)
     years = [2026, 2027]
     full = [whole.run_year(y, keep_per_agent=True) for y in years]
     full_out = {k: whole.out[k].cpu().numpy()[np.argsort(whole.perm)] for k in ("system_kw", "npv", "batt_kw")}
     tot = [np.zeros_like(r.totals.cpu().numpy()) for r in full]
     hrs = [np.zeros_like(r.hourly.cpu().numpy()) for r in full]
     seen = np.zeros(N, bool)
-    for rank in range(2):
-        mine = np.isin(ag["state"], rank_states(rank, 2))
+    for rank in range(world):
+        mine = np.isin(ag["state"], rank_states(rank, world, state_work=sw))
         idx = np.nonzero(mine)[0]
         seen |= mine
         sp = subset(pop, idx)
