@@ -110,6 +110,9 @@ def parse():
                     help="profile_order grouping: by (cf_row, load_row) or (load_row, cf_row)")
     ap.add_argument("--caller-order", action="store_true",
                     help="keep the generator's agent order on device (no profile_order grouping)")
+    ap.add_argument("--replan-hours", type=int, default=24, choices=[24, 1],
+                    help="peak-shaving re-plan interval: 24 = a plan per day, 1 = re-planned every hour "
+                         "over the next 24 h (DESIGN.md section 3)")
     ap.add_argument("--no-batt", action="store_true",
                     help="PV-only variant: no PV+battery forward run (SURVEY 8(d)); the reference always runs it")
     ap.add_argument("--pmc-dir", default=os.path.join(REPO, "profiles", "pmc"),
@@ -124,13 +127,13 @@ def dist_env():
     return ws, rank, local
 
 
-def cpu_baseline(pop, seconds: float, threads: int):
+def cpu_baseline(pop, seconds: float, threads: int, replan_hours: int = 24):
     """Time the CPU oracle ('port' of the reference semantics) on a bounded
     sample of the same workload (first agents of rank 0's shard)."""
     from oracle import oracle as orc
     from tests.helpers import oracle_population
     from dgen_amd.config import EngineConfig
-    cfg = orc.make_cfg(**EngineConfig().oracle_kwargs())
+    cfg = orc.make_cfg(**EngineConfig(batt_update_hours=replan_hours).oracle_kwargs())
     try:
         avail = len(os.sched_getaffinity(0))
     except Exception:
@@ -198,7 +201,8 @@ def main():
     pop = make_population(args.config, args.agents, seed=20260000 + 3 + 7919 * rank)
     # demand-charge configs run the extension mode; every other config the
     # reference's switch (SKIP_DEMAND_CHARGES = True, ff:35)
-    eng = Engine(local if ws > 1 else 0, EngineConfig(skip_demand_charges=pop.skip_demand_charges))
+    eng = Engine(local if ws > 1 else 0, EngineConfig(skip_demand_charges=pop.skip_demand_charges,
+                                                      batt_update_hours=args.replan_hours))
     if args.chunks is not None:
         eng.set_pipeline(args.chunks)
     if args.hb_months is not None:
@@ -282,7 +286,7 @@ def main():
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
         try:
-            cpu = cpu_baseline(pop, args.cpu_seconds, args.cpu_threads)
+            cpu = cpu_baseline(pop, args.cpu_seconds, args.cpu_threads, args.replan_hours)
         except Exception as e:  # the baseline never blocks the GPU number
             cpu = {"value": None, "unit": "agents/s", "cores": 0, "kind": "port",
                    "sample": f"unavailable: {type(e).__name__}: {e}"}
@@ -298,6 +302,7 @@ def main():
                        "hourly_outputs": not args.no_hourly,
                        "demand_charges": not pop.skip_demand_charges,
                        "battery_run": not args.no_batt,
+                       "battery_replan_hours": args.replan_hours,
                        "pipeline_chunks": eng.chunks, "hourly_months_per_launch": eng.hb_months,
                        "device_order": "caller" if args.caller_order else
                        ("profile (cf_row, load_row)" if args.order_major == "cf" else "profile (load_row, cf_row)"),

@@ -42,7 +42,7 @@ class Cfg(ctypes.Structure):
         ("itc_fed_max", _f64), ("depr_sl_years", _i32), ("pad0", _i32),
         ("batt_v_nom", _f64), ("batt_q_full", _f64), ("batt_min_soc", _f64),
         ("batt_max_soc", _f64), ("batt_init_soc", _f64), ("batt_eta_in", _f64),
-        ("batt_eta_out", _f64),
+        ("batt_eta_out", _f64), ("batt_update_hours", _i32), ("pad1", _i32),
     ]
 
 
@@ -53,7 +53,7 @@ class Tables(ctypes.Structure):
         ("wholesale", _vp), ("tariffs", _vp), ("switches", _vp),
         ("n_shapes", _i64), ("n_cfs", _i64), ("n_wholesale", _i64), ("n_switches", _i64),
         ("n_tariffs", _i32), ("max_periods", _i32),
-        ("demand", _vp), ("n_demand", _i32), ("pad", _i32),
+        ("demand", _vp), ("n_demand", _i32), ("peak_units", _i32),
     ]
 
 
@@ -101,7 +101,7 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
-ABI_VERSION = 6   # include/dgen_hip.h DGEN_ABI_VERSION
+ABI_VERSION = 7   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
 

@@ -215,11 +215,14 @@ class PopulationBuilder:
 
 def assign_scratch(cols: Dict[str, np.ndarray], tariffs: np.ndarray, switches: np.ndarray) -> int:
     """Give an hourly scratch slot to every agent whose battery-case tariff can
-    be net billing (mo 2) or carry demand charges (both bill hourly imports):
-    its initial tariff or any rate-switch candidate."""
+    be net billing (mo 2), carry demand charges (both bill hourly imports) or
+    bill its tiers in kWh/kW (month peaks): its initial tariff or any
+    rate-switch candidate."""
     n = len(cols["load_kwh"])
     # net billing (metering options 2 and 3) bills hourly imports
-    mo2 = ((tariffs["mo"] == 2) | (tariffs["mo"] == 3) | (tariffs["dc"] > 0)) if tariffs.size else np.zeros(0, bool)
+    # kWh/kW tier units (codes 1, 3) need the battery case's month peaks: the plane too
+    mo2 = ((tariffs["mo"] == 2) | (tariffs["mo"] == 3) | (tariffs["dc"] > 0) | (tariffs["unit"] == 1) |
+           (tariffs["unit"] == 3)) if tariffs.size else np.zeros(0, bool)
     need = mo2[cols["tariff0"]] if n else np.zeros(0, bool)
     if switches.size:
         sw_mo2 = mo2[switches["tariff"]]

@@ -31,10 +31,13 @@ class EngineConfig:
     batt_init_soc: float = 0.30         # ff:151
     batt_eta_in: float = 0.9408         # AC->DC 0.96 x cell 0.98
     batt_eta_out: float = 0.9408        # cell 0.98 x DC->AC 0.96
+    batt_update_hours: int = 24         # peak-shaving re-plan interval (24: a 24-h plan
+                                        # per calendar day; 1: re-planned every hour,
+                                        # bdh:86-87 read literally)
 
     def to_c(self) -> _lib.Cfg:
         d = asdict(self)
-        return _lib.Cfg(pad0=0, **d)
+        return _lib.Cfg(pad0=0, pad1=0, **d)
 
     def oracle_kwargs(self) -> dict:
         d = asdict(self)

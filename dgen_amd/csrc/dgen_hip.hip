@@ -50,6 +50,12 @@
 #ifndef DGEN_NO2_FIN_DC
 #define DGEN_NO2_FIN_DC 0
 #endif
+#ifndef DGEN_NO2_SIZE_PK
+#define DGEN_NO2_SIZE_PK 0
+#endif
+#ifndef DGEN_NO2_FIN_PK
+#define DGEN_NO2_FIN_PK 0
+#endif
 
 namespace {
 
@@ -281,6 +287,14 @@ __device__ __forceinline__ const dgen_demand* tariff_demand(const dgen_demand* t
 __device__ __forceinline__ const dgen_demand* tariff_demand(const dgen_tables& T, const dgen_cfg& cfg,
                                                             const dgen_tariff& t) {
     return tariff_demand(T.demand, T.n_demand, cfg.skip_demand_charges == 0, t);
+}
+// kWh/kW tier units (codes 1, 3): the caps scale with the month's peak import,
+// which the demand machinery computes from the record `dc` points to (its flat
+// peak), in either mode; its charges count only when demand charges are billed
+__device__ __forceinline__ bool peak_unit(const dgen_tariff& t) { return t.unit == 1 || t.unit == 3; }
+__device__ __forceinline__ const dgen_demand* tariff_peaks(const dgen_demand* table, int n_demand,
+                                                           const dgen_tariff& t) {
+    return peak_unit(t) ? tariff_demand(table, n_demand, true, t) : nullptr;
 }
 
 __device__ __forceinline__ double rate_switch(const dgen_switch* rows, int cnt, double size,
@@ -744,8 +758,23 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 // battery case's net-billing split (below) for the agents that bill net
 // without a TS sell rate, so k_batt_finance bills them without a pass over
 // the system-output plane.
-template <bool HOURLY, bool F64, bool NB>
-__global__ void __launch_bounds__(BLOCK, 2)
+// ROLL: the peak-shaving target is re-planned every hour over the next 24
+// hours (dgen_cfg.batt_update_hours = 1) instead of once per calendar day.
+// The window's deficits live in 24 registers (win) indexed by hour of day: at a
+// day's start they are that day's; after hour hh is dispatched, slot hh takes
+// tomorrow's hour hh (the window is a set, its order does not matter), read
+// from the LDS day buffer, which in this form holds TOMORROW during the day
+// (its DMA is waited for at the day's start).  In an hour where some lane can
+// discharge, the wave sorts a copy of the window and runs the same target
+// rule as the daily form -- the oracle's day_target over hours h .. h + 23,
+// wrapping past December 31 to January 1.  The hour loop is unrolled like the
+// daily form's (a rolled loop indexes the hour's registers dynamically, and
+// the compiler then keeps the window and both days in scratch: 592 B per
+// lane), so the network appears once per hour of the day (~27k instructions),
+// and the form runs one wave per SIMD: the window, its sorted copy and both
+// days' raw values need ~400 registers.
+template <bool HOURLY, bool F64, bool NB, bool ROLL>
+__global__ void __launch_bounds__(BLOCK, ROLL ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
               int repair) {
@@ -800,7 +829,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const int slot = A.scratch_slot[i];
     // the battery-case bill reads the hourly system output for net billing and
     // for demand charges (both need hourly imports, not bins)
-    const bool has_dc = tariff_demand(T, cfg, t) != nullptr;
+    const bool has_dc = tariff_demand(T, cfg, t) != nullptr ||
+                        tariff_peaks(T.demand, T.n_demand, t) != nullptr;   // kWh/kW tiers: peaks
     const bool need_sys = mo2 || has_dc;
     const bool put_sys = need_sys && slot >= 0 && batt_on;
     int status = O.status[i] | t.flags;
@@ -901,6 +931,10 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     day_dma(d_lo);
     const int d_last = c_month_start_day[m_hi] - 1;
     DayRaw r;
+    DayRaw r2;                     // ROLL: tomorrow's raw values
+    double win[24];                // ROLL: the 24-hour window's deficits by hour of day
+    (void)r2;
+    (void)win;
     double2* const bins2 = bins + (size_t)lds_half(T.max_periods) * BLOCK;   // NB: export sums
     for (int m = m_lo; m < m_hi; m++) {
         for (int p = 0; p < P; p++) bins[p * BLOCK] = make_double2(0.0, 0.0);
@@ -926,13 +960,22 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             swe[0] = b[0]; swe[1] = b[1]; swe[2] = b[2];
         }
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
-            if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);
+            if (ROLL && d > d_lo) day_reread(dlane, r);    // the DMA was waited for yesterday
+            else if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);
             else day_read<0>(dlane, r);
             const bool wkend = (d % 7) >= 5;
             const uint64_t sched[3] = {wkend ? swe[0] : swd[0], wkend ? swe[1] : swd[1],
                                        wkend ? swe[2] : swd[2]};
             double target = 0.0;
-            if (has_batt) {
+            if constexpr (ROLL) {
+                // the window at the day's first hour is the day itself; then the
+                // day after (January 1 after December 31) comes in as it is read
+#pragma unroll
+                for (int hh = 0; hh < 24; hh++)
+                    win[hh] = fmax((double)r.s[hh] * ls - (double)r.c[hh] * cs6, 0.0);
+                day_dma(d + 1 < 365 ? d + 1 : 0);
+                day_read<0>(dlane, r2);                    // vmcnt(0): tomorrow has landed
+            } else if (has_batt) {
                 // the day's deficits d_h = max(load_h - pv_h, 0), sorted; the raw
                 // registers are dead meanwhile and re-read from the LDS buffer
                 double dv[24];
@@ -964,7 +1007,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
 #endif
                 day_reread(dlane, r);
             }
-            if (d < d_last) day_dma(d + 1);                     // after the last read of the buffer
+            if (!ROLL && d < d_last) day_dma(d + 1);            // after the last read of the buffer
             const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);
 #pragma unroll
             for (int hh = 0; hh < 24; hh++) {
@@ -974,8 +1017,26 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 annual += pl;
                 const double pv = cfv * cs2;                 // battery run (kW*)
                 const double nn = ld - pv;
+                if constexpr (ROLL) {
+                    // this hour's plan over hours h .. h + 23, from the energy
+                    // stored now; only an hour that can discharge needs one
+                    // (elsewhere the dispatch is the same for any target)
+                    const double av = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
+                    const bool need = has_batt && nn > 0.0 && av > 0.0;
+                    target = 0.0;
+                    if (__ballot(need)) {
+                        double dv[24];
+#pragma unroll
+                        for (int k = 0; k < 24; k++) dv[k] = win[k];
+                        sort24_desc(dv);
+                        const double t = day_target_sorted(dv, power, av);
+                        target = need ? t : 0.0;
+                    }
+                }
                 HourStep st = batt_hour(nn, pv, target, power, bank, soc, cfg, inv_eta_in,
                                         in_per_bank, out_per_bank);
+                if constexpr (ROLL)     // the window moves on: tomorrow's hour hh comes in
+                    win[hh] = fmax((double)r2.s[hh] * ls - (double)r2.c[hh] * cs6, 0.0);
                 if constexpr (HOURLY) {
                     const double dn = ld - pl;
                     qb[hh & 3] = (PT)ld;
@@ -1149,25 +1210,29 @@ __device__ __forceinline__ void wave_lds_sync() {
 //   tariff [WAVE / LPA][dgen_tariff]                 (LPA < WAVE: staged copy, see stage_tariff)
 //   bins  [WAVE / LPA][L[12 * half], G[12 * half]]  (segment-uniform, broadcast reads)
 //   lane  [4 * half][WAVE]                          (per-lane per-period state)
+//   peaks [12][WAVE]                                (dgen_tables.peak_units only:
+//                                                   the lane's month peaks, kWh/kW tiers)
 struct YLds {
     dgen_tariff* trf;   // the segment's staged tariff (LPA < WAVE only)
     double* L;
     double* G;
     double* lane;   // lane column base (already offset by lane)
+    double* pk;     // the lane's month peak imports (stride WAVE), or nullptr
     int half;
     __device__ double& at(int k) const { return lane[k * WAVE]; }
 };
+constexpr int PK_SLOTS = 12;
 
 static_assert(sizeof(dgen_tariff) % sizeof(double) == 0, "tariff staging copies qwords");
 constexpr int TRF_QW = (int)(sizeof(dgen_tariff) / sizeof(double));
 
-__host__ __device__ inline size_t ylds_bytes(int half, int lpa) {
+__host__ __device__ inline size_t ylds_bytes(int half, int lpa, bool pk) {
     const size_t trf = lpa < WAVE ? (size_t)(WAVE / lpa) * sizeof(dgen_tariff) : 0;
-    return trf + sizeof(double) * ((size_t)24 * half * (WAVE / lpa) + (size_t)4 * half * WAVE);
+    return trf + sizeof(double) * ((size_t)24 * half * (WAVE / lpa) + (size_t)(4 * half + (pk ? PK_SLOTS : 0)) * WAVE);
 }
 
 template <int LPA>
-__device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>& g) {
+__device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>& g, bool pk) {
     YLds y;
     y.trf = nullptr;
     if (LPA < WAVE) {
@@ -1177,6 +1242,7 @@ __device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>
     y.L = base + (LPA == WAVE ? 0 : (g.lane / LPA) * 24 * half);
     y.G = y.L + 12 * half;
     y.lane = base + (WAVE / LPA) * 24 * half + g.lane;
+    y.pk = pk ? y.lane + 4 * half * WAVE : nullptr;
     y.half = half;
     return y;
 }
@@ -1213,6 +1279,19 @@ __device__ __forceinline__ const dgen_tariff* stage_tariff(const dgen_tariff* sr
     }
 }
 
+// Tier-cap scale of month m by usage unit (oracle/orc.c month_energy_charge):
+// 0 kWh: 1, 2 kWh daily: days, 1 kWh/kW: the month's peak import (kW), 3 kWh/kW
+// daily: peak x days -- pk: the lane's month peaks (stride WAVE), written by
+// the demand pass ahead of the bill (units 1 / 3 only).
+__device__ __forceinline__ double tier_scale(const dgen_tariff& t, int m, const double* pk) {
+    // the kernels without peak slots (pk a constant nullptr) keep units 0 / 2
+    // only: a kWh/kW tariff never bills there (DGEN_ST_UNIT)
+    if (!pk) return (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
+    const double a = (t.unit & 1) ? pk[m * WAVE] : 1.0;
+    const double b = (t.unit & 2) ? (double)c_days_in_month[m] : 1.0;
+    return a * b;
+}
+
 // month energy charge from the lane's billed kWh u_p = at(uoff + p)
 __device__ __forceinline__ double yl_month_charge(const dgen_tariff& t, int m, const YLds& S, int uoff) {
     const int P = t.P, T = t.T;
@@ -1224,7 +1303,7 @@ __device__ __forceinline__ double yl_month_charge(const dgen_tariff& t, int m, c
         for (int p = 0; p < P; p++) charge += S.at(uoff + p) * t.buy[p][0];
         return charge;
     }
-    double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
+    double scale = tier_scale(t, m, S.pk);
     double charge = 0.0, prev = 0.0;
     for (int k = 0; k < T; k++) {
         double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
@@ -1325,7 +1404,6 @@ __device__ __forceinline__ double yl_bill_mo0_reg(const dgen_tariff& t, const YL
                                                   double yearend) {
     const int P = t.P, T = t.T, half = S.half;
     const double fixed = t.fixed;
-    const bool daily = t.unit == 2;
     // first-tier prices in registers (every month reads them)
     double b0[PREG];
 #pragma unroll
@@ -1365,7 +1443,7 @@ __device__ __forceinline__ double yl_bill_mo0_reg(const dgen_tariff& t, const YL
                 double fr[PREG];
 #pragma unroll
                 for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
-                const double scale = daily ? (double)c_days_in_month[m] : 1.0;
+                const double scale = tier_scale(t, m, S.pk);
                 double prev = 0.0;
                 for (int k = 0; k < T; k++) {
                     double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
@@ -1442,7 +1520,7 @@ __device__ __forceinline__ double yl_bill_nem_nosys(const dgen_tariff& t, const 
             double fr[PREG];
 #pragma unroll
             for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
-            const double scale = t.unit == 2 ? (double)c_days_in_month[m] : 1.0;
+            const double scale = tier_scale(t, m, S.pk);
             double prev = 0.0;
             for (int k = 0; k < T; k++) {
                 double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
@@ -1490,7 +1568,8 @@ __device__ __forceinline__ void sys_quad(const YSrc& src, int h, double* g) {
 
 // Month energy charge from register-held billed kWh (P <= PREG), the same
 // arithmetic and order as yl_month_charge.
-__device__ __forceinline__ double reg_month_charge(const dgen_tariff& t, int m, const double (&u)[PREG]) {
+__device__ __forceinline__ double reg_month_charge(const dgen_tariff& t, int m, const double (&u)[PREG],
+                                                   const double* pk) {
     const int P = t.P, T = t.T;
     double U = 0.0;
 #pragma unroll
@@ -1507,7 +1586,7 @@ __device__ __forceinline__ double reg_month_charge(const dgen_tariff& t, int m, 
     double fr[PREG];
 #pragma unroll
     for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
-    const double scale = (t.unit == 2) ? (double)c_days_in_month[m] : 1.0;
+    const double scale = tier_scale(t, m, pk);
     double prev = 0.0;
     for (int k = 0; k < T; k++) {
         double hi = (k == T - 1) ? INFINITY : t.cap[k] * scale;
@@ -1530,7 +1609,7 @@ __device__ __forceinline__ double reg_month_charge(const dgen_tariff& t, int m, 
 // others adding an exact +0.0 -- the same sums in the same hour order.
 constexpr int MO2_CH = 8;
 __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YSrc& src, double s,
-                                                  bool with_gen) {
+                                                  bool with_gen, const double* pk) {
     const int P = t.P;
     double total = 0.0, carry = 0.0;
     int h = 0;
@@ -1593,7 +1672,7 @@ __device__ __forceinline__ double yl_bill_mo2_reg(const dgen_tariff& t, const YS
 #pragma unroll
         for (int p = 0; p < PREG; p++)
             if (p < P) cr += src.ts ? exv[p] : exv[p] * t.sell[p][0];
-        total += nb_month(t, reg_month_charge(t, m, imp), cr, carry);
+        total += nb_month(t, reg_month_charge(t, m, imp, pk), cr, carry);
     }
     return total;
 }
@@ -1695,7 +1774,7 @@ __device__ __forceinline__ double yl_bill_mo2(const dgen_tariff& t, const YSrc& 
 // version's chunk buffers push its 168-VGPR budget into spills, measured slower)
 __device__ __forceinline__ double yl_bill_net(const dgen_tariff& t, const YSrc& src, double s,
                                               bool with_gen, const YLds& S) {
-    return (t.P <= PREG) ? yl_bill_mo2_reg(t, src, s, with_gen) : yl_bill_mo2(t, src, s, with_gen, S);
+    return (t.P <= PREG) ? yl_bill_mo2_reg(t, src, s, with_gen, S.pk) : yl_bill_mo2(t, src, s, with_gen, S);
 }
 
 // ---------------------------------------------------------------------------
@@ -1780,6 +1859,7 @@ __device__ __forceinline__ double yl_demand(const dgen_demand* D, const YSrc& sr
                 }
             }
         }
+        if (S.pk) S.pk[m * WAVE] = flat;          // the month's peak import (kWh/kW tiers)
         double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
         for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
         total += c;
@@ -1918,6 +1998,7 @@ __device__ double yl_demand_staged(const dgen_demand* D, const YSrc& src, double
                 pk = mx > pk ? mx : pk;
             }
         }
+        if (S.pk) S.pk[m * WAVE] = flat;          // the month's peak import (kWh/kW tiers)
         double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
         for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
         total += c;
@@ -2061,6 +2142,7 @@ __device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& 
             S.at(q) = pk;
             flat = pk > flat ? pk : flat;
         }
+        if (S.pk) S.pk[m * WAVE] = flat;          // the month's peak import (kWh/kW tiers)
         double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
         for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
         total += c;
@@ -2661,8 +2743,11 @@ struct YCtx {
     const dgen_tariff* tp;      // current tariff (global record or LDS copy)
     const dgen_switch* sw_rows;
     const dgen_demand* dem_table;
-    const dgen_demand* dem;     // current tariff's demand charges (or nullptr)
+    const dgen_demand* dem;     // current tariff's demand record (charges, or the peaks of kWh/kW tiers)
     int n_dem;
+    bool dc_on;                 // demand charges billed (extension mode)
+    bool dem_bill;              // the record's charges count (dc_on and the tariff's own record)
+    bool pk13;                  // kWh/kW tiers: the demand pass runs ahead of the energy bill
     bool dem_wo_pending;        // wo1 still lacks the new tariff's demand charge
     bool env_ok;                // the demand envelopes of the current tariff fit
     DcEnv env;                  // the agent's envelope storage
@@ -2691,7 +2776,7 @@ struct YCtx {
 // NEM-only instantiation compiles the net-billing paths out, so the common
 // case's register allocation does not carry them (an agent that would still
 // reach one flags DGEN_ST_SCRATCH, which assign_scratch rules out).
-template <int LPA, bool DC, bool NET>
+template <int LPA, bool DC, bool NET, bool PK>
 __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
     c.tp = stage_tariff(c.tariffs + tix, c.S, c.g);
     const dgen_tariff& t = *c.tp;
@@ -2699,6 +2784,30 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
     c.status |= t.flags;
     // the 8760 TS sell rate applies under net billing option 2 only (ff:626-641)
     c.src.ts = (t.mo == 2) ? c.ts_row : nullptr;
+    double wo_dem = 0.0;
+    if constexpr (DC && !PK) {   // launched only with demand charges billed
+        c.dem = tariff_demand(c.dem_table, c.n_dem, true, t);
+        c.dem_wo_pending = c.dem != nullptr;
+    } else if constexpr (PK) {
+        const dgen_demand* bill = tariff_demand(c.dem_table, c.n_dem, c.dc_on, t);
+        c.pk13 = peak_unit(t);
+        c.dem = c.pk13 ? tariff_peaks(c.dem_table, c.n_dem, t) : bill;
+        c.dem_bill = bill != nullptr;
+        c.dem_wo_pending = c.dem != nullptr;
+        if (c.pk13 && (!c.dem || !c.S.pk)) c.status |= DGEN_ST_UNIT;
+        if (c.pk13 && c.dem && c.S.pk) {
+            // kWh/kW tiers: the month peaks come before the energy bills, so
+            // the envelopes are built and the no-system pass runs here (its
+            // charge, when billed, joins the no-system bill below)
+            c.env_ok = c.env.lines && yl_dc_build(c.dem, c.src, c.tlo, c.thi, c.env, c.g);
+            const double v0 = c.env_ok ? yl_dc_eval(c.dem, c.env, 0.0, 1.0, false, c.S)
+                                       : yl_demand(c.dem, c.src, 0.0, 1.0, false, c.S);
+            wo_dem = c.dem_bill ? v0 : 0.0;
+            c.dem_wo_pending = false;
+        }
+    } else {
+        if (peak_unit(t)) c.status |= DGEN_ST_UNIT;   // no peaks without the demand machinery
+    }
     if (!net_hourly(t)) {
         PH_T0(tn);
         wave_lds_sync();
@@ -2719,16 +2828,14 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
         c.status |= DGEN_ST_SCRATCH;
         c.wo1 = NAN;
     }
-    if constexpr (DC) {   // its no-system charge is added by the next objective
-        c.dem = tariff_demand(c.dem_table, c.n_dem, true, t);
-        c.dem_wo_pending = c.dem != nullptr;
-    }
+    // other tariffs' no-system demand charge is added by the next objective
+    c.wo1 += wo_dem;
 }
 
 // calc_system_performance(kw, en_batt=False) with lanes = years; returns -NPV
 // (wave-uniform).  Every evaluation leaves its per-lane results in `c.last`:
 // after the search they are the outputs of the last evaluation (ff:449-474).
-template <int LPA, bool DC, bool NET>
+template <int LPA, bool DC, bool NET, bool PK>
 __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double otc = 0.0;
     if (kw > 0.0) {
@@ -2736,13 +2843,24 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
         otc = rate_switch(c.sw_rows, c.sw_cnt, kw, &nt);
         if (nt >= 0) {
             c.switched = 1;
-            if (nt != c.tariff) yl_set_tariff<LPA, DC, NET>(c, nt);
+            if (nt != c.tariff) yl_set_tariff<LPA, DC, NET, PK>(c, nt);
         }
     }
     const dgen_tariff& t = *c.tp;
     double kws = ((kw * 1000.0) * 0.96) / 1000.0;                  // ff:118-120
     double total = ((c.capex * kw + 0.0) * c.ccm) + 0.0 + otc;     // ff:263,280-282
     double wb;
+    double v13 = 0.0;
+    if constexpr (PK) {
+        if (c.pk13 && c.dem && c.S.pk) {
+            // kWh/kW tiers: this evaluation's month peaks (and demand charge)
+            // ahead of the energy bill, whose tier caps scale with them
+            c.src.gen_scale = kws;
+            const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, c.s_y, true, c.S)
+                                      : yl_demand(c.dem, c.src, kw, c.s_y, true, c.S);
+            v13 = c.dem_bill ? v : 0.0;
+        }
+    }
     if (!net_hourly(t)) {
         PH_T0(tn);
         wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
@@ -2757,7 +2875,9 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
         wb = NAN;
     }
     if constexpr (DC) {
-        if (c.dem) {
+        if (PK && c.pk13) {
+            wb += v13;
+        } else if (c.dem) {
             // one inlined demand pass for both uses: the no-system charge of a
             // newly set tariff (pass 0, once), then this evaluation's (pass 1)
             c.src.gen_scale = kws;
@@ -2796,7 +2916,11 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 // a divergent join's exec restore; the build guard
 // (dgen_amd/spill_guard.py) rejects any build with that pattern and falls
 // back to one agent per wave for the flagged kernel.
-template <int LPA, bool DC, bool NET>
+// PK (with DC): some tariff bills its tiers in kWh/kW (dgen_tables.peak_units):
+// the lanes keep the month peaks, which the demand pass computes ahead of the
+// energy bill; a separate instantiation so the other builds' registers are
+// untouched.
+template <int LPA, bool DC, bool NET, bool PK>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
          void* dcws, char* nbws) {
@@ -2808,11 +2932,14 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     YCtx<LPA> c(lane);
     const int sl = c.g.sl;
     c.y = sl + 1;
-    c.S = ylds_make(dyn_lds, half, c.g);
+    c.S = ylds_make(dyn_lds, half, c.g, PK && T.peak_units != 0);
     c.tariffs = T.tariffs;
     c.dem_table = T.demand;
     c.n_dem = T.n_demand;
     c.dem = nullptr;
+    c.dc_on = cfg.skip_demand_charges == 0;
+    c.dem_bill = false;
+    c.pk13 = false;
     c.dem_wo_pending = false;
     c.env_ok = false;
     c.env.lines = nullptr;
@@ -2861,10 +2988,16 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     bool bad = false;
     if (c.N < 1 || c.N > MAXY || c.N > LPA) { c.status |= DGEN_ST_YEARS; bad = true; }
     if (t0 < 0 || t0 >= T.n_tariffs) { c.status |= DGEN_ST_TARIFF; bad = true; }
-    // kWh/kW tier units (SSC scales those caps by the month's peak demand, not
-    // restated here): the agent is reported unsized, per agent (DGEN_ST_UNIT),
-    // instead of being billed with the wrong caps
-    else if (T.tariffs[t0].flags & DGEN_ST_UNIT) { c.status |= DGEN_ST_UNIT; bad = true; }
+    // kWh/kW tier units scale the caps by the month's peak import: the
+    // batch's demand machinery supplies it (DC kernels, dgen_tables.peak_units,
+    // a record behind `dc`); without it the agent is reported unsized, per
+    // agent (DGEN_ST_UNIT), instead of being billed with the wrong caps
+    else if ((T.tariffs[t0].flags & DGEN_ST_UNIT) ||
+             (peak_unit(T.tariffs[t0]) &&
+              !(PK && T.peak_units && tariff_peaks(T.demand, T.n_demand, T.tariffs[t0])))) {
+        c.status |= DGEN_ST_UNIT;
+        bad = true;
+    }
     const double max_load = c.kwh / naep0;                         // ff:440-444
     const double low = max_load * 0.8, high = max_load * 1.25;
     const double span = high - low;
@@ -2898,12 +3031,12 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     }
     PH_ADD_KS(15, t_pro, sl == 0);             // prologue: agent loads, loan, bracket
     PH_T0(t_all);
-    yl_set_tariff<LPA, DC, NET>(c, t0);
+    yl_set_tariff<LPA, DC, NET, PK>(c, t0);
     int nfev = 0;
     double x_last = 0.0;
     double kw_star = brent_bounded(
         [&](double x) __attribute__((always_inline)) {
-            return yl_objective<LPA, DC, NET>(c, x);
+            return yl_objective<LPA, DC, NET, PK>(c, x);
         },
         low, high, xatol, &nfev, &x_last);
     const YLast& l = c.last;
@@ -2942,7 +3075,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
 }
 
 // Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
-template <int LPA, bool DC, bool NET>
+template <int LPA, bool DC, bool NET, bool PK>
 __global__ void __launch_bounds__(WAVE)
 k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
                  int64_t n_scratch, int64_t i0, int64_t i1, char* nbws, int nb_scan) {
@@ -2955,7 +3088,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     const Seg<LPA> g(lane);
     const int y = g.sl + 1;
     const int half = lds_half(T.max_periods);
-    YLds S = ylds_make(dyn_lds, half, g);
+    YLds S = ylds_make(dyn_lds, half, g, PK && T.peak_units != 0);
     WsLayout W = ws_layout(ws, n);
     const bool is_res = (A.flags[i] & 1) != 0;
     const bool is_ca = (A.flags[i] & 2) != 0;
@@ -2975,7 +3108,14 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     double total = ((system_costs + batt_costs) * A.ccm[i]) + 0.0 + otc;
     const double vor = A.vor[i];
     const bool mo2 = net_hourly(t);
-    const dgen_demand* dem = DC ? tariff_demand(T, cfg, t) : nullptr;
+    // demand record: its charges (extension mode), or the month peaks the
+    // kWh/kW tiers scale with (pk13: that pass runs ahead of the energy bills)
+    const dgen_demand* bill_dem = DC ? tariff_demand(T, cfg, t) : nullptr;
+    const bool pk13 = PK && peak_unit(t) && S.pk != nullptr && tariff_peaks(T.demand, T.n_demand, t);
+    const dgen_demand* dem = pk13 ? tariff_peaks(T.demand, T.n_demand, t) : bill_dem;
+    // the segment's LDS stage of the staged demand pass sits after the year-lane layout
+    DemStage* const stage = reinterpret_cast<DemStage*>(reinterpret_cast<char*>(dyn_lds) +
+                                                        ylds_bytes(half, LPA, S.pk != nullptr)) + (lane / LPA);
     YSrc src;
     {
         const int lr = A.load_row[i];
@@ -2991,6 +3131,11 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         src.ts_mult = A.price_mult[i];
     }
     double wo1 = NAN, wb = NAN;
+    // kWh/kW tiers: the no-system month peaks ahead of the no-system bill (k_size's
+    // first_without already holds it for the same tariff), the battery case's
+    // ahead of its bill
+    double v0 = 0.0, v1 = 0.0;
+    if (pk13 && !same_tariff) v0 = yl_demand_staged(dem, src, 1.0, false, S, stage, g);
     if (!mo2) {
         const double2* lg = W.LGb + (int64_t)i * NBIN;
         for (int cell = g.sl; cell < 12 * t.P; cell += LPA) {
@@ -3001,6 +3146,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         }
         wave_lds_sync();
         wo1 = same_tariff ? O.first_without[i] : yl_bill_nem_nosys(t, S, cfg.nm_yearend_sell_rate, g);
+        if (pk13) v1 = yl_demand_staged(dem, src, s_y, true, S, stage, g);
         wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
     } else if constexpr (NET) {
         if (same_tariff) {
@@ -3011,6 +3157,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
                           src.load_scale, S, g);
             wo1 = yl_bill_mo2_nogen_par(t, S, g);
         }
+        if (pk13) v1 = yl_demand_staged(dem, src, s_y, true, S, stage, g);
         // the split of the battery-case hours over the lanes' degradation
         // factors [s_lo, s_hi] (the agent's net-billing record is free: its
         // search finished in k_size)
@@ -3038,12 +3185,14 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         }
         if (!nb_ok) wb = yl_bill_net(t, src, s_y, true, S);
     }
-    if (DC && dem) {   // k_size's first_without already carries the no-system demand charge
+    if (pk13) {
+        if (bill_dem) {
+            wb += v1;
+            if (!same_tariff) wo1 += v0;
+        }
+    } else if (DC && dem) {   // k_size's first_without already carries the no-system demand charge
         for (int pass = same_tariff ? 1 : 0; pass < 2; pass++) {
             const bool wg = pass == 1;
-            // the segment's LDS stage sits after the year-lane layout
-            DemStage* stage = reinterpret_cast<DemStage*>(reinterpret_cast<char*>(dyn_lds) +
-                                                          ylds_bytes(half, LPA)) + (lane / LPA);
             const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);
             if (wg) wb += v;
             else wo1 += v;
@@ -3649,6 +3798,10 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
         set_err("dgen_open: invalid battery/loan configuration");
         return DGEN_E_ARG;
     }
+    if (cfg->batt_update_hours != 24 && cfg->batt_update_hours != 1) {
+        set_err("dgen_open: batt_update_hours must be 24 (a plan per day) or 1 (re-planned every hour)");
+        return DGEN_E_ARG;
+    }
     HIP_TRY(hipSetDevice(device));
     dgen_ctx* c = new (std::nothrow) dgen_ctx();
     if (!c) { set_err("dgen_open: out of host memory"); return DGEN_E_ARG; }
@@ -3778,7 +3931,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // the year-lane kernels keep the TOU demand peaks in the lane's LDS column
     // (4 x half slots): with demand charges billed it must hold DGEN_DCP
     dgen_tables Tk = *T;
-    const bool dc = c->cfg.skip_demand_charges == 0 && Tk.n_demand > 0;
+    // the demand machinery also supplies the month peaks of kWh/kW tier units
+    const bool dc = (c->cfg.skip_demand_charges == 0 && Tk.n_demand > 0) || (Tk.peak_units && Tk.n_demand > 0);
     if (dc && 4 * lds_half(Tk.max_periods) < DCP) Tk.max_periods = (DCP + 3) / 4;
     // yl_bill_nb stages its entries and month sums in slots 2 half .. 2 half + 4
     if (n_scratch > 0 && lds_half(Tk.max_periods) < 3) Tk.max_periods = 3;
@@ -3827,11 +3981,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // two agents per wave when every analysis period fits 32 lanes, unless the
     // build guard withdrew that kernel's 32-lane instantiation (DGEN_NO2_*)
     const bool fits32 = A->max_years >= 1 && A->max_years <= 32;
-    const int lpa_s = (fits32 && !(dc ? DGEN_NO2_SIZE_DC : DGEN_NO2_SIZE)) ? 32 : WAVE;
-    const int lpa_f = (fits32 && !(dc ? DGEN_NO2_FIN_DC : DGEN_NO2_FIN)) ? 32 : WAVE;
-    const size_t ylds_s = ylds_bytes(lds_half(T->max_periods), lpa_s);
+    const bool pk = dc && T->peak_units != 0;       // kWh/kW tiers: the PK instantiations
+    const int lpa_s = (fits32 && !(pk ? DGEN_NO2_SIZE_PK : dc ? DGEN_NO2_SIZE_DC : DGEN_NO2_SIZE)) ? 32 : WAVE;
+    const int lpa_f = (fits32 && !(pk ? DGEN_NO2_FIN_PK : dc ? DGEN_NO2_FIN_DC : DGEN_NO2_FIN)) ? 32 : WAVE;
+    const size_t ylds_s = ylds_bytes(lds_half(T->max_periods), lpa_s, pk);
     // k_batt_finance's demand-charge instantiations stage hours per segment
-    const size_t ylds_f = ylds_bytes(lds_half(T->max_periods), lpa_f) +
+    const size_t ylds_f = ylds_bytes(lds_half(T->max_periods), lpa_f, pk) +
                           (dc ? (size_t)(WAVE / lpa_f) * DEM_STAGE_BYTES : 0);
     hipStream_t s2 = c->s2;
     char* const nbws = n_scratch > 0 ? ws_nb(ws, n, n_scratch) : nullptr;
@@ -3850,27 +4005,35 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         if (lpa_s == 32 && !dc) {
 #if !DGEN_NO2_SIZE
             if (net)
-                hipLaunchKernelGGL((k_size_w<32, false, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
+                hipLaunchKernelGGL((k_size_w<32, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
                                    n, i0, i1, nullptr, nbws);
             else
-                hipLaunchKernelGGL((k_size_w<32, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws);
 #endif
-        } else if (lpa_s == 32) {
+        } else if (lpa_s == 32 && !pk) {
 #if !DGEN_NO2_SIZE_DC
-            hipLaunchKernelGGL((k_size_w<32, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg, n,
-                               i0, i1, c->dc_buf, nbws);
+            hipLaunchKernelGGL((k_size_w<32, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                               c->cfg, n, i0, i1, c->dc_buf, nbws);
+#endif
+        } else if (lpa_s == 32) {
+#if !DGEN_NO2_SIZE_PK
+            hipLaunchKernelGGL((k_size_w<32, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                               c->cfg, n, i0, i1, c->dc_buf, nbws);
 #endif
         } else if (!dc) {
             if (net)
-                hipLaunchKernelGGL((k_size_w<WAVE, false, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                hipLaunchKernelGGL((k_size_w<WAVE, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws);
             else
-                hipLaunchKernelGGL((k_size_w<WAVE, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws);
+        } else if (!pk) {
+            hipLaunchKernelGGL((k_size_w<WAVE, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                               c->cfg, n, i0, i1, c->dc_buf, nbws);
         } else {
-            hipLaunchKernelGGL((k_size_w<WAVE, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
-                               n, i0, i1, c->dc_buf, nbws);
+            hipLaunchKernelGGL((k_size_w<WAVE, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                               c->cfg, n, i0, i1, c->dc_buf, nbws);
         }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
@@ -3878,14 +4041,19 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         dim3 grid((unsigned)((m + BLOCK - 1) / BLOCK)), block(BLOCK);
         for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
-#define DGEN_HB_LAUNCH(H, F, REP)                                                                 \
+#define DGEN_HB_LAUNCH_R(H, F, REP, R)                                                            \
     do {                                                                                          \
         if (nb_scan && !(REP))                                                                    \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, true>), grid, block, lds, s2, *T, *A, *O, c->cfg, n, \
-                               ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0);         \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, true, R>), grid, block, lds, s2, *T, *A, *O, c->cfg, \
+                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0);      \
         else                                                                                      \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, false>), grid, block, lds, s2, *T, *A, *O, c->cfg,   \
-                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? 1 : 0);   \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false, R>), grid, block, lds, s2, *T, *A, *O,      \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? 1 : 0); \
+    } while (0)
+#define DGEN_HB_LAUNCH(H, F, REP)                                                                 \
+    do {                                                                                          \
+        if (c->cfg.batt_update_hours == 1) DGEN_HB_LAUNCH_R(H, F, REP, true);                     \
+        else DGEN_HB_LAUNCH_R(H, F, REP, false);                                                  \
     } while (0)
             if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, false);
             else if (hourly) DGEN_HB_LAUNCH(true, false, false);
@@ -3898,6 +4066,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             else if (hourly) DGEN_HB_LAUNCH(true, false, true);
             else DGEN_HB_LAUNCH(false, false, true);
 #undef DGEN_HB_LAUNCH
+#undef DGEN_HB_LAUNCH_R
         }
         HIP_TRY(hipEventRecord(e[3], s2));
         if (!c->battery) {
@@ -3905,27 +4074,35 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         } else if (lpa_f == 32 && !dc) {
 #if !DGEN_NO2_FIN
             if (net)
-                hipLaunchKernelGGL((k_batt_finance_w<32, false, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                hipLaunchKernelGGL((k_batt_finance_w<32, false, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
             else
-                hipLaunchKernelGGL((k_batt_finance_w<32, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                hipLaunchKernelGGL((k_batt_finance_w<32, false, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
 #endif
-        } else if (lpa_f == 32) {
+        } else if (lpa_f == 32 && !pk) {
 #if !DGEN_NO2_FIN_DC
-            hipLaunchKernelGGL((k_batt_finance_w<32, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
-                               c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+            hipLaunchKernelGGL((k_batt_finance_w<32, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                               *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+#endif
+        } else if (lpa_f == 32) {
+#if !DGEN_NO2_FIN_PK
+            hipLaunchKernelGGL((k_batt_finance_w<32, true, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                               *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
 #endif
         } else if (!dc) {
             if (net)
-                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
             else
-                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
+                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
                                    *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+        } else if (!pk) {
+            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
+                               *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
         } else {
-            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A, *O,
-                               c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
+                               *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
         }
         HIP_TRY(hipEventRecord(e[4], s2));
     }

@@ -143,13 +143,17 @@ class Engine:
     def set_tariffs(self, records: np.ndarray, demand: Optional[np.ndarray] = None):
         """Upload compiled tariff records (+ the demand-charge records their
         ``dc`` field indexes, TariffTable.demand_array(); billed only when the
-        engine's cfg.skip_demand_charges is 0)."""
-        from .tariff import DEMAND_DTYPE, TARIFF_DTYPE
+        engine's cfg.skip_demand_charges is 0).  Tariffs whose tiers are in
+        kWh/kW get a zero-charge record for their month peaks when they have
+        none (tariff.attach_peak_records)."""
+        from .tariff import TARIFF_DTYPE, attach_peak_records
         recs = np.ascontiguousarray(records, dtype=TARIFF_DTYPE)
         if recs.size == 0:
             raise ValueError("empty tariff table")
         self._tariff_mo = recs["mo"].copy()
-        dem = np.zeros(0, DEMAND_DTYPE) if demand is None else np.ascontiguousarray(demand, DEMAND_DTYPE)
+        # kWh/kW tier units (codes 1, 3): month peaks from a demand record
+        recs, dem, peak_units = attach_peak_records(recs, demand)
+        self.tables.peak_units = int(peak_units)
         if int(recs["dc"].max()) > dem.size or int(recs["dc"].min()) < 0:
             raise ValueError("tariff dc index outside the demand table")
         self.tables.n_demand = int(dem.size)

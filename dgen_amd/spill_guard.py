@@ -43,11 +43,14 @@ LABEL = re.compile(r"^(\.LBB\w+|[A-Za-z_]\w*):")
 PASS = ("s_", "v_writelane", "v_readlane", "v_mov", "v_accvgpr_read", "v_accvgpr_mov", "v_cndmask")
 
 # 32-lane instantiations with a one-agent-per-wave fallback (compile macro)
+# (symbol prefix: <LPA, DC, NET, PK>; the kWh/kW-peak builds (PK) have their own)
 REMEDY = {
     "k_size_wILi32ELb0E": "DGEN_NO2_SIZE",
-    "k_size_wILi32ELb1E": "DGEN_NO2_SIZE_DC",
+    "k_size_wILi32ELb1ELb1ELb0E": "DGEN_NO2_SIZE_DC",
+    "k_size_wILi32ELb1ELb1ELb1E": "DGEN_NO2_SIZE_PK",
     "k_batt_finance_wILi32ELb0E": "DGEN_NO2_FIN",
-    "k_batt_finance_wILi32ELb1E": "DGEN_NO2_FIN_DC",
+    "k_batt_finance_wILi32ELb1ELb1ELb0E": "DGEN_NO2_FIN_DC",
+    "k_batt_finance_wILi32ELb1ELb1ELb1E": "DGEN_NO2_FIN_PK",
 }
 
 

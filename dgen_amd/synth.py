@@ -36,6 +36,9 @@ CONFIGS = {
     # parity case (not a bench line): tariffs spread over SAM's metering
     # options 0-4 (the reference passes ur_metering_option through, ff:586)
     "metering_mix": (6, "mixed", "all", "mixed population, metering options 0-4"),
+    # parity case: commercial tariffs whose tiers are in kWh/kW (unit 1) or
+    # kWh/kW daily (unit 3) on 60 %, caps scaled by the month's peak import
+    "com_kwkw": (7, "com", "kwkw", "commercial, kWh/kW tier units"),
 }
 
 
@@ -133,17 +136,30 @@ def random_tariffs(rng, n: int, metering: str):
             mo = int(rng.integers(0, 5))
         else:
             mo = 0 if metering in ("nem", "nem_dc") else (2 if metering == "nb" else int(rng.random() < 0.2) * 2)
+        unit = 0
+        if metering == "kwkw":
+            unit = int(rng.choice([1, 3, 0], p=[0.35, 0.25, 0.40]))
+            if unit and T == 1:
+                T = 2
+                prices = np.sort(np.round(rng.uniform(0.06, 0.40, (T, P)), 5), axis=0)
         lv = None
         if T > 1:
-            lv = np.sort(rng.choice([250.0, 400.0, 600.0, 900.0], size=(T, P)), axis=0)
+            if unit == 1:        # kWh per kW of the month's peak
+                lv = np.sort(rng.choice([120.0, 200.0, 300.0, 450.0], size=(T, P)), axis=0)
+            elif unit == 3:      # kWh per kW per day
+                lv = np.sort(rng.choice([4.0, 7.0, 10.0, 15.0], size=(T, P)), axis=0)
+            else:
+                lv = np.sort(rng.choice([250.0, 400.0, 600.0, 900.0], size=(T, P)), axis=0)
             lv[-1, :] = 1e38
         if k % 2 == 0:
             d = {"e_prices": prices.tolist(), "e_wkday_12by24": wk.tolist(),
                  "e_wkend_12by24": we.tolist(), "fixed_charge": fixed, "ur_metering_option": mo}
             if lv is not None:
                 d["e_levels"] = lv.tolist()
+            if unit:
+                d["energy_rate_unit"] = {1: "kWh/kW", 3: "kWh/kW daily"}[unit]
         else:
-            rows = [[p + 1, t + 1, 1e38 if lv is None else float(lv[t, p]), 0, float(prices[t, p]), 0.0]
+            rows = [[p + 1, t + 1, 1e38 if lv is None else float(lv[t, p]), unit, float(prices[t, p]), 0.0]
                     for p in range(P) for t in range(T)]
             d = {"ur_ec_tou_mat": rows, "ur_ec_sched_weekday": (wk + 1).tolist(),
                  "ur_ec_sched_weekend": (we + 1).tolist(), "ur_monthly_fixed_charge": fixed,

@@ -425,6 +425,28 @@ class TariffError(ValueError):
     pass
 
 
+def peak_only_record() -> np.ndarray:
+    """A demand record with no charges and one demand period (every hour in
+    period 0): the month peaks of a tariff whose tiers are in kWh/kW (unit
+    codes 1 and 3, SSC scales those caps by the month's peak import) come from
+    the demand machinery's flat peak, whether or not demand charges are billed."""
+    return np.zeros((), dtype=DEMAND_DTYPE)
+
+
+def attach_peak_records(records: np.ndarray, demand: Optional[np.ndarray]):
+    """(records, demand) with every kWh/kW-tier tariff that has no demand record
+    pointing at one shared peak_only_record (appended), and whether any tariff
+    bills its tiers in kWh/kW (dgen_tables.peak_units)."""
+    recs = np.array(records, dtype=TARIFF_DTYPE, copy=True)
+    dem = np.zeros(0, DEMAND_DTYPE) if demand is None else np.ascontiguousarray(demand, DEMAND_DTYPE)
+    pk = (recs["unit"] == 1) | (recs["unit"] == 3)
+    need = pk & (recs["dc"] == 0)
+    if need.any():
+        dem = np.concatenate([dem, peak_only_record()[None]])
+        recs["dc"][need] = dem.size
+    return recs, dem, bool(pk.any())
+
+
 @dataclass
 class CompiledTariff:
     fields: Dict[str, Any]          # ElectricityRates fields (ts variant: no TS series)
@@ -458,7 +480,7 @@ def pack_record(fields: Dict[str, Any]) -> np.ndarray:
             raise TariffError("tariff matrix is not a complete period x tier grid")
         rec["P"], rec["T"] = P, T
         unit = int(m[0, 3])
-        if unit not in (0, 2):
+        if unit not in (0, 1, 2, 3):
             flags |= ST_UNIT
         rec["unit"] = unit
         for row in m:

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 6
+#define DGEN_ABI_VERSION 7
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_NH    8760   /* hours per year                                    */
@@ -88,6 +88,11 @@ typedef struct {
     double  batt_init_soc;         /* fraction (ff:151: 30 %)                       */
     double  batt_eta_in;           /* AC -> stored                                  */
     double  batt_eta_out;          /* stored -> AC                                  */
+    int32_t batt_update_hours;     /* peak-shaving re-plan interval: 24 = one 24-h  */
+                                   /* plan per calendar day (SSC's BTM peak-shaving */
+                                   /* update), 1 = a 24-h look-ahead plan every     */
+                                   /* hour (bdh:86-87 read literally); DESIGN.md 3  */
+    int32_t pad1;
 } dgen_cfg;
 
 /* Compiled tariff = the Utilityrate5.ElectricityRates energy fields that
@@ -96,7 +101,13 @@ typedef struct {
 typedef struct {
     int32_t P, T;                  /* periods, tiers                               */
     int32_t mo;                    /* ur_metering_option (0 or 2)                  */
-    int32_t unit;                  /* usage unit code (0 kWh/mo, 2 kWh/day)        */
+    int32_t unit;                  /* usage unit code: 0 kWh/mo, 1 kWh/kW, 2 kWh    */
+                                   /* daily, 3 kWh/kW daily (ff:778-779, one code   */
+                                   /* per tariff, ff:939-956); 1 and 3 scale the tier*/
+                                   /* caps by the month's peak import (kW), which the*/
+                                   /* kernels take from the record `dc` points to    */
+                                   /* (its flat peak; a zero-charge one-period record*/
+                                   /* when the tariff has no demand charges)         */
     double  fixed;                 /* ur_monthly_fixed_charge ($/month)            */
     double  cap[DGEN_MAXT];        /* tier upper bounds (single cap per tier)      */
     double  buy[DGEN_MAXP][DGEN_MAXT];
@@ -105,6 +116,8 @@ typedef struct {
     uint8_t wkend[12][24];
     int32_t flags;                 /* DGEN_ST_EMPTY_EC / _UNIT / _DEMAND if so      */
     int32_t dc;                    /* 1 + index into dgen_tables.demand; 0 = none  */
+                                   /* (charges billed in extension mode only; the   */
+                                   /* peaks of units 1 / 3 are read in both modes)  */
 } dgen_tariff;
 
 /* Demand charges of one tariff (extension mode): the ur_dc_flat_mat /
@@ -152,7 +165,9 @@ typedef struct {
     int32_t max_periods;           /* max P over tariffs (sizes LDS; 0 = DGEN_MAXP) */
     const dgen_demand* demand;     /* [n_demand] (may be NULL when n_demand == 0)   */
     int32_t n_demand;
-    int32_t pad;
+    int32_t peak_units;            /* 1: some tariff bills its tiers in kWh/kW (unit */
+                                   /* codes 1, 3): the year-lane kernels keep month  */
+                                   /* peaks per lane (see dgen_tariff.unit)          */
 } dgen_tables;
 
 /* Agent batch, structure of arrays (device pointers, length n).  Column

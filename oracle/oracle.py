@@ -54,7 +54,7 @@ class Cfg(ctypes.Structure):
         ("batt_v_nom", _c_double), ("batt_q_full", _c_double),
         ("batt_min_soc", _c_double), ("batt_max_soc", _c_double),
         ("batt_init_soc", _c_double), ("batt_eta_in", _c_double),
-        ("batt_eta_out", _c_double),
+        ("batt_eta_out", _c_double), ("batt_update_hours", _c_int32),
     ]
 
 
@@ -113,7 +113,7 @@ class LoanIn(ctypes.Structure):
 DEFAULT_CFG = dict(
     nm_yearend_sell_rate=0.02, loan_rate_pct=7.5, insurance_rate_pct=0.0, itc_fed_max=1e38,
     depr_sl_years=7, batt_v_nom=3.6, batt_q_full=3.2, batt_min_soc=0.10, batt_max_soc=0.95,
-    batt_init_soc=0.30, batt_eta_in=0.9408, batt_eta_out=0.9408,
+    batt_init_soc=0.30, batt_eta_in=0.9408, batt_eta_out=0.9408, batt_update_hours=24,
 )
 
 

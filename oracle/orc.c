@@ -136,7 +136,12 @@ static void hour_calendar(const orc_tariff* t, int* month_of, int* period_of) {
  * period billed its share u_p/U of every tier at its own price.  One tier:
  * every period's kWh at its own price, sum_p u_p * buy_p (the same quantity
  * without the share / re-multiplication round trip). */
-static double month_energy_charge(const orc_tariff* t, int m, const double* u) {
+/* Tier caps per usage unit (the compile's code, ff:778-779, harmonised to one
+ * code per tariff, ff:939-956): 0 kWh, 2 kWh daily (x days in month), 1 kWh/kW
+ * (x the month's peak demand: the largest hourly grid import of the billed
+ * case, kW; SSC's billing demand with ur_enable_billing_demand = 0, ff:614),
+ * 3 kWh/kW daily (x peak x days).  Parity unpinned (SSC restatement). */
+static double month_energy_charge(const orc_tariff* t, int m, const double* u, double peak) {
     double U = 0.0;
     for (int p = 0; p < t->P; p++) U += u[p];
     if (!(U > 0.0)) return 0.0;
@@ -145,7 +150,8 @@ static double month_energy_charge(const orc_tariff* t, int m, const double* u) {
         for (int p = 0; p < t->P; p++) charge += u[p] * t->buy[p][0];
         return charge;
     }
-    double scale = (t->unit == 2) ? (double)kDaysInMonth[m] : 1.0;
+    const double days = (double)kDaysInMonth[m];
+    double scale = (t->unit == 2) ? days : (t->unit == 1) ? peak : (t->unit == 3) ? peak * days : 1.0;
     double charge = 0.0, prev = 0.0;
     for (int k = 0; k < t->T; k++) {
         double hi = (k == t->T - 1) ? INFINITY : t->cap[k] * scale;
@@ -177,7 +183,7 @@ static double month_energy_charge(const orc_tariff* t, int m, const double* u) {
  * Fixed charges are always billed. */
 static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* net /*[12][P]*/,
                         const double* imp, const double* exv /*[12][P] $ or kWh*/, const double* lbin,
-                        const double* gbin, int ts) {
+                        const double* gbin, const double* peak /*[12]*/, int ts) {
     double total = 0.0, carry = 0.0;
     double credit[ORC_MAXP];
     for (int p = 0; p < ORC_MAXP; p++) credit[p] = 0.0;
@@ -196,7 +202,7 @@ static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* n
                     credit[p] += -n;
                 }
             }
-            bill += month_energy_charge(t, m, u);
+            bill += month_energy_charge(t, m, u, peak[m]);
             if (m == 11) {
                 double c = 0.0;
                 for (int p = 0; p < t->P; p++) c += credit[p];
@@ -209,7 +215,7 @@ static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* n
                 u[p] = n > 0.0 ? n : 0.0;
                 cr += (n < 0.0 ? -n : 0.0) * t->sell[p][0];
             }
-            double e = month_energy_charge(t, m, u) - cr - carry;
+            double e = month_energy_charge(t, m, u, peak[m]) - cr - carry;
             carry = e < 0.0 ? -e : 0.0;
             bill += e < 0.0 ? 0.0 : e;
         } else if (t->mo == 4) {
@@ -218,11 +224,11 @@ static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* n
                 u[p] = lbin[m * ORC_MAXP + p];
                 cr += gbin[m * ORC_MAXP + p] * t->sell[p][0];
             }
-            bill += month_energy_charge(t, m, u) - cr;
+            bill += month_energy_charge(t, m, u, peak[m]) - cr;
         } else {
             double cr = 0.0;
             for (int p = 0; p < t->P; p++) u[p] = imp[m * ORC_MAXP + p];
-            double charge = month_energy_charge(t, m, u);
+            double charge = month_energy_charge(t, m, u, peak[m]);
             if (ts) {
                 for (int p = 0; p < t->P; p++) cr += exv[m * ORC_MAXP + p];
             } else {
@@ -242,15 +248,18 @@ static double year_bill(const orc_tariff* t, const orc_cfg* cfg, const double* n
     return total;
 }
 
-/* Bins one year: gen scaled by s (degradation), hour by hour in time order. */
+/* Bins one year: gen scaled by s (degradation), hour by hour in time order;
+ * peak[m] = the month's largest hourly grid import (0 without import). */
 static void bin_year(const orc_tariff* t, const int* mon, const int* per, const double* gen,
                      const double* load, const double* ts, double s, double* net, double* imp,
-                     double* exv, double* lbin, double* gbin) {
+                     double* exv, double* lbin, double* gbin, double* peak) {
     for (int i = 0; i < 12 * ORC_MAXP; i++) net[i] = imp[i] = exv[i] = lbin[i] = gbin[i] = 0.0;
+    for (int m = 0; m < 12; m++) peak[m] = 0.0;
     for (int h = 0; h < ORC_NH; h++) {
         double g = gen ? gen[h] * s : 0.0;
         double d = load[h] - g;            /* > 0: import */
         int b = mon[h] * ORC_MAXP + per[h];
+        if (d > peak[mon[h]]) peak[mon[h]] = d;
         net[b] += d;
         lbin[b] += load[h];
         gbin[b] += g;
@@ -316,19 +325,19 @@ int orc_ur5(const orc_tariff* t, const orc_cfg* cfg, const double* gen, const do
     int ts = (t->mo == 2) && ts_sell != NULL;
     const double* tsp = ts ? ts_sell : NULL;
     double net[12 * ORC_MAXP], imp[12 * ORC_MAXP], exv[12 * ORC_MAXP];
-    double lbin[12 * ORC_MAXP], gbin[12 * ORC_MAXP];
+    double lbin[12 * ORC_MAXP], gbin[12 * ORC_MAXP], peak[12];
     double rate_base = 1.0 + inflation_pct * 0.01 + escal_pct * 0.01;
     double sys_base = 1.0 - degr_pct * 0.01;
 
-    bin_year(t, mon, per, NULL, load, tsp, 1.0, net, imp, exv, lbin, gbin);
-    double wo1 = year_bill(t, cfg, net, imp, exv, lbin, gbin, ts);
+    bin_year(t, mon, per, NULL, load, tsp, 1.0, net, imp, exv, lbin, gbin, peak);
+    double wo1 = year_bill(t, cfg, net, imp, exv, lbin, gbin, peak, ts);
     if (t->dc_on) wo1 += year_demand(t, NULL, load, 1.0);
     bill_w[0] = bill_wo[0] = aev[0] = 0.0;
     for (int i = 0; i < nyears; i++) {
         double r = pow_int(rate_base, i);
         double s = pow_int(sys_base, i);
-        bin_year(t, mon, per, gen, load, tsp, s, net, imp, exv, lbin, gbin);
-        double wb = year_bill(t, cfg, net, imp, exv, lbin, gbin, ts);
+        bin_year(t, mon, per, gen, load, tsp, s, net, imp, exv, lbin, gbin, peak);
+        double wb = year_bill(t, cfg, net, imp, exv, lbin, gbin, peak, ts);
         if (t->dc_on) wb += year_demand(t, gen, load, s);
         double w = wb * r;
         double wo = wo1 * r;
@@ -447,7 +456,7 @@ void orc_batt_size(double desired_kw, double desired_kwh, double desired_v, cons
     *power_kw = bank * (desired_kw / desired_kwh);
 }
 
-/* Daily peak-shaving target with perfect 24 h look-ahead: the smallest grid
+/* Peak-shaving target with perfect 24 h look-ahead: the smallest grid
  * import level T >= 0 such that holding imports at T needs no more than the
  * energy stored at the start of the day:
  *     f(T) = sum_h min(max(d_h - T, 0), P) <= E,   d_h = max(load_h - pv_h, 0).
@@ -464,10 +473,14 @@ void orc_batt_size(double desired_kw, double desired_kwh, double desired_v, cons
  * k largest, so T = (S_K - E) / K for the largest K with S_K - K s[K-1] <= E.
  * Otherwise bisection until no breakpoint (s_k, s_k - P) lies inside the
  * bracket, then the exact linear piece. */
+/* The window is hours h0 .. h0 + 23; past the last hour of the year it wraps
+ * to the first (a typical year repeats: the forecast for January 1 of the next
+ * year is this year's January 1).  Only the hourly re-plan reaches past 8759. */
 static double day_target(const double* load, const double* pv, int h0, double power, double avail) {
     double s[24];
     for (int k = 0; k < 24; k++) {
-        double v = load[h0 + k] - pv[h0 + k];
+        const int h = (h0 + k) % ORC_NH;
+        double v = load[h] - pv[h];
         s[k] = v > 0.0 ? v : 0.0;
     }
     for (int i = 1; i < 24; i++) {          /* insertion sort, descending */
@@ -519,11 +532,20 @@ static double day_target(const double* load, const double* pv, int h0, double po
 }
 
 /* BTM dispatch (bdh:59-98): peak shaving with 24 h look-ahead, charge only from
- * PV surplus, no grid charging, discharge whenever imports exceed the target. */
+ * PV surplus, no grid charging, discharge whenever imports exceed the target.
+ * Re-plan interval (cfg->batt_update_hours):
+ *   24  one plan per calendar day, made at its first hour from the energy
+ *       stored then over that day's 24 hours (SSC's BTM peak-shaving update);
+ *    1  a plan every hour from the energy stored at that hour over the next 24
+ *       hours (bdh:86-87 read literally: batt_look_ahead_hours = 24,
+ *       batt_dispatch_update_frequency_hours = 1).  A plan only matters in an
+ *       hour that can discharge (net load > 0, energy stored > 0), so the
+ *       hourly rule forms it only there; the result is the same.            */
 void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, double power_kw,
                        const orc_cfg* cfg, double* sysgen, double* grid_to_load) {
     double soc = cfg->batt_init_soc;
     double target = 0.0;
+    const int hourly = cfg->batt_update_hours == 1;
     /* per-step constants (multiplications instead of divisions in the scan) */
     const double inv_eta_in = 1.0 / cfg->batt_eta_in;
     const double in_per_bank = bank_kwh > 0.0 ? cfg->batt_eta_in / bank_kwh : 0.0;
@@ -535,7 +557,7 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
             grid_to_load[h] = n > 0.0 ? n : 0.0;
             continue;
         }
-        if (h % 24 == 0) {
+        if (!hourly && h % 24 == 0) {
             double avail = (soc - cfg->batt_min_soc) * bank_kwh * cfg->batt_eta_out;
             if (avail < 0.0) avail = 0.0;
             target = day_target(load, pv, h, power_kw, avail);
@@ -552,6 +574,7 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
         } else {
             double avail = (soc - cfg->batt_min_soc) * bank_kwh * cfg->batt_eta_out;
             if (avail < 0.0) avail = 0.0;
+            if (hourly) target = (n > 0.0 && avail > 0.0) ? day_target(load, pv, h, power_kw, avail) : 0.0;
             double d = n - target;
             if (d < 0.0) d = 0.0;
             if (d > power_kw) d = power_kw;

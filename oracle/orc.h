@@ -78,6 +78,7 @@ typedef struct {
     double batt_init_soc;          /* fraction (ff:151: 30 %)                     */
     double batt_eta_in;            /* AC->stored efficiency                       */
     double batt_eta_out;           /* stored->AC efficiency                       */
+    int32_t batt_update_hours;     /* 24: daily plan, 1: re-planned every hour    */
 } orc_cfg;
 
 /* One row of the rate-switch table, already filtered to (tech, eia_id, res_com). */

@@ -6,8 +6,9 @@
 # Steps
 #   tests      pytest -m gpu (TESTS: paths / -k expression, default the suite)
 #   smoke      __graft_entry__.smoke()
-#   bench      one bench line per BENCH ("config:agents[:extra args]" ...,
-#              default the driver's own no-flag run)
+#   bench      one bench line per BENCH ("config:agents[:extra,args]" ..., the
+#              extra bench.py arguments comma-separated; default the driver's
+#              own no-flag run)
 #   ab         one bench line per ';'-separated VARIANTS entry
 #              ("[lib=<name>] <bench.py args>"; lib= picks ablate/libdgen_<name>.so,
 #              built by scripts/make_ablations.py)
@@ -59,8 +60,9 @@ for step in "$@"; do
   bench)
     for b in ${BENCH:-default}; do
       if [ "$b" = default ]; then args=""; name=default
-      else IFS=: read -r cfg ag extra <<< "$b"; args="--config $cfg --agents $ag ${extra:---steps 5 --warmup 1 --no-cpu}"
-           name=${cfg}_$ag; fi
+      else IFS=: read -r cfg ag extra <<< "$b"; extra=${extra//,/ }
+           args="--config $cfg --agents $ag ${extra:---steps 5 --warmup 1 --no-cpu}"
+           name=${cfg}_$ag${BENCH_SUFFIX:-}; [ -n "$extra" ] && name=${name}_$(echo "$extra" | tr -dc 'a-z0-9' | cut -c1-24); fi
       timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py $args > $O/bench_$name.log 2> $O/bench_$name.err; rc=$?
       echo "bench $name rc=$rc"; line $O/bench_$name.log; stop $rc
     done;;

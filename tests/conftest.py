@@ -30,3 +30,14 @@ def engine_dc():
     eng = Engine(0, EngineConfig(skip_demand_charges=0))
     yield eng
     eng.close()
+
+
+@pytest.fixture(scope="session")
+def engine_hourly_plan():
+    """Engine whose peak-shaving target is re-planned every hour
+    (cfg.batt_update_hours = 1)."""
+    from dgen_amd.config import EngineConfig
+    from dgen_amd.engine import Engine
+    eng = Engine(0, EngineConfig(batt_update_hours=1))
+    yield eng
+    eng.close()

@@ -254,6 +254,15 @@ def tariff_cases(rng):
     cases.append(("mismatched_levels", {"e_prices": [[0.1, 0.2]], "e_levels": [[100]],
                                         "e_wkday_12by24": sched_tou(10, 14)}))
     cases.append(("ragged_sched", {"e_prices": [[0.1, 0.2]], "e_wkday_12by24": [[1] * 10] * 6}))
+    # kWh/kW tier units (ff:778-779): caps x the month's peak import (x days for 3)
+    cases.append(("kwkw_unit", {"e_prices": [[0.11, 0.24], [0.17, 0.33]], "e_levels": [[180, 180], [1e9, 1e9]],
+                                "energy_rate_unit": "kWh/kW", "e_wkday_12by24": sched_tou(14, 19),
+                                "e_wkend_12by24": sched_tou(0, 0), "fixed_charge": 30.0}))
+    cases.append(("kwkw_daily_nb", {"ur_ec_tou_mat": [[1, 1, 6.0, 3, 0.12, 0.04], [1, 2, 1e38, 3, 0.19, 0.04],
+                                                      [2, 1, 6.0, 3, 0.21, 0.05], [2, 2, 1e38, 3, 0.29, 0.05]],
+                                    "ur_ec_sched_weekday": sched_tou(16, 21, 1, 2),
+                                    "ur_ec_sched_weekend": sched_tou(0, 0, 1, 2),
+                                    "ur_monthly_fixed_charge": 15.0, "ur_metering_option": 2}))
     cases.append(("unit_mode", {"ur_ec_tou_mat": [[1, 1, 1e38, 2, 0.1, 0], [2, 1, 1e38, 0, 0.2, 0],
                                                   [3, 1, 1e38, 0, 0.3, 0]],
                                 "ur_ec_sched_weekday": sched_tou(9, 17, 1, 3),
@@ -422,6 +431,10 @@ def agent_specs(tariffs):
     add("res_rand", BASE_RES, state_abbr="NY", load_kwh_per_customer_in_bin=9300.0,
         tariff="rand10", load_row=3, cf_row=4, wholesale_row=1, eia_id=107,
         economic_lifetime_yrs=20, loan_term_yrs=10)
+    add("com_kwkw", BASE_COM, state_abbr="OH", load_kwh_per_customer_in_bin=180000.0,
+        tariff="kwkw_unit", load_row=0, cf_row=3, wholesale_row=0, eia_id=305)
+    add("res_kwkw_daily_nb", BASE_RES, state_abbr="AZ", load_kwh_per_customer_in_bin=11500.0,
+        tariff="kwkw_daily_nb", load_row=2, cf_row=1, wholesale_row=1, eia_id=108)
     for s in specs:
         s["tariff_dict"] = t[s["tariff"]]
     return specs

@@ -70,31 +70,46 @@ def test_zero_load_raises_like_reference():
         ff.calc_system_size_and_performance(store, r, None, table)
 
 
-def test_kwh_per_kw_units_leave_only_that_agent_unsized():
-    """kWh/kW tier units (unit code 1) are not restated: that agent comes back
-    unsized (NaN outputs, a RuntimeWarning) and the rest of the chunk is sized
-    exactly as without it; its no-system planes keep the aggregate finite."""
+def test_kwh_per_kw_units_are_sized_like_the_oracle():
+    """kWh/kW tier units (codes 1 and 3: SSC scales the caps by the month's
+    peak import) are billed: the agents are sized, no warning, and every
+    agent of the chunk matches the oracle's restatement (oracle/orc.c
+    month_energy_charge with the month peaks of the billed case)."""
     import warnings
+    from dgen_amd.columnar import columnize_frame
+    from oracle import oracle as orc
     rows, store, table = helpers.golden_rows()
     df = pd.DataFrame(rows[:6]).copy()
     ones = [[1] * 24 for _ in range(12)]
-    df.at[df.index[2], "tariff_dict"] = {"ur_ec_tou_mat": [[1, 1, 500.0, 1, 0.2, 0.0], [1, 2, 1e38, 1, 0.25, 0.0]],
+    df.at[df.index[2], "tariff_dict"] = {"ur_ec_tou_mat": [[1, 1, 150.0, 1, 0.2, 0.0], [1, 2, 1e38, 1, 0.25, 0.0]],
                                          "ur_ec_sched_weekday": ones, "ur_ec_sched_weekend": ones,
                                          "ur_metering_option": 0}
+    df.at[df.index[4], "tariff_dict"] = {"e_prices": [[0.12, 0.2], [0.18, 0.3]], "e_levels": [[6.0, 6.0], [1e9, 1e9]],
+                                         "energy_rate_unit": "kWh/kW daily",
+                                         "e_wkday_12by24": [[1 if 15 <= h < 20 else 0 for h in range(24)]] * 12,
+                                         "e_wkend_12by24": [[0] * 24] * 12}
     ff._worker_conn = store
-    with pytest.warns(RuntimeWarning, match="kWh/kW"):
-        out, agg = ff.size_chunk(df, None, table, "simple")
-    r = out.iloc[2]
-    for k in ("system_kw", "npv", "payback_period", "batt_kw"):
-        assert np.isnan(r[k]), k
-    assert np.isnan(np.asarray(r["cash_flow"], float)).all()
-    assert np.isfinite(agg["net_sum_kw"]).all()
     with warnings.catch_warnings():
         warnings.simplefilter("error")
-        ref, _ = ff.size_chunk(df.drop(index=df.index[2]), None, table, "simple")
-    got = out.drop(index=df.index[2])
-    for k in ("system_kw", "npv", "payback_period", "batt_kwh", "npv_pv_batt" if "npv_pv_batt" in ref else "npv"):
-        assert np.array_equal(got[k].to_numpy(float), ref[k].to_numpy(float), equal_nan=True), k
+        out, agg = ff.size_chunk(df, None, table, "simple", hourly="array")
+    assert np.isfinite(out["system_kw"].to_numpy(float)).all() and np.isfinite(agg["net_sum_kw"]).all()
+    b = columnize_frame(df, store, table)
+    cols = b.frame_columns
+    recs = b.tariffs.array()
+    assert set(recs["unit"][cols["tariff0"][[2, 4]]]) == {1, 3}
+    opop = helpers.oracle_population(cols, recs, b.switches.array(), store.shapes, store.cfs, b.wholesale.array())
+    ref = opop.run(orc.make_cfg())
+    for i, r in enumerate(ref):
+        row = out.iloc[i]
+        assert abs(row["system_kw"] - r["system_kw"]) <= 1e-9 * max(1.0, r["system_kw"]), i
+        for k in ("npv", "batt_kwh"):
+            assert np.isclose(row[k], r[k], rtol=1e-6, atol=1e-6), (i, k, row[k], r[k])
+        assert row["payback_period"] == r["payback_period"], i
+        n1 = int(df["economic_lifetime_yrs"].iloc[i]) + 1
+        assert np.allclose(np.asarray(row["utility_bill_w_sys_pv_only"], float), r["bill_w_pv_only"][:n1],
+                           rtol=1e-6, atol=1e-5), i
+        assert np.allclose(np.asarray(row["utility_bill_w_sys_pv_batt"], float), r["bill_w_pv_batt"][:n1],
+                           rtol=1e-6, atol=1e-5), i
 
 
 def test_size_chunk_array_mode_equals_list_mode():

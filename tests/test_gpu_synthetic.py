@@ -17,7 +17,7 @@ from tests import helpers
 pytestmark = pytest.mark.gpu
 
 CASES = [("de_res", 300), ("res_1m_nem_tou", 600), ("ca_res_storage", 300), ("com_8m", 200),
-         ("national_mixed", 400), ("metering_mix", 400)]
+         ("national_mixed", 400), ("metering_mix", 400), ("com_kwkw", 240)]
 
 
 def _small_pop(cfg, n):
@@ -69,6 +69,9 @@ def test_synthetic_population_matches_oracle(engine, cfg, n, long_life):
             assert np.allclose(o[k_o][i], ref_h, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(ref_h).max())), (i, k_o)
     if cfg != "ca_res_storage":
         assert n_switch > 0          # the population exercises the DG switch
+    if cfg == "com_kwkw":            # kWh/kW tier units on >= 30 % of the agents, all sized
+        u = pop.tariffs["unit"][pop.cols["tariff0"]]
+        assert np.isin(u, (1, 3)).mean() >= 0.3
 
 
 @pytest.mark.parametrize("cfg,n", [("national_mixed", 3000), ("ca_res_storage", 2000)])
@@ -289,3 +292,40 @@ def test_nb_scan_overflow_repair_pass(engine):
     for k, v in a.items():
         if v is not None:
             assert np.array_equal(v, b[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("cfg,n", [("res_1m_nem_tou", 300), ("ca_res_storage", 200), ("com_8m", 160),
+                                   ("national_mixed", 300)])
+def test_hourly_replan_matches_oracle(engine_hourly_plan, cfg, n):
+    """The peak-shaving target re-planned every hour over the next 24 hours
+    (batt_update_hours = 1, k_hourly_batt<ROLL>) against the oracle's rule:
+    the battery-case planes, bills, NPV; the PV-only search is unchanged."""
+    eng = engine_hourly_plan
+    pop = _small_pop(cfg, n)
+    eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    eng.set_tariffs(pop.tariffs)
+    eng.set_switches(pop.switches)
+    batch = eng.upload_agents(pop.cols, pop.n_scratch)
+    out = eng.alloc_outputs(batch.n, hourly=True)
+    eng.size(batch, out)
+    torch.cuda.synchronize()
+    o = outputs_to_host(out)
+    opop = helpers.oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs,
+                                     pop.wholesale)
+    ref = opop.run(orc.make_cfg(batt_update_hours=1), hourly=True)
+    daily = opop.run(orc.make_cfg(), hourly=True, idx=range(min(n, 40)))
+    moved = 0
+    for i, r in enumerate(ref):
+        assert o["status"][i] == 0 and r["status"] == 0, i
+        assert o["nfev"][i] == r["nfev"], i
+        for k in ("npv", "batt_kwh", "npv_pv_batt"):
+            assert np.isclose(o[k][i], r[k], rtol=1e-6, atol=1e-6), (i, k, o[k][i], r[k])
+        N1 = int(pop.cols["econ_life"][i]) + 1
+        for k_o, k_r in (("cfev_batt", "cf_energy_value_pv_batt"), ("bill_w_batt", "bill_w_pv_batt")):
+            assert np.allclose(o[k_o][i, :N1], r[k_r], rtol=1e-6, atol=1e-5), (i, k_o)
+        ref_h = r["adopter_net_hourly_with_batt"]
+        assert np.allclose(o["net_with_batt"][i], ref_h, rtol=1e-5,
+                           atol=1e-5 * max(1.0, np.abs(ref_h).max())), i
+        if i < len(daily):
+            moved += not np.allclose(daily[i]["adopter_net_hourly_with_batt"], ref_h)
+    assert moved > 0                 # the re-plan interval changes the dispatch

@@ -193,3 +193,119 @@ def test_oracle_metering_options_known_answer(gen_kw, expect):
         assert r["bill_w"][1] == pytest.approx(expect[mo], rel=1e-7, abs=1e-6), mo
         # no system: every option bills the 24 kWh / day of load
         assert r["bill_wo"][1] == pytest.approx(24 * 365 * 0.2, rel=1e-7), mo
+
+
+# ---------------------------------------------------------------------------
+# peak-shaving re-plan interval: a plan per day vs a
+# 24-hour look-ahead plan every hour (bdh:86-87 read literally)
+# ---------------------------------------------------------------------------
+def _py_target(w, power, avail):
+    """The target rule restated by bisection on f(T) = sum min(max(d - T, 0), P)
+    (independent of the oracle's sorted-prefix form; exact to ~1e-13)."""
+    f = lambda t: sum(min(max(x - t, 0.0), power) for x in w)
+    if f(0.0) <= avail:
+        return 0.0
+    lo, hi = 0.0, max(w)
+    for _ in range(200):
+        mid = 0.5 * (lo + hi)
+        if f(mid) <= avail:
+            hi = mid
+        else:
+            lo = mid
+    return hi
+
+
+def _py_dispatch(load, pv, bank, power, cfg, hourly):
+    d = np.maximum(load - pv, 0.0)
+    soc, target = cfg.batt_init_soc, 0.0
+    sg, g2l = np.zeros(orc.NH), np.zeros(orc.NH)
+    for h in range(orc.NH):
+        n = load[h] - pv[h]
+        avail = max((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0)
+        if not hourly and h % 24 == 0:
+            target = _py_target(d[h:h + 24], power, avail)
+        if n < 0:
+            room = max((cfg.batt_max_soc - soc) * bank / cfg.batt_eta_in, 0.0)
+            c = min(-n, power, room)
+            soc += c * cfg.batt_eta_in / bank
+            sg[h], g2l[h] = pv[h] - c, 0.0
+        else:
+            if hourly:
+                w = np.concatenate([d, d])[h:h + 24]          # wraps past hour 8759
+                target = _py_target(w, power, avail) if (n > 0 and avail > 0) else 0.0
+            x = min(max(n - target, 0.0), power, avail)
+            soc -= x / (cfg.batt_eta_out * bank)
+            sg[h], g2l[h] = pv[h] + x, n - x
+    return sg, g2l
+
+
+@pytest.mark.parametrize("hourly", [False, True])
+def test_dispatch_rule_matches_python_restatement(hourly):
+    """orc_batt_dispatch (both re-plan intervals) against a direct Python
+    restatement with a bisection target, on a load with evening peaks, a PV
+    bell and days where an hour exceeds the power limit."""
+    rng = np.random.default_rng(41)
+    h = np.arange(orc.NH)
+    hod = h % 24
+    load = 0.6 + 0.9 * np.exp(-((hod - 19) / 2.5) ** 2) + 0.3 * rng.random(orc.NH)
+    load[rng.integers(0, orc.NH, 40)] += 4.0                 # saturating spikes
+    pv = np.maximum(0.0, np.sin((hod - 6) / 12 * np.pi)) * (2.2 + rng.random(orc.NH))
+    cfg = orc.make_cfg(batt_update_hours=1 if hourly else 24)
+    bank, power = 10.0, 2.5
+    sg, g2l = orc.batt_dispatch(load, pv, bank, power, cfg)
+    rs, rg = _py_dispatch(load, pv, bank, power, cfg, hourly)
+    assert np.allclose(sg, rs, rtol=1e-9, atol=1e-9)
+    assert np.allclose(g2l, rg, rtol=1e-9, atol=1e-9)
+
+
+def test_hourly_replan_differs_from_the_daily_plan_and_conserves_energy():
+    rng = np.random.default_rng(42)
+    hod = np.arange(orc.NH) % 24
+    load = 0.5 + 1.2 * np.exp(-((hod - 20) / 2.0) ** 2) + 0.2 * rng.random(orc.NH)
+    pv = np.maximum(0.0, np.sin((hod - 6) / 12 * np.pi)) * 3.0
+    day = orc.batt_dispatch(load, pv, 8.0, 2.0, orc.make_cfg())
+    hour = orc.batt_dispatch(load, pv, 8.0, 2.0, orc.make_cfg(batt_update_hours=1))
+    assert not np.allclose(day[1], hour[1])
+    for sg, g2l in (day, hour):
+        # grid import never exceeds the no-battery import, system output >= 0
+        assert (g2l <= np.maximum(load - pv, 0.0) + 1e-12).all() and (sg >= -1e-12).all()
+    # the rolling plan cuts the year's peak import at least as well here
+    assert hour[1].max() <= day[1].max() + 1e-9
+
+
+@pytest.mark.parametrize("unit", [0, 1, 2, 3])
+def test_oracle_kwh_per_kw_tiers_known_answer(unit):
+    """Tier caps by usage unit (oracle/orc.c month_energy_charge): a 2-tier
+    tariff, cap 100 (kWh, kWh/kW, kWh/day, kWh/kW/day), a flat 2 kW load with
+    one 5 kW hour per month: month peak 5 kW, usage 2 x hours + 3 kWh.  With a
+    PV system covering that hour the peak (and the kWh/kW caps) drop to 2 kW."""
+    from tests.helpers import oracle_tariffs
+    from dgen_amd.tariff import TariffTable
+    ones = [[1] * 24 for _ in range(12)]
+    tt = TariffTable()
+    tt.add({"ur_ec_tou_mat": [[1, 1, 100.0, unit, 0.1, 0.0], [1, 2, 1e38, unit, 0.3, 0.0]],
+            "ur_ec_sched_weekday": ones, "ur_ec_sched_weekend": ones, "ur_metering_option": 0}, False)
+    rec = tt.array()
+    assert int(rec["unit"][0]) == unit and not (int(rec["flags"][0]) & 0x08)
+    t = oracle_tariffs(rec)[0]
+    days = np.array([31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31], float)
+    start = np.concatenate([[0], np.cumsum(days)[:-1]]).astype(int) * 24
+    load = np.full(orc.NH, 2.0)
+    load[start + 18] = 5.0                      # one 5 kW evening hour per month
+    gen = np.zeros(orc.NH)
+    gen[start + 18] = 3.0                       # the system shaves exactly that hour
+    b1, b2 = np.float32(0.1), np.float32(0.3)   # the compile's float32 rates
+
+    def bill(peak):
+        use = 2.0 * days * 24 + 3.0 * (peak > 2.0)
+        cap = 100.0 * {0: 1.0, 1: peak, 2: 0.0, 3: peak}[unit] * (days if unit in (2, 3) else 1.0)
+        if unit == 2:
+            cap = 100.0 * days
+        lo = np.minimum(use, cap)
+        return float((lo * float(b1) + (use - lo) * float(b2)).sum())
+
+    r = orc.ur5(t, orc.make_cfg(), gen, load, None, 1, 0.0, 0.0, 0.0)
+    assert r["bill_wo"][1] == pytest.approx(bill(5.0), rel=1e-12)
+    assert r["bill_w"][1] == pytest.approx(bill(2.0), rel=1e-12)
+    if unit in (1, 3):       # the lower peak shrank the cheap tier: the 3 kWh saved are not all
+        assert bill(5.0) - r["bill_w"][1] < 12 * 3 * float(b2) - 1.0    # billed at the top rate

@@ -7,7 +7,7 @@ import os
 from dgen_amd import build as B
 from dgen_amd import spill_guard as G
 
-BAD = """_ZN12_GLOBAL__N_18k_size_wILi32ELb1EEEv11dgen_tablesPc:
+BAD = """_ZN12_GLOBAL__N_18k_size_wILi32ELb1ELb1ELb0EEEv11dgen_tablesPc:
 \tv_mov_b32_e32 v1, 0
 .LBB13_10:
 \tbuffer_inv sc1
@@ -19,7 +19,7 @@ BAD = """_ZN12_GLOBAL__N_18k_size_wILi32ELb1EEEv11dgen_tablesPc:
 \tglobal_load_dwordx4 v[4:7], v[116:117], off
 """
 
-GOOD = """_ZN12_GLOBAL__N_18k_size_wILi32ELb1EEEv11dgen_tablesPc:
+GOOD = """_ZN12_GLOBAL__N_18k_size_wILi32ELb1ELb1ELb0EEEv11dgen_tablesPc:
 .LBB13_11:
 \ts_or_b64 exec, exec, s[2:3]
 \tv_accvgpr_write_b32 a12, v244
@@ -30,7 +30,7 @@ GOOD = """_ZN12_GLOBAL__N_18k_size_wILi32ELb1EEEv11dgen_tablesPc:
 \ts_or_b64 exec, exec, s[4:5]
 """
 
-OTHER = BAD.replace("_ZN12_GLOBAL__N_18k_size_wILi32ELb1EEEv11dgen_tablesPc",
+OTHER = BAD.replace("_ZN12_GLOBAL__N_18k_size_wILi32ELb1ELb1ELb0EEEv11dgen_tablesPc",
                     "_ZN12_GLOBAL__N_113k_hourly_battILb1EEEv11dgen_tables")
 
 
