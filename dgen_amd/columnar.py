@@ -237,6 +237,26 @@ def assign_scratch(cols: Dict[str, np.ndarray], tariffs: np.ndarray, switches: n
     return int(need.sum())
 
 
+def _factorize_rows(*cols):
+    """(codes, first row of each distinct key) over the row tuples of `cols`,
+    keys numbered in order of first appearance -- the order a row-by-row pass
+    meets them; key equality is the dict's (identity, then ==).  None when a
+    key is unhashable."""
+    n = len(cols[0])
+    if n == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    try:
+        codes, uniq = pd.factorize(pd.Series(list(zip(*cols)), dtype=object), sort=False)
+    except TypeError:
+        return None
+    codes = np.asarray(codes, np.int64)
+    if (codes < 0).any():          # a NaN-like key pandas will not number: take the row path
+        return None
+    first = np.empty(len(uniq), np.int64)
+    first[codes[::-1]] = np.arange(n - 1, -1, -1, dtype=np.int64)
+    return codes, first
+
+
 def _num(series) -> np.ndarray:
     """float(x) per cell, NaN where that raises (financial_functions._finite_float)."""
     out = pd.to_numeric(series, errors="coerce")
@@ -256,23 +276,35 @@ def columnize_frame(df, src, rate_switch_table=None, skip_demand_charges=None) -
     cols = empty_columns(n)
     sector = df["sector_abbr"].tolist()
     state = df["state_abbr"].tolist() if "state_abbr" in df else [""] * n
-    is_ca = np.array([_is_ca(s) for s in state], bool)
-    is_res = np.array([s == "res" for s in sector], bool)
-    # profile rows: one lookup per distinct key
-    lk, sk = {}, {}
+    st_s = pd.Series(state, dtype=object)
+    is_ca = (st_s.where(st_s.notna(), "").astype(str).str.upper() == "CA").to_numpy(bool) if n else np.zeros(0, bool)
+    is_res = (pd.Series(sector, dtype=object) == "res").to_numpy(bool) if n else np.zeros(0, bool)
+    # profile rows: one lookup per distinct key (the store is append-only, so
+    # the key -> row maps are kept on it across calls)
     bldg, gid = df["bldg_id"].tolist(), df["solar_re_9809_gid"].tolist()
     tilt, az = df["tilt"].tolist(), df["azimuth"].tolist()
-    for i in range(n):
-        k1 = (bldg[i], sector[i], state[i])
-        r = lk.get(k1)
-        if r is None:
-            r = lk[k1] = src.load_row({"bldg_id": bldg[i], "sector_abbr": sector[i], "state_abbr": state[i]})
-        cols["load_row"][i] = r
-        k2 = (gid[i], tilt[i], az[i])
-        r = sk.get(k2)
-        if r is None:
-            r = sk[k2] = src.solar_row({"solar_re_9809_gid": gid[i], "tilt": tilt[i], "azimuth": az[i]})
-        cols["cf_row"][i] = r
+    lk = src.__dict__.setdefault("_columnar_load_rows", {})
+    sk = src.__dict__.setdefault("_columnar_solar_rows", {})
+
+    def rows_of(keys, cache, lookup):
+        f = _factorize_rows(*keys)
+        if f is None:
+            out = np.empty(n, np.int64)
+            for i, k in enumerate(zip(*keys)):
+                r = cache.get(k)
+                out[i] = r if r is not None else cache.setdefault(k, lookup(*k))
+            return out
+        codes, first = f
+        rows = np.empty(first.size, np.int64)
+        for j, i in enumerate(first.tolist()):
+            k = tuple(c[i] for c in keys)
+            r = cache.get(k)
+            rows[j] = r if r is not None else cache.setdefault(k, lookup(*k))
+        return rows[codes]
+    cols["load_row"] = rows_of((bldg, sector, state), lk, lambda b_, s_, t_: src.load_row(
+        {"bldg_id": b_, "sector_abbr": s_, "state_abbr": t_})).astype(cols["load_row"].dtype)
+    cols["cf_row"] = rows_of((gid, tilt, az), sk, lambda g_, t_, a_: src.solar_row(
+        {"solar_re_9809_gid": g_, "tilt": t_, "azimuth": a_})).astype(cols["cf_row"].dtype)
     # tariffs: content key once per distinct dict / string object
     from .tariff import tariff_key
     tdict = df["tariff_dict"].tolist()
@@ -285,28 +317,36 @@ def columnize_frame(df, src, rate_switch_table=None, skip_demand_charges=None) -
     # repeat these combinations (pandas merges share the objects), and
     # resolving a combination at its first row keeps the tariff and switch
     # tables in the row-by-row order of first use
-    memo: Dict[Tuple, Tuple[int, int, int, int, int]] = {}
-    res: List[Tuple[int, int, int, int, int]] = []
     ca_l = is_ca.tolist()
-    for i in range(n):
+
+    def resolve(i):
         raw, ca, e = tdict[i], ca_l[i], eia[i]
-        try:
-            ck = (id(raw), ca, e, sector[i])
-            hit = memo.get(ck)
-        except TypeError:          # unhashable eia_id: resolve the row on its own
-            ck, hit = None, None
-        if hit is None:
-            key = tkey.get(id(raw))
-            if key is None:
-                key = tkey[id(raw)] = tariff_key(raw)
-            t0 = b.tariffs.add(raw, ca, key=key)
-            so, sc = b.switches.candidates("solar", e, sector[i], ca)
-            to, tc = b.switches.candidates("storage", e, sector[i], ca)
-            hit = (t0, so, sc, to, tc)
-            if ck is not None:
-                memo[ck] = hit
-        res.append(hit)
-    res = np.array(res, np.int64).reshape(n, 5)
+        key = tkey.get(id(raw))
+        if key is None:
+            key = tkey[id(raw)] = tariff_key(raw)
+        t0 = b.tariffs.add(raw, ca, key=key)
+        so, sc = b.switches.candidates("solar", e, sector[i], ca)
+        to, tc = b.switches.candidates("storage", e, sector[i], ca)
+        return (t0, so, sc, to, tc)
+    f = _factorize_rows([id(x) for x in tdict], ca_l, eia, sector)
+    if f is not None:        # distinct combinations in first-use order, then mapped back
+        codes, first = f
+        res = np.array([resolve(i) for i in first.tolist()], np.int64).reshape(-1, 5)[codes]
+    else:                    # an unhashable eia_id: the row-by-row memo
+        memo: Dict[Tuple, Tuple[int, int, int, int, int]] = {}
+        out: List[Tuple[int, int, int, int, int]] = []
+        for i in range(n):
+            try:
+                ck = (id(tdict[i]), ca_l[i], eia[i], sector[i])
+                hit = memo.get(ck)
+            except TypeError:          # unhashable eia_id: resolve the row on its own
+                ck, hit = None, None
+            if hit is None:
+                hit = resolve(i)
+                if ck is not None:
+                    memo[ck] = hit
+            out.append(hit)
+        res = np.array(out, np.int64).reshape(n, 5)
     cols["tariff0"] = res[:, 0].astype(cols["tariff0"].dtype)
     cols["sw_solar_off"] = res[:, 1].astype(cols["sw_solar_off"].dtype)
     cols["sw_solar_cnt"] = res[:, 2].astype(cols["sw_solar_cnt"].dtype)

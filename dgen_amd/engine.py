@@ -439,12 +439,26 @@ def _staging(k: int, nbytes: int):
     return t
 
 
+_D2H_LOCK = None
+
+
 def hourly_to_host(t, inv=None, chunk: int = 4096, threads: Optional[int] = None) -> np.ndarray:
     """One hour-quad-tiled plane [NH/4][n][4] -> host [n][NH] (caller order when
     `inv` gathers it): per chunk of agents, a device gather into agent-major
     order, an async copy into one of two pinned staging buffers, and host
     threads copying the previous chunk out into the destination while the
-    next chunk crosses PCIe."""
+    next chunk crosses PCIe.  One download at a time (the staging buffers are
+    shared; HostPlane runs it on a background thread), on t's device."""
+    global _D2H_LOCK
+    import threading
+    if _D2H_LOCK is None:
+        _D2H_LOCK = threading.Lock()
+    torch = _torch()
+    with _D2H_LOCK, torch.cuda.device(t.device):
+        return _hourly_to_host(t, inv, chunk, threads)
+
+
+def _hourly_to_host(t, inv, chunk, threads):
     torch = _torch()
     import os
     from concurrent.futures import ThreadPoolExecutor
@@ -486,11 +500,86 @@ def hourly_to_host(t, inv=None, chunk: int = 4096, threads: Optional[int] = None
     return dst
 
 
-def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None) -> Dict[str, np.ndarray]:
+class HostPlane:
+    """An hourly plane on its way to the host: the download runs on a background
+    thread (pinned, chunked, threaded copy-out: hourly_to_host) while the caller
+    goes on; result() waits for it and returns the [n][8760] array.  The device
+    tensor is released once it has crossed."""
+
+    _pool = None
+
+    def __init__(self, t, inv):
+        from concurrent.futures import ThreadPoolExecutor
+        if HostPlane._pool is None:
+            HostPlane._pool = ThreadPoolExecutor(1, thread_name_prefix="dgen-plane")
+        self.n = int(t.shape[1])
+        self._fut = HostPlane._pool.submit(hourly_to_host, t, inv)
+        self._arr = None
+
+    def result(self) -> np.ndarray:
+        if self._arr is None:
+            self._arr = self._fut.result()
+            self._fut = None
+        return self._arr
+
+    def done(self) -> bool:
+        return self._arr is not None or self._fut.done()
+
+
+class HourlyRow:
+    """One agent's 8760-h series of a HostPlane, array-like: np.asarray(row)
+    (what the reference's consumers call, attachment_rate_functions.py:180-182),
+    len(), indexing, iteration and tolist() wait for the plane and read the
+    agent's row; pickling stores the plain array."""
+    __slots__ = ("_plane", "_i")
+
+    def __init__(self, plane: HostPlane, i: int):
+        self._plane, self._i = plane, i
+
+    def _row(self) -> np.ndarray:
+        return self._plane.result()[self._i]
+
+    def __array__(self, dtype=None, copy=None):
+        a = self._row()
+        if dtype is not None and np.dtype(dtype) != a.dtype:
+            return a.astype(dtype)
+        return a.copy() if copy else a
+
+    def __len__(self):
+        return _lib.NH
+
+    def __getitem__(self, k):
+        return self._row()[k]
+
+    def __iter__(self):
+        return iter(self._row())
+
+    def tolist(self):
+        return self._row().tolist()
+
+    @property
+    def shape(self):
+        return (_lib.NH,)
+
+    @property
+    def dtype(self):
+        return self._plane.result().dtype
+
+    def __reduce__(self):
+        return (np.array, (self._row(),))
+
+    def __repr__(self):
+        return f"HourlyRow({'ready' if self._plane.done() else 'downloading'}, agent {self._i})"
+
+
+def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None,
+                    hourly_async: bool = False) -> Dict[str, object]:
     """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly),
     in caller order when `perm` (AgentBatch.perm) is given.  The reorder to
     caller order (and the hourly tiles' transpose) is one device gather per
-    array, so each crosses PCIe once, already in its final layout."""
+    array, so each crosses PCIe once, already in its final layout.
+    hourly_async: the hourly planes come back as HostPlane (background
+    download) instead of arrays, the scalars and yearly arrays at once."""
     torch = _torch()
     res = {}
     inv = None
@@ -509,6 +598,8 @@ def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None) -
         t = out.get(name)
         if t is None:
             res[name] = None
+        elif hourly_async:
+            res[name] = HostPlane(t, inv)
         elif t.shape[1] >= 16384:         # large planes: pinned, chunked, threaded
             res[name] = hourly_to_host(t, inv)
         elif inv is None:

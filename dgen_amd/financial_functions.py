@@ -110,15 +110,16 @@ def _columnarize(rows, src: ProfileStore, rate_switch_table):
 
 def _raise_for_status(status: np.ndarray, agent_ids) -> None:
     """Raise like the reference for a chunk-fatal agent status.  Agents whose
-    tariff has kWh/kW tier units (ST_UNIT) are not fatal: they come back
-    unsized (NaN outputs, no-system hourly planes) with a warning, and the
-    rest of the chunk is sized."""
+    tariff bills kWh/kW tiers whose month peaks the batch cannot supply
+    (ST_UNIT: no demand record behind the tariff) are not fatal: they come
+    back unsized (NaN outputs, no-system hourly planes) with a warning, and
+    the rest of the chunk is sized."""
     unit = np.nonzero(status & _lib.ST_UNIT)[0]
     if unit.size:
         import warnings
         ids = [agent_ids[int(k)] for k in unit[:5]]
-        warnings.warn(f"{unit.size} agent(s) left unsized: tariff usage unit kWh/kW (tiers scaled by "
-                      f"peak demand) is not supported; NaN outputs (first: {ids})", RuntimeWarning,
+        warnings.warn(f"{unit.size} agent(s) left unsized: kWh/kW tiers without month peaks (no demand "
+                      f"record behind the tariff); NaN outputs (first: {ids})", RuntimeWarning,
                       stacklevel=3)
     bad = np.nonzero(status & ((_lib.ST_FATAL & ~_lib.ST_UNIT) | _lib.ST_ZERO_LOAD | _lib.ST_EMPTY_EC))[0]
     if bad.size == 0:
@@ -158,11 +159,13 @@ def _device_tables(eng, src: ProfileStore, b: PopulationBuilder):
 
 
 def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[dict] = None,
-                net_weights: Optional[Tuple[np.ndarray, np.ndarray]] = None):
+                net_weights: Optional[Tuple[np.ndarray, np.ndarray]] = None, hourly_async: bool = False):
     """Size the batch; net_weights = (number_of_adopters, non-adopters) per
     caller row also returns o["net_sum_kw"], size_chunk's hourly aggregate
     summed on the device from the planes in place (k_state_hourly, one
-    segment, fixed order) instead of a host loop over the agents."""
+    segment, fixed order) instead of a host loop over the agents.
+    hourly_async: the three hourly planes come back as engine.HostPlane
+    (downloading on a background thread), everything else at once."""
     import time
     import torch
     from .attachment import state_hourly
@@ -186,9 +189,10 @@ def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[
                            [0, batch.n])[0] * 1000.0
     torch.cuda.synchronize(eng.dev)
     t2 = time.perf_counter()
-    o = outputs_to_host(out, batch.perm)
+    o = outputs_to_host(out, batch.perm, hourly_async=hourly_async)
+    del out
     unsized = (o["status"] & _lib.ST_UNIT) != 0
-    if unsized.any():          # kWh/kW tier units: every sizing output NaN
+    if unsized.any():          # kWh/kW tiers without month peaks: every sizing output NaN
         for k, v in o.items():
             if v is not None and k not in _lib.OUTPUT_HOURLY and v.dtype.kind == "f":
                 v[unsized] = np.nan
@@ -303,18 +307,23 @@ def _yearly_lists(a: np.ndarray, n1: np.ndarray, fmt: str = "list"):
     return list(out)
 
 
-def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
+def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "array",
                timing: Optional[dict] = None, net_weights=None):
     """The batched form of calc_system_size_and_performance over a whole agent
     frame (what size_chunk needs), built by column: the frame is columnised
     at once (columnar.columnize_frame), sized in one device call, and the
     output columns are assigned whole.  Same values and columns as mapping
     calc_system_size_and_performance over the rows (ff:449-565 write order);
-    hourly: "list" (the reference's fp64 lists), "array" (each hourly and
-    yearly cell a float64 row view of one [n, 8760] / [n, years] array, no
-    per-agent copy and no per-value Python float) or "none" (no hourly
-    columns, yearly lists).  The
-    device computes the hourly planes in fp64 for this path.
+    hourly: "array" (the default: each hourly and yearly cell a float64 row
+    view of one [n, 8760] / [n, years] array, no per-agent copy and no
+    per-value Python float -- the reference's consumers read the cells with
+    np.asarray, attachment_rate_functions.py:180-182), "list" (the
+    reference's fp64 lists), "lazy" (hourly cells are engine.HourlyRow
+    array-likes whose plane is still crossing PCIe on a background thread
+    when the frame is returned; np.asarray(cell) waits for it) or "none" (no
+    hourly columns, yearly lists).  The device computes the hourly planes in
+    fp64 for this path; their download (the PCIe-bound phase: 3 x 8760 x 8 B
+    per agent) overlaps the assembly of the frame.
     timing: filled with the host / device phases (seconds)."""
     import time
     if rate_switch_table is None:
@@ -326,7 +335,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     cols = b.frame_columns
     t1 = time.perf_counter()
     dev_t: dict = {}
-    o = _run_device(b, cols, src, dev_t, net_weights)
+    o = _run_device(b, cols, src, dev_t, net_weights, hourly_async=hourly != "none")
     t2 = time.perf_counter()
     ids = df["agent_id"].tolist() if "agent_id" in df else list(df.index)
     _raise_for_status(o["status"], ids)
@@ -361,9 +370,18 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     out["cf_energy_value_pv_batt"] = _yearly_lists(o["cfev_batt"], n1, yfmt)
     out["utility_bill_w_sys_pv_batt"] = _yearly_lists(o["bill_w_batt"], n1, yfmt)
     out["utility_bill_wo_sys_pv_batt"] = _yearly_lists(o["bill_wo_batt"], n1, yfmt)
+    t_wait = 0.0
     if hourly != "none":
-        conv = ((lambda a: a.tolist()) if hourly == "list"
-                else (lambda a: list(a)))
+        from .engine import HourlyRow
+
+        def conv(plane):
+            nonlocal t_wait
+            if hourly == "lazy":
+                return [HourlyRow(plane, i) for i in range(plane.n)]
+            tw = time.perf_counter()
+            a = plane.result()
+            t_wait += time.perf_counter() - tw
+            return a.tolist() if hourly == "list" else list(a)
         out["baseline_net_hourly"] = conv(o["baseline"])
         out["adopter_net_hourly_pvonly"] = conv(o["net_pvonly"])
         out["adopter_net_hourly_with_batt"] = conv(o["net_with_batt"])
@@ -379,12 +397,14 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "list",
     out["batt_kwh"] = o["batt_kwh"]
     t3 = time.perf_counter()
     if timing is not None:
-        timing.update(columnize_s=t1 - t0, device_call_s=t2 - t1, output_frame_s=t3 - t2, **dev_t)
+        # download_wait_s: time the frame assembly waited for the hourly planes
+        timing.update(columnize_s=t1 - t0, device_call_s=t2 - t1, output_frame_s=t3 - t2,
+                      download_wait_s=t_wait, **dev_t)
     return out, o
 
 
 def size_chunk(static_agents_df: pd.DataFrame, sectors, rate_switch_table, mode="simple",
-               hourly: str = "list", timing: Optional[dict] = None):
+               hourly: str = "array", timing: Optional[dict] = None):
     """ff:1136 -- size a chunk; returns (df_out, agg) with
     agg["net_sum_kw"][h] = sum_agents adopter[h] * n_adopt + baseline[h] * (n_cust - n_adopt)."""
     global _worker_conn

@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import ast
 import json
+from collections import OrderedDict
 import re
 from dataclasses import dataclass
 from typing import Any, Dict, Iterable, List, Optional, Tuple
@@ -573,6 +574,27 @@ def tariff_key(raw) -> str:
         return "r:" + repr(raw)
 
 
+_COMPILE_CACHE: "OrderedDict[Tuple[str, bool, Any], CompiledTariff]" = OrderedDict()
+_COMPILE_CACHE_MAX = 8192
+
+
+def _compiled(raw, key: str, is_ca: bool, skip_demand_charges) -> CompiledTariff:
+    """compile_tariff, memoised across tables by the tariff's content (a chunk
+    loop meets the same tariffs call after call): a copy of the records, so a
+    table may set its own `dc`."""
+    ck = (key if key[:2] in ("s:", "j:", "r:") else tariff_key(raw), is_ca, skip_demand_charges)
+    ct = _COMPILE_CACHE.get(ck)
+    if ct is None:
+        ct = compile_tariff(raw, is_ca, skip_demand_charges)
+        _COMPILE_CACHE[ck] = ct
+        if len(_COMPILE_CACHE) > _COMPILE_CACHE_MAX:
+            _COMPILE_CACHE.popitem(last=False)
+    else:
+        _COMPILE_CACHE.move_to_end(ck)
+    return CompiledTariff(fields=ct.fields, record=ct.record.copy(),
+                          demand=None if ct.demand is None else ct.demand.copy())
+
+
 class TariffTable:
     """Deduplicating table of compiled tariffs (one entry per (tariff, CA?)).
     With demand charges on, tariffs that carry them get a ``dgen_demand``
@@ -592,7 +614,7 @@ class TariffTable:
         hit = self._index.get(key)
         if hit is not None:
             return hit
-        ct = compile_tariff(raw, bool(is_ca), self.skip_demand_charges)
+        ct = _compiled(raw, key[0], bool(is_ca), self.skip_demand_charges)
         if ct.demand is not None:
             self.demand.append(ct.demand)
             ct.record["dc"] = len(self.demand)

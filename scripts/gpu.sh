@@ -18,6 +18,7 @@
 #   loop       bench_loop.py (LOOP_ARGS) and its kernel trace
 #   rehearse   2-rank gloo rehearsal of the N > 1 bench.py and bench_loop.py flows
 #   dropin     bench_dropin.py (DROPIN_ARGS)
+#   diag       scripts/diag_pop.py per DIAG entry ("config:n[:replan_hours]")
 #
 # Every GPU step runs under its own timeout; a crash-type exit (fault, abort,
 # segfault, time limit) ends the session, an assertion failure in the tests
@@ -51,7 +52,7 @@ GROUPS_=("FETCH_SIZE" "WRITE_SIZE"
 for step in "$@"; do
   case $step in
   tests)
-    timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 \
+    timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} -m gpu ${PYTEST_X--x} -v --timeout 300 \
       --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
     echo "pytest gpu rc=$rc"; grep -E "passed|failed|error" $O/pytest_gpu.log | tail -3; stop $rc;;
   smoke)
@@ -113,6 +114,12 @@ for step in "$@"; do
       --master-addr 127.0.0.1 --master-port 29534 bench_loop.py ${REH_LOOP_ARGS:---agents 200000 --years 3} \
       > $O/bench_loop_n2_gloo.log 2>&1; rc=$?
     echo "bench_loop n2 gloo rc=$rc"; tail -2 $O/bench_loop_n2_gloo.log | cut -c1-600; stop $rc;;
+  diag)
+    for d in ${DIAG:-com_8m:160}; do
+      IFS=: read -r cfg n rh <<< "$d"
+      timeout -k 10 300 python -u scripts/diag_pop.py $cfg $n ${rh:-24} > $O/diag_${cfg}_${n}_${rh:-24}.log 2>&1; rc=$?
+      echo "diag $d rc=$rc"; head -12 $O/diag_${cfg}_${n}_${rh:-24}.log; stop $rc
+    done;;
   dropin)
     timeout -k 10 600 python -u bench_dropin.py ${DROPIN_ARGS:-} > $O/bench_dropin.log 2>&1; rc=$?
     echo "dropin rc=$rc"; tail -4 $O/bench_dropin.log | cut -c1-600; stop $rc;;

@@ -127,3 +127,24 @@ def test_size_chunk_array_mode_equals_list_mode():
         for a, l in zip(arr[k], lst[k]):
             assert isinstance(a, np.ndarray) and a.dtype == np.float64, k
             assert np.array_equal(a, np.asarray(l, np.float64)), k
+
+
+def test_size_chunk_lazy_mode_equals_array_mode():
+    """hourly="lazy": the hourly cells are array-likes whose plane downloads in
+    the background; np.asarray(cell), len, indexing and pickling give the
+    array mode's values exactly."""
+    import pickle
+    rows, store, table = helpers.golden_rows()
+    df = pd.DataFrame(rows)
+    ff._worker_conn = store
+    arr, agg_a = ff.size_chunk(df, None, table, "simple", hourly="array")
+    lz, agg_l = ff.size_chunk(df, None, table, "simple", hourly="lazy")
+    assert agg_a["net_sum_kw"] == agg_l["net_sum_kw"]
+    for k in ("baseline_net_hourly", "adopter_net_hourly_pvonly", "adopter_net_hourly_with_batt",
+              "adopter_net_hourly"):
+        for a, c in zip(arr[k], lz[k]):
+            assert len(c) == 8760 and c[17] == a[17]
+            assert np.array_equal(np.asarray(c, dtype=float), a), k
+            assert np.array_equal(pickle.loads(pickle.dumps(c)), a), k
+    for k in SCALARS + ["payback_period"]:
+        assert np.array_equal(arr[k].to_numpy(float), lz[k].to_numpy(float)), k
