@@ -2116,27 +2116,83 @@ __device__ bool yl_dc_build(const dgen_demand* D, const YSrc& src, double tlo, d
     return g.first(!ok) < 0;
 }
 
+// The agent's envelope lines staged in the wave's LDS (k_size): an evaluation
+// reads every present group's few lines, and from global memory each read was
+// a dependent L2 round trip inside the month / group loops (the C4 k_size was
+// latency-bound: SQ_WAIT_ANY ~4.6x its VALU instructions).  The groups' lines
+// are packed in group order, off[k] .. off[k + 1] for group k = m x DCP + p.
+constexpr int DCS_CAP = 128;                       // lines per agent (else the global path)
+constexpr int DCS_NG = 12 * DCP;
+struct DcStage {
+    double2 lines[DCS_CAP];
+    uint16_t off[DCS_NG + 1];
+    uint16_t pad[(8 - (DCS_NG + 1) % 8) % 8];
+};
+constexpr size_t DCS_BYTES = sizeof(DcStage);
+static_assert(DCS_BYTES % 16 == 0, "stage keeps 16-B alignment");
+
+// Stage the envelope the segment just built (yl_dc_build's global record):
+// lane sl takes groups sl, sl + LPA, ...; offsets by a segment scan in group
+// order.  Segment-uniform result: false when the lines exceed DCS_CAP.
+template <int LPA>
+__device__ bool yl_dc_stage(const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
+    constexpr int PER = (DCS_NG + LPA - 1) / LPA;
+    int cnt[PER], off[PER];
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int k = g.sl + j * LPA;
+        const int v = k < DCS_NG ? E.cnt[k] : 0;
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < LPA; o <<= 1) {
+            const int t = __shfl_up(incl, o, WAVE);
+            if (g.sl >= o) incl += t;
+        }
+        cnt[j] = v;
+        off[j] = base + incl - v;
+        base += __shfl(incl, g.base + LPA - 1, WAVE);
+    }
+    if (base > DCS_CAP) return false;
+    wave_lds_sync();                                   // the previous stage is no longer read
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int k = g.sl + j * LPA;
+        if (k < DCS_NG) {
+            st->off[k] = (uint16_t)off[j];
+            const double2* src = E.lines + (size_t)k * DC_NL;
+            for (int l = 0; l < cnt[j]; l++) st->lines[off[j] + l] = src[l];
+        }
+    }
+    if (g.sl == 0) st->off[DCS_NG] = (uint16_t)base;
+    wave_lds_sync();
+    return true;
+}
+
 // One lane's year of demand charges from the envelopes (same month / period /
 // tier order as yl_demand): system output x s at system kW kw (ref_gen, the
 // reference's operation order), or the no-system peaks (max load) when !with_gen.
+// st: the agent's staged lines (or nullptr: the global record).
 __device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& E, double kw, double s,
-                                             bool with_gen, const YLds& S) {
+                                             bool with_gen, const YLds& S, const DcStage* st = nullptr) {
     double total = 0.0;
     for (int m = 0; m < 12; m++) {
         double flat = 0.0;
         for (int q = 0; q < DCP; q++) {
-            const int n_l = E.cnt[m * DCP + q];
+            const int gk = m * DCP + q;
+            const int o0 = (st && with_gen) ? st->off[gk] : 0;
+            const int n_l = (st && with_gen) ? st->off[gk + 1] - o0 : E.cnt[gk];
             double pk = 0.0;
             if (n_l > 0) {
                 if (with_gen) {
-                    const double2* ln = E.lines + (m * DCP + q) * DC_NL;
+                    const double2* ln = st ? st->lines + o0 : E.lines + gk * DC_NL;
                     for (int k = 0; k < n_l; k++) {
                         const double2 v = ln[k];
                         const double imp = v.x - ref_gen(v.y, kw) * s;
                         pk = imp > pk ? imp : pk;
                     }
                 } else {
-                    pk = E.maxl[m * DCP + q];
+                    pk = E.maxl[gk];
                 }
             }
             S.at(q) = pk;
@@ -2751,6 +2807,8 @@ struct YCtx {
     bool dem_wo_pending;        // wo1 still lacks the new tariff's demand charge
     bool env_ok;                // the demand envelopes of the current tariff fit
     DcEnv env;                  // the agent's envelope storage
+    DcStage* stg;               // the segment's LDS stage of the envelope lines (k_size)
+    bool stg_ok;                // the current envelope is staged
     char* nb;                   // the agent's net-billing split record (or nullptr)
     bool nb_ok;                 // the split of the current (mo 2) tariff fits
     double tlo, thi;            // generation-scale range of the search
@@ -2800,6 +2858,7 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
             // the envelopes are built and the no-system pass runs here (its
             // charge, when billed, joins the no-system bill below)
             c.env_ok = c.env.lines && yl_dc_build(c.dem, c.src, c.tlo, c.thi, c.env, c.g);
+            c.stg_ok = c.env_ok && c.stg && yl_dc_stage(c.env, c.stg, c.g);
             const double v0 = c.env_ok ? yl_dc_eval(c.dem, c.env, 0.0, 1.0, false, c.S)
                                        : yl_demand(c.dem, c.src, 0.0, 1.0, false, c.S);
             wo_dem = c.dem_bill ? v0 : 0.0;
@@ -2856,7 +2915,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
             // kWh/kW tiers: this evaluation's month peaks (and demand charge)
             // ahead of the energy bill, whose tier caps scale with them
             c.src.gen_scale = kws;
-            const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, c.s_y, true, c.S)
+            const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, c.s_y, true, c.S, c.stg_ok ? c.stg : nullptr)
                                       : yl_demand(c.dem, c.src, kw, c.s_y, true, c.S);
             v13 = c.dem_bill ? v : 0.0;
         }
@@ -2881,11 +2940,14 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
             // one inlined demand pass for both uses: the no-system charge of a
             // newly set tariff (pass 0, once), then this evaluation's (pass 1)
             c.src.gen_scale = kws;
-            if (c.dem_wo_pending) c.env_ok = c.env.lines && yl_dc_build(c.dem, c.src, c.tlo, c.thi, c.env, c.g);
+            if (c.dem_wo_pending) {
+                c.env_ok = c.env.lines && yl_dc_build(c.dem, c.src, c.tlo, c.thi, c.env, c.g);
+                c.stg_ok = c.env_ok && c.stg && yl_dc_stage(c.env, c.stg, c.g);
+            }
             for (int pass = c.dem_wo_pending ? 0 : 1; pass < 2; pass++) {
                 const bool wg = pass == 1;
                 const double s = wg ? c.s_y : 1.0;
-                const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, s, wg, c.S)
+                const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, s, wg, c.S, c.stg_ok ? c.stg : nullptr)
                                           : yl_demand(c.dem, c.src, kw, s, wg, c.S);
                 if (wg) wb += v;
                 else c.wo1 += v;
@@ -2943,8 +3005,13 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.dem_wo_pending = false;
     c.env_ok = false;
     c.env.lines = nullptr;
+    c.stg = nullptr;
+    c.stg_ok = false;
     if constexpr (DC) {
         if (dcws) c.env = dc_env_at(dcws, i);
+        // the segment's envelope stage sits after the year-lane layout
+        c.stg = reinterpret_cast<DcStage*>(reinterpret_cast<char*>(dyn_lds) +
+                                           ylds_bytes(half, LPA, PK && T.peak_units != 0)) + lane / LPA;
     }
     {
         const int slot = A.scratch_slot[i];
@@ -3984,7 +4051,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     const bool pk = dc && T->peak_units != 0;       // kWh/kW tiers: the PK instantiations
     const int lpa_s = (fits32 && !(pk ? DGEN_NO2_SIZE_PK : dc ? DGEN_NO2_SIZE_DC : DGEN_NO2_SIZE)) ? 32 : WAVE;
     const int lpa_f = (fits32 && !(pk ? DGEN_NO2_FIN_PK : dc ? DGEN_NO2_FIN_DC : DGEN_NO2_FIN)) ? 32 : WAVE;
-    const size_t ylds_s = ylds_bytes(lds_half(T->max_periods), lpa_s, pk);
+    const size_t ylds_s = ylds_bytes(lds_half(T->max_periods), lpa_s, pk) +
+                          (dc ? (size_t)(WAVE / lpa_s) * DCS_BYTES : 0);   // k_size's envelope stage
     // k_batt_finance's demand-charge instantiations stage hours per segment
     const size_t ylds_f = ylds_bytes(lds_half(T->max_periods), lpa_f, pk) +
                           (dc ? (size_t)(WAVE / lpa_f) * DEM_STAGE_BYTES : 0);
