@@ -526,52 +526,6 @@ class HostPlane:
         return self._arr is not None or self._fut.done()
 
 
-class HourlyRow:
-    """One agent's 8760-h series of a HostPlane, array-like: np.asarray(row)
-    (what the reference's consumers call, attachment_rate_functions.py:180-182),
-    len(), indexing, iteration and tolist() wait for the plane and read the
-    agent's row; pickling stores the plain array."""
-    __slots__ = ("_plane", "_i")
-
-    def __init__(self, plane: HostPlane, i: int):
-        self._plane, self._i = plane, i
-
-    def _row(self) -> np.ndarray:
-        return self._plane.result()[self._i]
-
-    def __array__(self, dtype=None, copy=None):
-        a = self._row()
-        if dtype is not None and np.dtype(dtype) != a.dtype:
-            return a.astype(dtype)
-        return a.copy() if copy else a
-
-    def __len__(self):
-        return _lib.NH
-
-    def __getitem__(self, k):
-        return self._row()[k]
-
-    def __iter__(self):
-        return iter(self._row())
-
-    def tolist(self):
-        return self._row().tolist()
-
-    @property
-    def shape(self):
-        return (_lib.NH,)
-
-    @property
-    def dtype(self):
-        return self._plane.result().dtype
-
-    def __reduce__(self):
-        return (np.array, (self._row(),))
-
-    def __repr__(self):
-        return f"HourlyRow({'ready' if self._plane.done() else 'downloading'}, agent {self._i})"
-
-
 def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None,
                     hourly_async: bool = False) -> Dict[str, object]:
     """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly),

@@ -307,23 +307,26 @@ def _yearly_lists(a: np.ndarray, n1: np.ndarray, fmt: str = "list"):
     return list(out)
 
 
-def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "array",
+def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
                timing: Optional[dict] = None, net_weights=None):
     """The batched form of calc_system_size_and_performance over a whole agent
     frame (what size_chunk needs), built by column: the frame is columnised
     at once (columnar.columnize_frame), sized in one device call, and the
     output columns are assigned whole.  Same values and columns as mapping
     calc_system_size_and_performance over the rows (ff:449-565 write order);
-    hourly: "array" (the default: each hourly and yearly cell a float64 row
-    view of one [n, 8760] / [n, years] array, no per-agent copy and no
-    per-value Python float -- the reference's consumers read the cells with
-    np.asarray, attachment_rate_functions.py:180-182), "list" (the
-    reference's fp64 lists), "lazy" (hourly cells are engine.HourlyRow
-    array-likes whose plane is still crossing PCIe on a background thread
-    when the frame is returned; np.asarray(cell) waits for it) or "none" (no
-    hourly columns, yearly lists).  The device computes the hourly planes in
-    fp64 for this path; their download (the PCIe-bound phase: 3 x 8760 x 8 B
-    per agent) overlaps the assembly of the frame.
+    hourly: "lazy" (the default: every series column is an
+    hourly_column.RowColumn, a pandas extension array built in O(1) -- an
+    hourly cell is the agent's float64 row of a plane that is still crossing
+    PCIe on a background thread when the frame is returned (reading a cell
+    waits for it), a yearly cell the agent's Python list, made when read; the
+    reference's consumers read hourly cells with len() and np.asarray,
+    attachment_rate_functions.py:166-182, and yearly cells as lists,
+    finance_series_export.py:51-64), "array" (the planes on the host before
+    returning: hourly and yearly cells float64 row views -- the reference's
+    own finance export skips non-list cells), "list" (the reference's fp64
+    lists throughout) or "none" (no hourly columns, yearly lists).  The device
+    computes the hourly planes in fp64 for this path (the PCIe-bound phase:
+    3 x 8760 x 8 B per agent), downloaded while the frame is assembled.
     timing: filled with the host / device phases (seconds)."""
     import time
     if rate_switch_table is None:
@@ -343,11 +346,17 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "array",
     if "agent_id" not in out.columns:
         out.insert(len(out.columns), "agent_id", list(df.index))
     n1 = df["economic_lifetime_yrs"].astype(np.int64).to_numpy() + 1
-    yfmt = "array" if hourly == "array" else "list"
+    from .hourly_column import hourly_column, yearly_column
+    if hourly == "lazy":
+        def ycol(a):     # O(1): lists made when a cell is read
+            return pd.Series(yearly_column(a, n1), index=out.index, copy=False)
+    else:
+        def ycol(a):
+            return _yearly_lists(a, n1, "array" if hourly == "array" else "list")
     out["naep"] = o["naep"]
-    out["cf_energy_value_pv_only"] = _yearly_lists(o["cfev_pv"], n1, yfmt)
-    out["utility_bill_w_sys_pv_only"] = _yearly_lists(o["bill_w_pv"], n1, yfmt)
-    out["utility_bill_wo_sys_pv_only"] = _yearly_lists(o["bill_wo_pv"], n1, yfmt)
+    out["cf_energy_value_pv_only"] = ycol(o["cfev_pv"])
+    out["utility_bill_w_sys_pv_only"] = ycol(o["bill_w_pv"])
+    out["utility_bill_wo_sys_pv_only"] = ycol(o["bill_wo_pv"])
     sw = np.nonzero(o["switched"] != 0)[0]
     if sw.size:
         # elec.py:852-855: the sticky switch rewrites the agent in place
@@ -367,17 +376,16 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "array",
         if tid is not None:
             out["tariff_id"] = pd.Series(tid, index=out.index).infer_objects()
         out["tariff_dict"] = pd.Series(tdi, index=out.index)
-    out["cf_energy_value_pv_batt"] = _yearly_lists(o["cfev_batt"], n1, yfmt)
-    out["utility_bill_w_sys_pv_batt"] = _yearly_lists(o["bill_w_batt"], n1, yfmt)
-    out["utility_bill_wo_sys_pv_batt"] = _yearly_lists(o["bill_wo_batt"], n1, yfmt)
+    out["cf_energy_value_pv_batt"] = ycol(o["cfev_batt"])
+    out["utility_bill_w_sys_pv_batt"] = ycol(o["bill_w_batt"])
+    out["utility_bill_wo_sys_pv_batt"] = ycol(o["bill_wo_batt"])
     t_wait = 0.0
     if hourly != "none":
-        from .engine import HourlyRow
-
         def conv(plane):
             nonlocal t_wait
             if hourly == "lazy":
-                return [HourlyRow(plane, i) for i in range(plane.n)]
+                # O(1): the column is the plane and its row index
+                return pd.Series(hourly_column(plane), index=out.index, copy=False)
             tw = time.perf_counter()
             a = plane.result()
             t_wait += time.perf_counter() - tw
@@ -392,7 +400,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "array",
     out["price_per_kwh"] = o["price_per_kwh"]
     out["npv"] = o["npv"]
     out["payback_period"] = o["payback_period"]
-    out["cash_flow"] = _yearly_lists(o["cash_flow"], n1, yfmt)
+    out["cash_flow"] = ycol(o["cash_flow"])
     out["batt_kw"] = o["batt_kw"]
     out["batt_kwh"] = o["batt_kwh"]
     t3 = time.perf_counter()
@@ -404,7 +412,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "array",
 
 
 def size_chunk(static_agents_df: pd.DataFrame, sectors, rate_switch_table, mode="simple",
-               hourly: str = "array", timing: Optional[dict] = None):
+               hourly: str = "lazy", timing: Optional[dict] = None):
     """ff:1136 -- size a chunk; returns (df_out, agg) with
     agg["net_sum_kw"][h] = sum_agents adopter[h] * n_adopt + baseline[h] * (n_cust - n_adopt)."""
     global _worker_conn

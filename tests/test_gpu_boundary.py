@@ -130,9 +130,9 @@ def test_size_chunk_array_mode_equals_list_mode():
 
 
 def test_size_chunk_lazy_mode_equals_array_mode():
-    """hourly="lazy": the hourly cells are array-likes whose plane downloads in
-    the background; np.asarray(cell), len, indexing and pickling give the
-    array mode's values exactly."""
+    """hourly="lazy" (the default): the hourly cells are rows of a plane that
+    downloads in the background; np.asarray(cell), len, indexing and pickling
+    give the array mode's values exactly."""
     import pickle
     rows, store, table = helpers.golden_rows()
     df = pd.DataFrame(rows)
@@ -148,3 +148,8 @@ def test_size_chunk_lazy_mode_equals_array_mode():
             assert np.array_equal(pickle.loads(pickle.dumps(c)), a), k
     for k in SCALARS + ["payback_period"]:
         assert np.array_equal(arr[k].to_numpy(float), lz[k].to_numpy(float)), k
+    # yearly cells: Python lists, as the reference's finance export requires
+    # (finance_series_export.py:51-64), with the array mode's values
+    for k in ARRAYS:
+        for a, c in zip(arr[k], lz[k]):
+            assert isinstance(c, list) and c == a.tolist(), k
