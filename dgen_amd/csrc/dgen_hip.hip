@@ -1886,7 +1886,7 @@ constexpr size_t DEM_STAGE_BYTES = sizeof(DemStage);
 static_assert(DEM_STAGE_BYTES % 16 == 0, "stage keeps 16-B alignment");
 
 template <int LPA>
-__device__ double yl_demand_staged(const dgen_demand* D, const YSrc& src, double s, bool with_gen,
+__device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const YSrc& src, double s, bool with_gen,
                                    const YLds& S, DemStage* st, const Seg<LPA>& g) {
     constexpr int HPL = DEM_BATCH / LPA;              // hours each lane stages (1 or 2)
     const uint64_t segmask = LPA == WAVE ? ~0ull : (((1ull << LPA) - 1ull) << g.base);
@@ -2043,7 +2043,7 @@ __device__ __forceinline__ DcEnv dc_env_at(void* base, int64_t i) {
 // over the month per demand period present).  Returns true when every group
 // fit in DC_NL lines (segment-uniform).
 template <int LPA>
-__device__ bool yl_dc_build(const dgen_demand* D, const YSrc& src, double tlo, double thi,
+__device__ __forceinline__ bool yl_dc_build(const dgen_demand* D, const YSrc& src, double tlo, double thi,
                             const DcEnv& E, const Seg<LPA>& g) {
     bool ok = true;
     const int m = g.sl;
@@ -2135,7 +2135,7 @@ static_assert(DCS_BYTES % 16 == 0, "stage keeps 16-B alignment");
 // lane sl takes groups sl, sl + LPA, ...; offsets by a segment scan in group
 // order.  Segment-uniform result: false when the lines exceed DCS_CAP.
 template <int LPA>
-__device__ bool yl_dc_stage(const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
+__device__ __forceinline__ bool yl_dc_stage(const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
     constexpr int PER = (DCS_NG + LPA - 1) / LPA;
     int cnt[PER], off[PER];
     int base = 0;

@@ -35,6 +35,9 @@ VARIANTS = {
     # whose whole need fits, wave-days where it fits for all lanes, saturated)
     "phase_day": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
                   ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1")],
+    # k_size evaluates the demand envelopes from the global record, not the LDS stage
+    "no_dcstage": [("    {\n        const int slot = A.scratch_slot[i];\n        c.nb = (nbws",
+                    "    c.stg = nullptr;\n    {\n        const int slot = A.scratch_slot[i];\n        c.nb = (nbws")],
     "db_cf4": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 4")],
     "db_cf12": [("#define DGEN_NB_DB_CF 6", "#define DGEN_NB_DB_CF 12")],
     "hb_w3": [(HB, occ(HB, 3))],
