@@ -418,8 +418,13 @@ __host__ __device__ inline char* ws_nb(void* base, int64_t n, int64_t n_scratch)
 
 // Phase timers (DGEN_PHASE_PROF=1 ablation builds only): per-segment shader
 // cycles spent in a phase, summed over segments, read by dgen_phase_read.
-// Slots 0-15: year-lane kernels; with DGEN_DAY_COUNTERS, 12-15 count
-// k_hourly_batt day targets instead.
+// Slots 0-15: year-lane kernels -- 0 k_size, 1 set_tariff's net-billing split
+// build or demand envelopes (build + stage), 2 / 3 net-billing evaluation
+// (split / hourly) or 3 the demand-charge evaluation, 4 k_batt_finance, 5 / 6
+// its split build / evaluation or 5 its staged demand pass, 7 / 8 split builds
+// / evaluations counted (or envelope builds / demand evaluations), 9 Brent evaluations, 10 / 11 split entries visited /
+// their loop, 12-15 NEM set_tariff, NEM bill, cash flow, prologue.  With
+// DGEN_DAY_COUNTERS, 12-15 count k_hourly_batt day targets instead.
 #ifndef DGEN_PHASE_PROF
 #define DGEN_PHASE_PROF 0
 #endif
@@ -2169,6 +2174,180 @@ __device__ __forceinline__ bool yl_dc_stage(const DcEnv& E, DcStage* st, const S
     return true;
 }
 
+// The same envelopes built by the segment's hour lanes (k_size: the serial
+// month-lane build above was 60 % of the C4 search's cycles, each month lane
+// walking its 730 hours twice per demand period).  Lane hd < 24 takes hour of
+// day hd of every day, whose demand period is fixed per day type, so one walk
+// over the year serves every period: pass 1 keeps, per day type, the lane's
+// first maximiser of the import at tlo and at thi and its max load; the
+// segment merges the 48 partials per (month, period) through LDS (ties to the
+// earlier hour: the serial build's first maximiser); pass 2 appends the lines
+// above the crossing bound (an LDS counter per period hands out positions:
+// the envelope is a set, evaluations take its max).  Same lines kept, same
+// overflow rule as yl_dc_build.  Loads run DCB_DAYS days ahead (the serial
+// build waited on an L2 round trip per 4 hours).  `st`: the segment's stage,
+// free while the envelope is rebuilt, holds the partials (240 doubles), the
+// per-period bounds (16) and the counters.
+// Per-day-type running maximisers of one hour lane (pass 1)
+struct DcPart {
+    double av, aL, ag, bv, bL, bg, mL;
+    int ah, bh;
+};
+__device__ __forceinline__ void dc_part_init(DcPart& q) {
+    q.av = -INFINITY; q.aL = 0.0; q.ag = 0.0; q.bv = -INFINITY; q.bL = 0.0; q.bg = 0.0; q.mL = 0.0;
+    q.ah = 0x7fffffff; q.bh = 0x7fffffff;
+}
+__device__ __forceinline__ void dc_part_add(DcPart& q, double L, double gp, int h, double tlo, double thi) {
+    q.mL = L > q.mL ? L : q.mL;
+    const double vlo = L - gp * tlo, vhi = L - gp * thi;
+    if (vlo > q.av) { q.av = vlo; q.aL = L; q.ag = gp; q.ah = h; }
+    if (vhi > q.bv) { q.bv = vhi; q.bL = L; q.bg = gp; q.bh = h; }
+}
+constexpr int DCB_DAYS = 8;          // days of loads in flight per hour lane
+
+template <int LPA>
+__device__ __forceinline__ bool yl_dc_build_coop(const dgen_demand* D, const YSrc& src, double tlo, double thi,
+                                                 const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
+    static_assert(sizeof(DcStage) >= 256 * sizeof(double), "stage holds the build's partials");
+    double* const part = reinterpret_cast<double*>(st);          // [10][24]: 9 fields + the lane's period
+    double* const prm = part + 240;                               // [2][DCP]: ts, Ms (pass 2)
+    int* const ctr = reinterpret_cast<int*>(part);                // [DCP] (pass 2: partials are dead)
+    const int hd = g.sl;
+    const bool act = hd < 24;
+    const int hq = act ? hd : 23;                                 // in-range loads for idle lanes
+    bool ok = true;
+    for (int m = 0; m < 12; m++) {
+        const int d0 = c_month_start_day[m], d1 = c_month_start_day[m + 1];
+        const int pd = (int)D->wkday[m][hq], pe = (int)D->wkend[m][hq];
+        uint32_t mask = act ? (1u << pd) | (1u << pe) : 0u;
+#pragma unroll
+        for (int o = 1; o < LPA; o <<= 1) mask |= (uint32_t)__shfl_xor((int)mask, o, WAVE);
+        // pass 1: the month's days in batches, both day types at once (the
+        // day type is segment-uniform, so the branch picks one partial)
+        DcPart qw, qe;
+        dc_part_init(qw);
+        dc_part_init(qe);
+        for (int db = d0; db < d1; db += DCB_DAYS) {
+            float sv[DCB_DAYS];
+            int32_t cv[DCB_DAYS];
+#pragma unroll
+            for (int k = 0; k < DCB_DAYS; k++) {
+                const int d = db + k < d1 ? db + k : d1 - 1;
+                sv[k] = src.shape[d * 24 + hq];
+                cv[k] = src.cf[d * 24 + hq];
+            }
+#pragma unroll
+            for (int k = 0; k < DCB_DAYS; k++) {
+                const int d = db + k;
+                if (d >= d1) break;
+                const double L = (double)sv[k] * src.load_scale;
+                const double gp = cf_per_kw(cv[k]);
+                if ((d % 7) >= 5) dc_part_add(qe, L, gp, d * 24 + hd, tlo, thi);
+                else dc_part_add(qw, L, gp, d * 24 + hd, tlo, thi);
+            }
+        }
+        // merge the 24 lanes' partials per period: reduction lane r = period r
+        const bool red = hd < DCP && ((mask >> hd) & 1u);
+        double A = -INFINITY, AL = 0.0, Ag = 0.0, B = -INFINITY, BL = 0.0, Bg = 0.0, ML = 0.0;
+        int AH = 0x7fffffff, BH = 0x7fffffff;
+        for (int dt = 0; dt < 2; dt++) {
+            const DcPart& q = dt ? qe : qw;
+            wave_lds_sync();
+            if (act) {
+                part[0 * 24 + hd] = q.av; part[1 * 24 + hd] = q.aL; part[2 * 24 + hd] = q.ag;
+                part[3 * 24 + hd] = (double)q.ah;
+                part[4 * 24 + hd] = q.bv; part[5 * 24 + hd] = q.bL; part[6 * 24 + hd] = q.bg;
+                part[7 * 24 + hd] = (double)q.bh; part[8 * 24 + hd] = q.mL;
+                part[9 * 24 + hd] = (double)(dt ? pe : pd);
+            }
+            wave_lds_sync();
+            if (red) {
+                for (int k = 0; k < 24; k++) {
+                    if ((int)part[9 * 24 + k] != hd) continue;
+                    const double v = part[0 * 24 + k], w = part[4 * 24 + k];
+                    const int kh = (int)part[3 * 24 + k], kb = (int)part[7 * 24 + k];
+                    if (v > A || (v == A && kh < AH)) { A = v; AL = part[1 * 24 + k]; Ag = part[2 * 24 + k]; AH = kh; }
+                    if (w > B || (w == B && kb < BH)) { B = w; BL = part[5 * 24 + k]; Bg = part[6 * 24 + k]; BH = kb; }
+                    const double ml = part[8 * 24 + k];
+                    ML = ml > ML ? ml : ML;
+                }
+            }
+        }
+        // the period's crossing bound (yl_dc_build's pass-1 hand-over)
+        double ts = tlo, Ms = 0.0;
+        if (red) {
+            if (Ag > Bg) {
+                ts = (AL - BL) / (Ag - Bg);
+                ts = ts < tlo ? tlo : (ts > thi ? thi : ts);
+            }
+            const double va = AL - Ag * ts, vb = BL - Bg * ts;
+            Ms = va > vb ? va : vb;
+            Ms -= 1e-10 * (fabs(AL) + fabs(BL) + 1.0);               // the slack
+            E.lines[(m * DCP + hd) * DC_NL] = make_double2(AL, Ag);
+            E.lines[(m * DCP + hd) * DC_NL + 1] = make_double2(BL, Bg);
+        }
+        wave_lds_sync();
+        if (red) { prm[hd] = ts; prm[DCP + hd] = Ms; }
+        wave_lds_sync();
+        // each lane's two periods' bounds and excluded hours
+        const double tw = prm[pd], mw = prm[DCP + pd], te = prm[pe], me = prm[DCP + pe];
+        const int aw = __shfl((int)AH, g.base + pd, WAVE), bw = __shfl((int)BH, g.base + pd, WAVE);
+        const int ae = __shfl((int)AH, g.base + pe, WAVE), be = __shfl((int)BH, g.base + pe, WAVE);
+        wave_lds_sync();
+        if (hd < DCP) ctr[hd] = 2;
+        wave_lds_sync();
+        // pass 2: the lines above the bound
+        for (int db = d0; db < d1; db += DCB_DAYS) {
+            float sv[DCB_DAYS];
+            int32_t cv[DCB_DAYS];
+#pragma unroll
+            for (int k = 0; k < DCB_DAYS; k++) {
+                const int d = db + k < d1 ? db + k : d1 - 1;
+                sv[k] = src.shape[d * 24 + hq];
+                cv[k] = src.cf[d * 24 + hq];
+            }
+#pragma unroll
+            for (int k = 0; k < DCB_DAYS; k++) {
+                const int d = db + k;
+                if (d >= d1) break;
+                const bool we = (d % 7) >= 5;
+                const int h = d * 24 + hd;
+                const double L = (double)sv[k] * src.load_scale;
+                const double gp = cf_per_kw(cv[k]);
+                const double t_ = we ? te : tw, M_ = we ? me : mw;
+                const int a_ = we ? ae : aw, b_ = we ? be : bw, pp = we ? pe : pd;
+                if (act && h != a_ && h != b_ && L - gp * t_ > M_) {
+                    const int pos = atomicAdd(&ctr[pp], 1);
+                    if (pos < DC_NL) E.lines[(m * DCP + pp) * DC_NL + pos] = make_double2(L, gp);
+                    else ok = false;
+                }
+            }
+        }
+        wave_lds_sync();
+        if (hd < DCP) {
+            const bool here = (mask >> hd) & 1u;
+            const int n_l = here ? ctr[hd] : 0;
+            E.cnt[m * DCP + hd] = n_l < DC_NL ? n_l : DC_NL;
+            E.maxl[m * DCP + hd] = here ? ML : 0.0;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return g.first(!ok) < 0;
+}
+
+// k_size's build: the hour-lane form when the segment has its stage
+#ifndef DGEN_DC_SERIAL
+#define DGEN_DC_SERIAL 0
+#endif
+template <int LPA>
+__device__ __forceinline__ bool yl_dc_build_any(const dgen_demand* D, const YSrc& src, double tlo, double thi,
+                                                const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
+    if (!DGEN_DC_SERIAL && st) return yl_dc_build_coop(D, src, tlo, thi, E, st, g);
+    return yl_dc_build(D, src, tlo, thi, E, g);
+}
+
 // One lane's year of demand charges from the envelopes (same month / period /
 // tier order as yl_demand): system output x s at system kW kw (ref_gen, the
 // reference's operation order), or the no-system peaks (max load) when !with_gen.
@@ -2857,7 +3036,7 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
             // kWh/kW tiers: the month peaks come before the energy bills, so
             // the envelopes are built and the no-system pass runs here (its
             // charge, when billed, joins the no-system bill below)
-            c.env_ok = c.env.lines && yl_dc_build(c.dem, c.src, c.tlo, c.thi, c.env, c.g);
+            c.env_ok = c.env.lines && yl_dc_build_any(c.dem, c.src, c.tlo, c.thi, c.env, c.stg, c.g);
             c.stg_ok = c.env_ok && c.stg && yl_dc_stage(c.env, c.stg, c.g);
             const double v0 = c.env_ok ? yl_dc_eval(c.dem, c.env, 0.0, 1.0, false, c.S)
                                        : yl_demand(c.dem, c.src, 0.0, 1.0, false, c.S);
@@ -2941,9 +3120,13 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
             // newly set tariff (pass 0, once), then this evaluation's (pass 1)
             c.src.gen_scale = kws;
             if (c.dem_wo_pending) {
-                c.env_ok = c.env.lines && yl_dc_build(c.dem, c.src, c.tlo, c.thi, c.env, c.g);
+                PH_T0(tdb);
+                c.env_ok = c.env.lines && yl_dc_build_any(c.dem, c.src, c.tlo, c.thi, c.env, c.stg, c.g);
                 c.stg_ok = c.env_ok && c.stg && yl_dc_stage(c.env, c.stg, c.g);
+                PH_ADD(1, tdb, c.g.sl == 0);          // demand envelopes: build + stage
+                PH_CNT(7, 1, c.g.sl == 0);
             }
+            PH_T0(tde);
             for (int pass = c.dem_wo_pending ? 0 : 1; pass < 2; pass++) {
                 const bool wg = pass == 1;
                 const double s = wg ? c.s_y : 1.0;
@@ -2952,6 +3135,8 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
                 if (wg) wb += v;
                 else c.wo1 += v;
             }
+            PH_ADD(3, tde, c.g.sl == 0);              // demand-charge evaluation
+            PH_CNT(8, 1, c.g.sl == 0);
             c.dem_wo_pending = false;
         }
     }
@@ -3258,12 +3443,14 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             if (!same_tariff) wo1 += v0;
         }
     } else if (DC && dem) {   // k_size's first_without already carries the no-system demand charge
+        PH_T0(tds);
         for (int pass = same_tariff ? 1 : 0; pass < 2; pass++) {
             const bool wg = pass == 1;
             const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);
             if (wg) wb += v;
             else wo1 += v;
         }
+        PH_ADD(5, tds, g.sl == 0);                // battery-case staged demand pass
     }
     double w = wb * r_y;
     double wo = wo1 * r_y;

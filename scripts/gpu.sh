@@ -74,7 +74,7 @@ for step in "$@"; do
       k=$((k+1)); lib=""; args="$v"
       case "$v" in lib=*) lib="${v%% *}"; lib="${lib#lib=}"; args="${v#* }";; esac
       if [ -n "$lib" ]; then export DGEN_LIB=$R/ablate/libdgen_$lib.so; else unset DGEN_LIB; fi
-      case "$lib" in phase*) export DGEN_PHASE_PROF=1;; *) unset DGEN_PHASE_PROF;; esac
+      case "$lib" in phase*|dcb_*) export DGEN_PHASE_PROF=1;; *) unset DGEN_PHASE_PROF;; esac
       timeout -k 10 400 python bench.py $args > $O/ab_$k.log 2>&1; rc=$?
       echo "== [$v] rc=$rc"; line $O/ab_$k.log; stop $rc
     done

@@ -35,6 +35,17 @@ VARIANTS = {
     # whose whole need fits, wave-days where it fits for all lanes, saturated)
     "phase_day": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
                   ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1")],
+    # k_size builds the demand envelopes with the serial month lanes
+    "dc_serial": [("#define DGEN_DC_SERIAL 0", "#define DGEN_DC_SERIAL 1")],
+    # timing probes of the hour-lane envelope build (wrong results by construction)
+    "dcb_nopass2": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
+                    ("        // pass 2: the lines above the bound, per day type\n        for (int dt = 0; dt < 2; dt++) {",
+                     "        // pass 2: the lines above the bound, per day type\n        for (int dt = 0; dt < 0; dt++) {")],
+    "dcb_noload": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
+                   ("                    const double L = (double)src.shape[h] * src.load_scale;\n                    const double gp = cf_per_kw(src.cf[h]);\n                    mL = L > mL",
+                    "                    const double L = (double)(h & 255) * src.load_scale;\n                    const double gp = cf_per_kw(h * 77);\n                    mL = L > mL"),
+                   ("                    const double L = (double)src.shape[h] * src.load_scale;\n                    const double gp = cf_per_kw(src.cf[h]);\n                    if (h != pah",
+                    "                    const double L = (double)(h & 255) * src.load_scale;\n                    const double gp = cf_per_kw(h * 77);\n                    if (h != pah")],
     # k_size evaluates the demand envelopes from the global record, not the LDS stage
     "no_dcstage": [("    {\n        const int slot = A.scratch_slot[i];\n        c.nb = (nbws",
                     "    c.stg = nullptr;\n    {\n        const int slot = A.scratch_slot[i];\n        c.nb = (nbws")],
