@@ -22,6 +22,7 @@ import numpy as np
 import pandas as pd
 
 from . import _lib
+from .hourly_column import RowColumn
 
 TABLE = "agent_finance_series"
 NORM = 25
@@ -83,6 +84,16 @@ def _as_float_list(x):
         return None
 
 
+def _stage_rows(col: RowColumn, dst: np.ndarray) -> None:
+    """A RowColumn's cells into dst [n][STRIDE], zero past each cell's length."""
+    a = col.to_2d()
+    k = min(a.shape[1], STRIDE)
+    dst[:, :k] = a[:, :k]
+    ln = col.cell_lens()
+    if (ln < k).any():
+        dst[np.arange(STRIDE)[None, :] >= ln[:, None]] = 0.0
+
+
 def export_agent_finance_series(engine, schema, owner, year: int, df_agents: pd.DataFrame,
                                 writer: Optional[Callable] = None, dev_engine=None):
     """finance_series_export.py:22 -- one record per agent and case, returned
@@ -101,11 +112,17 @@ def export_agent_finance_series(engine, schema, owner, year: int, df_agents: pd.
     eng = _engine(dev_engine)
     # stage the lists zero-padded to [6][n][51] (the first 25 entries are kept;
     # shorter lists are already zero past their end, so the kernel's list
-    # length is the full stride)
+    # length is the full stride).  A series column of the drop-in's frames
+    # (hourly_column.RowColumn) is staged whole from its [n][w] rows; any other
+    # column cell by cell as the reference reads it.
     host = np.zeros((6, n, STRIDE), dtype=np.float64)
     present = np.zeros((2, n), dtype=bool)
     for ci, (case, cols) in enumerate(CASES):
         for si, c in enumerate(cols):
+            if c in df.columns and isinstance(df[c].array, RowColumn):
+                _stage_rows(df[c].array, host[3 * ci + si])
+                present[ci] |= df[c].array.cells_are_lists()              # :54-56, 66-68
+                continue
             col = df[c].tolist() if c in df.columns else [None] * n   # r.get(c) is None
             for r, v in enumerate(col):
                 present[ci, r] |= isinstance(v, (list, tuple))            # :54-56, 66-68
@@ -117,18 +134,16 @@ def export_agent_finance_series(engine, schema, owner, year: int, df_agents: pd.
     dev = torch.from_numpy(host).to(eng.dev)
     c_out = _lib.Outputs(**{f: dev[j].data_ptr() for j, f in enumerate(OUT_FIELDS)})
     res = _run(eng, c_out, np.full(n, STRIDE, dtype=np.int32), n).cpu().numpy()
-    aid = df["agent_id"].tolist() if "agent_id" in df.columns else [-1] * n
-    recs = []
-    for r in range(n):                                                   # :50-73 iterrows order
-        for ci, (case, _) in enumerate(CASES):
-            if present[ci, r]:
-                rec = {"agent_id": int(aid[r]), "year": int(year), "scenario_case": case}
-                for si, s in enumerate(SERIES):
-                    rec[s] = res[3 * ci + si, r].tolist()
-                recs.append(rec)
-    if not recs:
+    aid = (df["agent_id"].to_numpy() if "agent_id" in df.columns else np.full(n, -1)).astype(np.int64)
+    # records in iterrows order (:50-73): per row its pv_only, then its pv_batt
+    r_idx, c_idx = np.nonzero(present.T)
+    if r_idx.size == 0:
         return None
-    out = pd.DataFrame.from_records(recs)
+    rec = {"agent_id": aid[r_idx].tolist(), "year": [int(year)] * r_idx.size,
+           "scenario_case": [CASES[c][0] for c in c_idx.tolist()]}
+    for si, s in enumerate(SERIES):
+        rec[s] = res[3 * c_idx + si, r_idx].tolist()
+    out = pd.DataFrame(rec)
     if writer is not None:
         writer(out, engine, schema, owner, TABLE, if_exists="append", append_transformations=False)
     return out

@@ -181,6 +181,14 @@ class RowColumn(ExtensionArray):
             return np.full(len(self), self._rows().shape[1], dtype=np.int64)
         return self._lens[self._idx]
 
+    def cell_lens(self) -> np.ndarray:
+        """Each cell's length (the row width where no lengths are kept)."""
+        return self._cell_lens()
+
+    def cells_are_lists(self) -> bool:
+        """True when cells read as Python lists (the reference's yearly cells)."""
+        return self._lists
+
     def ready(self) -> bool:
         """True once the rows are on the host (reading a cell will not wait)."""
         return self._plane.done()

@@ -34,3 +34,24 @@ def test_golden_covers_edges():
     assert any(isinstance(r["cf_energy_value_pv_only"], np.ndarray) for r in c["rows"])
     assert any(not np.all(np.isfinite(r["utility_bill_w_sys_pv_batt"])) for r in c["rows"]
                if isinstance(r["utility_bill_w_sys_pv_batt"], list))
+
+
+def test_row_column_staging_matches_cell_staging():
+    """finance_series._stage_rows (a yearly RowColumn staged whole) equals the
+    cell-by-cell staging of the same lists: first 51 entries, zero past each
+    list's end."""
+    from dgen_amd import finance_series as gfs
+    from dgen_amd.hourly_column import yearly_column
+    rng = np.random.default_rng(3)
+    n = 200
+    a = rng.normal(size=(n, 60))
+    lens = rng.integers(0, 61, n)
+    col = yearly_column(a, lens)[::-1]
+    got = np.full((n, gfs.STRIDE), 7.0)
+    gfs._stage_rows(col, got)
+    ref = np.zeros((n, gfs.STRIDE))
+    for r, v in enumerate(col):
+        k = min(len(v), gfs.STRIDE)
+        ref[r, :k] = v[:k]
+    assert np.array_equal(got, ref)
+    assert col.cells_are_lists()

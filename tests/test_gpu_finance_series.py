@@ -63,3 +63,29 @@ def test_series_from_sizing_outputs(engine):
             for i in range(batch.n):
                 ref = ofs.norm25(list(h[key][i, :life[i] + 1]))   # the agent's 26-long list
                 assert np.array_equal(g[i], np.asarray(ref)), (case, key, i)
+
+
+def test_export_stages_series_columns_whole(engine):
+    """The drop-in's yearly columns (hourly_column.RowColumn: cells are lists of
+    N + 1 values) are staged whole; the records equal those of the same frame
+    with plain list cells (the reference's form)."""
+    from dgen_amd.hourly_column import yearly_column
+    rng = np.random.default_rng(5)
+    n = 300
+    lens = rng.integers(10, 52, n)
+    cols = {}
+    for _, names in gfs.CASES:
+        for c in names:
+            a = rng.normal(size=(n, 51)) * 100
+            a[rng.random((n, 51)) < 0.02] = np.inf
+            cols[c] = a
+    aid = rng.permutation(10_000)[:n]
+    fast = pd.DataFrame({"agent_id": aid, **{c: yearly_column(a, lens) for c, a in cols.items()}})
+    slow = pd.DataFrame({"agent_id": aid, **{c: [list(a[i, :lens[i]]) for i in range(n)]
+                                             for c, a in cols.items()}})
+    got = gfs.export_agent_finance_series(None, "s", "o", 2030, fast, dev_engine=engine)
+    ref = gfs.export_agent_finance_series(None, "s", "o", 2030, slow, dev_engine=engine)
+    assert len(got) == 2 * n == len(ref)
+    assert got[["agent_id", "year", "scenario_case"]].equals(ref[["agent_id", "year", "scenario_case"]])
+    for k in gfs.SERIES:
+        assert all(np.array_equal(np.asarray(a), np.asarray(b)) for a, b in zip(got[k], ref[k])), k
