@@ -18,6 +18,7 @@ MAXP = 12
 MAXT = 6
 MAXY = 50
 NB_CAPM = 192   # include/dgen_hip.h DGEN_NB_CAPM (mixed hours per month of a net-billing record)
+DCR_CAP = 1024  # include/dgen_hip.h DGEN_DCR_CAP (kept hours per battery-case demand record)
 
 ST_BOUNDS = 0x01
 ST_TARIFF = 0x02
@@ -54,6 +55,7 @@ class Tables(ctypes.Structure):
         ("n_shapes", _i64), ("n_cfs", _i64), ("n_wholesale", _i64), ("n_switches", _i64),
         ("n_tariffs", _i32), ("max_periods", _i32),
         ("demand", _vp), ("n_demand", _i32), ("peak_units", _i32),
+        ("max_dc_periods", _i32), ("pad_t", _i32),
     ]
 
 
@@ -101,7 +103,7 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
-ABI_VERSION = 7   # include/dgen_hip.h DGEN_ABI_VERSION
+ABI_VERSION = 8   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
 
@@ -109,7 +111,7 @@ EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
     "dgen_kernel_times", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
-    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
+    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_set_dc_records", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
     "dgen_finance_series", "dgen_year_inputs", "dgen_initial_market_shares",
 ]
 
@@ -162,6 +164,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.dgen_set_battery.argtypes = [_vp, _i32]
     L.dgen_set_nb_scan.restype = _i32
     L.dgen_set_nb_scan.argtypes = [_vp, _i32]
+    L.dgen_set_dc_records.restype = _i32
+    L.dgen_set_dc_records.argtypes = [_vp, _i32]
     L.dgen_segment_sums.restype = _i32
     L.dgen_segment_sums.argtypes = [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _vp, _i64, _vp, _vp]
     if L.dgen_abi_version() != ABI_VERSION:

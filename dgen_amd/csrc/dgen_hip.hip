@@ -510,6 +510,44 @@ __device__ __forceinline__ NbRec nb_rec(char* p) {
 }
 
 
+// Battery-case demand records (k_hourly_batt<.., DCR = true> -> k_batt_finance):
+// per scratch slot, what the battery-case demand pass needs from the hours,
+// built in the scan as the system output is produced.  Per (month, demand
+// period): mxl = the max load (the no-system peak, exact) and lb = the running
+// max over the hours of min(import at s_lo, import at s_hi) -- every year
+// lane's import is between those two (fl(L - fl(sys s)) is monotone in s), so
+// lb bounds every lane's peak from below; and in hour order the hours whose
+// max(import at s_lo, import at s_hi) exceeds lb as it stood before them
+// (16-B entries: system output, float32 shape value, period).  An hour not
+// kept is at or below an earlier hour's import on every lane, so the lanes'
+// peaks over the kept hours from 0 equal their peaks over all hours (maxima:
+// bit-identical), and they may start from lb.  ~49 kept hours per agent-month
+// on the C4 population (of 730; a study on the oracle's dispatch), against the
+// staged pass's 8760 hours per lane group.  Entries of all months share one
+// list (off[m] .. off[m + 1]); a list beyond DCR_CAP sets flag 2 and the
+// finance kernel takes the staged pass over the system-output plane.
+constexpr int DCR_CAP = DGEN_DCR_CAP;
+struct DcrRec {
+    double* lb;      // [12][DCP]
+    double* mxl;     // [12][DCP]
+    int* off;        // [13] entry offsets per month (running count)
+    int* flag;       // 1: this step's scan built the record, 2: overflow, 0: none
+    NbEntC* ent;     // [DCR_CAP]
+};
+constexpr size_t DCR_HEAD = (size_t)2 * 12 * DCP * sizeof(double) + 64;
+constexpr size_t DCR_BYTES = DCR_HEAD + (size_t)DCR_CAP * sizeof(NbEntC);
+static_assert(DCR_BYTES % 16 == 0, "per-slot demand records stay 16-B aligned");
+__device__ __forceinline__ DcrRec dcr_rec(char* base, int64_t slot) {
+    char* p = base + (size_t)slot * DCR_BYTES;
+    DcrRec r;
+    r.lb = reinterpret_cast<double*>(p);
+    r.mxl = r.lb + 12 * DCP;
+    r.off = reinterpret_cast<int*>(p + (size_t)2 * 12 * DCP * sizeof(double));
+    r.flag = r.off + 13;
+    r.ent = reinterpret_cast<NbEntC*>(p + DCR_HEAD);
+    return r;
+}
+
 // ---------------------------------------------------------------------------
 // k_hourly_batt: one sequential scan over the year per agent
 // ---------------------------------------------------------------------------
@@ -778,11 +816,14 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 // lane), so the network appears once per hour of the day (~27k instructions),
 // and the form runs one wave per SIMD: the window, its sorted copy and both
 // days' raw values need ~400 registers.
-template <bool HOURLY, bool F64, bool NB, bool ROLL>
+// DCR: the batch bills demand charges (or kWh/kW tier peaks) and has room for
+// the battery-case demand records (dcr: DCR_BYTES per scratch slot, dc_nq the
+// batch's demand periods, which size the scan's per-period LDS maxima).
+template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR>
 __global__ void __launch_bounds__(BLOCK, ROLL ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
-              int repair) {
+              int repair, char* dcr, int dc_nq, int dcr_cap) {
     // agents [i0, i1) of a batch of n (row stride of every plane stays n),
     // months [m_lo, m_hi) of the year: the year is swept in month segments,
     // one launch each, so that every resident wave works on the same weeks
@@ -791,11 +832,17 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     int64_t i = i0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= i1) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
-    // repair pass: only the agents whose scan-built split overflowed and whose
-    // system-output plane was therefore not written (flag 2) run again, with
-    // the plane; every other output it writes is the same value again
-    if (repair && !(A.scratch_slot[i] >= 0 &&
-                    nbr_flag(ws_nb(ws, n, n_scratch) + (size_t)A.scratch_slot[i] * NB_BYTES) == 2)) return;
+    // repair pass: only the agents whose scan-built split (repair bit 1) or
+    // demand record (bit 2) overflowed and whose system-output plane was
+    // therefore not written (flag 2) run again, with the plane; every other
+    // output it writes is the same value again
+    if (repair) {
+        const int sl = A.scratch_slot[i];
+        const bool need = sl >= 0 &&
+            (((repair & 1) && nbr_flag(ws_nb(ws, n, n_scratch) + (size_t)sl * NB_BYTES) == 2) ||
+             ((repair & 2) && dcr && *dcr_rec(dcr, sl).flag == 2));
+        if (!need) return;
+    }
     WsLayout W = ws_layout(ws, n);
     // battery-case bins: (load, system output) pairs per period, [p][BLOCK]
     double2* bins = reinterpret_cast<double2*>(dyn_lds) + threadIdx.x;
@@ -864,10 +911,37 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             nbr = nb_rec(ws_nb(ws, n, n_scratch) + (size_t)slot * NB_BYTES);
         }
     }
+    // battery-case demand record (DcrRec) over the schedule the finance kernel
+    // bills with: the kWh/kW tier peaks' record where the batch bills those,
+    // else the tariff's demand charges; the year lanes' degradation range
+    // [dc_lo, dc_hi] as in the finance kernel (s_y for y = 1 .. N)
+    bool put_dcr = false;
+    DcrRec dr{nullptr, nullptr, nullptr, nullptr, nullptr};
+    const dgen_demand* dcd = nullptr;
+    double dc_lo = 1.0, dc_hi = 1.0;
+    int n_d = 0;
+    if constexpr (DCR) {
+        if (dcr && slot >= 0 && !repair) {
+            dr = dcr_rec(dcr, slot);
+            const dgen_demand* pkd = T.peak_units ? tariff_peaks(T.demand, T.n_demand, t) : nullptr;
+            dcd = pkd ? pkd : tariff_demand(T, cfg, t);
+            put_dcr = put_sys && dcd != nullptr;
+            if (m_lo == 0) { *dr.flag = 0; dr.off[0] = 0; }
+            if (put_dcr) {
+                const int N = A.econ_life[i];
+                const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+                const double sN = pow_seq(sys_base, (N >= 1 && N <= MAXY) ? N - 1 : 0);
+                dc_lo = sN < 1.0 ? sN : 1.0;
+                dc_hi = sN > 1.0 ? sN : 1.0;
+                n_d = m_lo == 0 ? 0 : dr.off[m_lo];
+            }
+        }
+    }
     // the split replaces the system-output plane for the energy bill; demand
     // charges still read the plane, and an overflowing split gets it from the
-    // repair pass
-    const bool skip_plane = put_nb && !has_dc;
+    // repair pass.  A demand record replaces it for an agent billed from bins
+    // (NEM: the energy bill does not read hours), the same way.
+    const bool skip_plane = (put_nb && !has_dc) || (DCR && put_dcr && !mo2);
 
     const double inv_eta_in = 1.0 / cfg.batt_eta_in;
     const double in_per_bank = bank > 0.0 ? cfg.batt_eta_in / bank : 0.0;
@@ -917,8 +991,12 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // read-back are inline asm: the compiler would otherwise order every LDS
     // access of the kernel (the bins) behind a vmcnt(0).  Per wave: 12 chunks
     // x 64 lanes x 16 B = HB_DAY_BYTES.  (ISA check: DESIGN.md section 5.)
+    // DCR: per-period (max load, lb) pairs [dc_nq][BLOCK] after the bins
+    double2* const dcb = reinterpret_cast<double2*>(reinterpret_cast<char*>(dyn_lds) +
+                         (size_t)(NB ? 32 : 16) * lds_half(T.max_periods) * BLOCK) + threadIdx.x;
     const uint32_t dbase = (uint32_t)(size_t)(lds_ptr_t)(reinterpret_cast<char*>(dyn_lds) +
                            (size_t)(NB ? 32 : 16) * lds_half(T.max_periods) * BLOCK +
+                           (DCR ? (size_t)16 * dc_nq * BLOCK : 0) +
                            (size_t)(threadIdx.x / 64) * HB_DAY_BYTES);
     const uint32_t dbase_s = __builtin_amdgcn_readfirstlane(dbase);
     const uint32_t dlane = dbase_s + (threadIdx.x & 63u) * 16u;
@@ -964,6 +1042,20 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             swd[0] = a[0]; swd[1] = a[1]; swd[2] = a[2];
             swe[0] = b[0]; swe[1] = b[1]; swe[2] = b[2];
         }
+        // DCR: the month's demand-period rows, loaded with the energy rows; the
+        // current period's (max load, lb) in registers like the bins
+        uint64_t dsd[3] = {0, 0, 0}, dse[3] = {0, 0, 0};
+        int dq = 0;
+        double2 dacc = make_double2(0.0, 0.0);
+        const int d_first = n_d;                      // the month's first kept hour
+        (void)d_first;
+        if (DCR && put_dcr) {
+            const uint64_t* a = reinterpret_cast<const uint64_t*>(dcd->wkday[m]);
+            const uint64_t* b = reinterpret_cast<const uint64_t*>(dcd->wkend[m]);
+            dsd[0] = a[0]; dsd[1] = a[1]; dsd[2] = a[2];
+            dse[0] = b[0]; dse[1] = b[1]; dse[2] = b[2];
+            for (int q = 0; q < dc_nq; q++) dcb[q * BLOCK] = make_double2(0.0, 0.0);
+        }
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             if (ROLL && d > d_lo) day_reread(dlane, r);    // the DMA was waited for yesterday
             else if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);
@@ -971,6 +1063,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             const bool wkend = (d % 7) >= 5;
             const uint64_t sched[3] = {wkend ? swe[0] : swd[0], wkend ? swe[1] : swd[1],
                                        wkend ? swe[2] : swd[2]};
+            const uint64_t dsch[3] = {wkend ? dse[0] : dsd[0], wkend ? dse[1] : dsd[1],
+                                      wkend ? dse[2] : dsd[2]};
+            (void)dsch;
             double target = 0.0;
             if constexpr (ROLL) {
                 // the window at the day's first hour is the day itself; then the
@@ -1054,6 +1149,30 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                         q16 += row16;
                     }
                 }
+                if constexpr (DCR) {
+                    if (put_dcr) {
+                        int q = (int)((dsch[hh >> 3] >> (8 * (hh & 7))) & 0xffu);
+                        q = q < DCP ? q : 0;
+                        if (q != dq) {
+                            dcb[dq * BLOCK] = dacc;
+                            dq = q;
+                            dacc = dcb[q * BLOCK];
+                        }
+                        const double i_lo = ld - st.sys * dc_lo, i_hi = ld - st.sys * dc_hi;
+                        if (fmax(i_lo, i_hi) > dacc.y) {       // may raise some lane's peak
+                            if (n_d < dcr_cap) {
+                                NbEntC e;
+                                e.g = st.sys;
+                                e.sh = r.s[hh];
+                                e.p = q;
+                                dr.ent[n_d] = e;
+                            }
+                            n_d++;
+                        }
+                        dacc.x = fmax(dacc.x, ld);
+                        dacc.y = fmax(dacc.y, fmin(i_lo, i_hi));
+                    }
+                }
                 qs[hh & 3] = st.sys;
                 if ((hh & 3) == 3) {
                     if (put_sys && !skip_plane) {               // tile [h / 4][slot][4]
@@ -1113,6 +1232,31 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             }
             nbr.cnt[m] = n_m <= nb_cap ? n_m : NB_CAPM + 1;     // > NB_CAPM: overflow
         }
+        if (DCR && put_dcr) {
+            dcb[dq * BLOCK] = dacc;
+            for (int q = 0; q < dc_nq; q++) {
+                const double2 v = dcb[q * BLOCK];
+                dr.mxl[m * DCP + q] = v.x;
+                dr.lb[m * DCP + q] = v.y;
+            }
+            // the month's kept hours against its final lower bounds: an hour at
+            // or below lb on both ends is at or below every lane's peak (~1.5 %
+            // of the month's hours stay, of ~7 % kept while lb was rising)
+            if (n_d <= dcr_cap) {
+                int w = d_first;
+                for (int k = d_first; k < n_d; k++) {
+                    const NbEntC e = dr.ent[k];
+                    const double L = (double)e.sh * ls;
+                    const double a = L - e.g * dc_lo, b = L - e.g * dc_hi;
+                    if (fmax(a, b) > dcb[e.p * BLOCK].y) {
+                        if (w != k) dr.ent[w] = e;
+                        w++;
+                    }
+                }
+                n_d = w;
+            }
+            dr.off[m + 1] = n_d;
+        }
         if (!mo2) bins[bcur * BLOCK] = bacc;
         if (!mo2) {
             // agent-major (load, system) pairs: k_batt_finance's lanes read the
@@ -1126,6 +1270,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
         W.carry[n + i] = annual;
         return;
     }
+    // 1: the record holds every kept hour; 2: it overflowed and the plane was
+    // not written (the repair pass writes it); 3: overflowed, plane written
+    if (DCR && put_dcr) *dr.flag = n_d <= dcr_cap ? 1 : (skip_plane ? 2 : 3);
     // the record holds this scan's battery-case split (1: k_batt_finance skips
     // its build), or it overflowed without a plane (2: the repair pass writes
     // the plane, k_batt_finance builds from it), or neither (0)
@@ -1890,9 +2037,16 @@ struct DemStage {
 constexpr size_t DEM_STAGE_BYTES = sizeof(DemStage);
 static_assert(DEM_STAGE_BYTES % 16 == 0, "stage keeps 16-B alignment");
 
+// R: the same pass over the agent's battery-case demand record (DcrRec, built
+// by k_hourly_batt) instead of the system-output plane: each month's lanes
+// start from the record's lower bounds lb and stage only its kept hours
+// (entries off[m] .. off[m + 1], segment-specific trip counts: the ballots and
+// the stage are per segment), with the filter below.  The no-system pass
+// (with_gen false) is the record's max loads, no hours at all.
 template <int LPA>
 __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const YSrc& src, double s, bool with_gen,
-                                   const YLds& S, DemStage* st, const Seg<LPA>& g) {
+                                   const YLds& S, DemStage* st, const Seg<LPA>& g,
+                                   bool REC = false, const DcrRec& R = DcrRec{}, int nq = DCP) {
     constexpr int HPL = DEM_BATCH / LPA;              // hours each lane stages (1 or 2)
     const uint64_t segmask = LPA == WAVE ? ~0ull : (((1ull << LPA) - 1ull) << g.base);
     const uint64_t below = ((1ull << g.lane) - 1ull) & segmask;   // segment lanes before this one
@@ -1912,7 +2066,23 @@ __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const Y
     for (int m = 0; m < 12; m++) {
         double flat = 0.0;
         for (int q = 0; q < DCP; q++) S.at(q) = 0.0;
-        const int h_lo = c_month_start_day[m] * 24, h_hi = c_month_start_day[m + 1] * 24;
+        if (REC) {
+            const double* from = with_gen ? R.lb + m * DCP : R.mxl + m * DCP;
+            for (int q = 0; q < nq; q++) {
+                const double v = from[q];
+                S.at(q) = v;
+                flat = v > flat ? v : flat;
+            }
+            if (!with_gen) {                      // the no-system peaks: exact from the record
+                if (S.pk) S.pk[m * WAVE] = flat;
+                double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
+                for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
+                total += c;
+                continue;
+            }
+        }
+        const int h_lo = REC ? R.off[m] : c_month_start_day[m] * 24;
+        const int h_hi = REC ? R.off[m + 1] : c_month_start_day[m + 1] * 24;
         // the batch's hours (load, system output, period), the next batch's
         // loads issued before the current batch is processed
         auto fetch = [&](int hb, double (&Lq)[HPL], double (&gq)[HPL], int (&pq)[HPL])
@@ -1921,12 +2091,19 @@ __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const Y
 #pragma unroll
             for (int u = 0; u < HPL; u++) {
                 const bool valid = hb < h_hi && k0 + u < nb;
-                const int hu = valid ? hb + k0 + u : h_lo;
-                const int d = hu / 24, hod = hu - d * 24;
-                const int pp = ((d % 7) >= 5) ? D->wkend[m][hod] : D->wkday[m][hod];
-                pq[u] = valid ? (pp < DCP ? pp : 0) : -1;
-                Lq[u] = (double)src.shape[hu] * src.load_scale;
-                gq[u] = with_gen ? src.sysgen[(int64_t)(hu >> 2) * src.sys_stride * 4 + (hu & 3)] : 0.0;
+                if (REC) {                        // a kept hour: its entry
+                    const NbEntC e = R.ent[valid ? hb + k0 + u : 0];
+                    pq[u] = valid ? e.p : -1;
+                    Lq[u] = (double)e.sh * src.load_scale;
+                    gq[u] = e.g;
+                } else {
+                    const int hu = valid ? hb + k0 + u : h_lo;
+                    const int d = hu / 24, hod = hu - d * 24;
+                    const int pp = ((d % 7) >= 5) ? D->wkend[m][hod] : D->wkday[m][hod];
+                    pq[u] = valid ? (pp < DCP ? pp : 0) : -1;
+                    Lq[u] = (double)src.shape[hu] * src.load_scale;
+                    gq[u] = with_gen ? src.sysgen[(int64_t)(hu >> 2) * src.sys_stride * 4 + (hu & 3)] : 0.0;
+                }
             }
         };
         double nL[HPL], ng[HPL];
@@ -3330,7 +3507,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
 template <int LPA, bool DC, bool NET, bool PK>
 __global__ void __launch_bounds__(WAVE)
 k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
-                 int64_t n_scratch, int64_t i0, int64_t i1, char* nbws, int nb_scan) {
+                 int64_t n_scratch, int64_t i0, int64_t i1, char* nbws, int nb_scan, char* dcr, int dc_nq) {
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -3382,12 +3559,20 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         src.ts = (t.mo == 2 && !is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
         src.ts_mult = A.price_mult[i];
     }
+    // the battery-case demand record this step's k_hourly_batt built (flag 1),
+    // else the staged pass over the system-output plane
+    DcrRec drec{nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool dr = false;
+    if (DC && dcr && A.scratch_slot[i] >= 0) {
+        drec = dcr_rec(dcr, A.scratch_slot[i]);
+        dr = *drec.flag == 1;
+    }
     double wo1 = NAN, wb = NAN;
     // kWh/kW tiers: the no-system month peaks ahead of the no-system bill (k_size's
     // first_without already holds it for the same tariff), the battery case's
     // ahead of its bill
     double v0 = 0.0, v1 = 0.0;
-    if (pk13 && !same_tariff) v0 = yl_demand_staged(dem, src, 1.0, false, S, stage, g);
+    if (pk13 && !same_tariff) v0 = yl_demand_staged(dem, src, 1.0, false, S, stage, g, dr, drec, dc_nq);
     if (!mo2) {
         const double2* lg = W.LGb + (int64_t)i * NBIN;
         for (int cell = g.sl; cell < 12 * t.P; cell += LPA) {
@@ -3398,7 +3583,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         }
         wave_lds_sync();
         wo1 = same_tariff ? O.first_without[i] : yl_bill_nem_nosys(t, S, cfg.nm_yearend_sell_rate, g);
-        if (pk13) v1 = yl_demand_staged(dem, src, s_y, true, S, stage, g);
+        if (pk13) v1 = yl_demand_staged(dem, src, s_y, true, S, stage, g, dr, drec, dc_nq);
         wb = yl_bill_nem(t, S, s_y, cfg.nm_yearend_sell_rate);
     } else if constexpr (NET) {
         if (same_tariff) {
@@ -3409,7 +3594,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
                           src.load_scale, S, g);
             wo1 = yl_bill_mo2_nogen_par(t, S, g);
         }
-        if (pk13) v1 = yl_demand_staged(dem, src, s_y, true, S, stage, g);
+        if (pk13) v1 = yl_demand_staged(dem, src, s_y, true, S, stage, g, dr, drec, dc_nq);
         // the split of the battery-case hours over the lanes' degradation
         // factors [s_lo, s_hi] (the agent's net-billing record is free: its
         // search finished in k_size)
@@ -3446,7 +3631,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         PH_T0(tds);
         for (int pass = same_tariff ? 1 : 0; pass < 2; pass++) {
             const bool wg = pass == 1;
-            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g);
+            const double v = yl_demand_staged(dem, src, wg ? s_y : 1.0, wg, S, stage, g, dr, drec, dc_nq);
             if (wg) wb += v;
             else wo1 += v;
         }
@@ -4000,6 +4185,9 @@ struct dgen_ctx {
     int64_t count;
     void* dc_buf = nullptr;   // demand-charge envelopes, DCW_BYTES per agent (grown on demand)
     size_t dc_cap = 0;
+    void* dcr_buf = nullptr;  // battery-case demand records, DCR_BYTES per scratch slot (grown on demand)
+    size_t dcr_cap = 0;
+    int dcr_enable = DCR_CAP; // kept hours per record, 0 = off (dgen_set_dc_records)
 };
 
 static int fold_one(dgen_ctx* c, int slot) {
@@ -4095,6 +4283,7 @@ int32_t dgen_close(dgen_ctx* c) {
     (void)hipEventDestroy(c->join);
     (void)hipStreamDestroy(c->s2);
     if (c->dc_buf) (void)hipFree(c->dc_buf);
+    if (c->dcr_buf) (void)hipFree(c->dcr_buf);
     delete c;
     return DGEN_OK;
 }
@@ -4227,11 +4416,33 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // split: import and export sums) + the waves' day buffers
     // (the scan form doubles the bins; kept within 64 KB of dynamic LDS per
     // block, i.e. batches whose tariffs have at most 10 periods)
-    const size_t lds_nb = sizeof(double) * 4 * (size_t)lds_half(T->max_periods) * BLOCK +
+    // battery-case demand records (DcrRec) built in the scan for the finance
+    // kernel's demand pass: demand-charge / kWh/kW batches with the daily plan
+    // (the hourly re-plan keeps the staged pass over the plane), DCR_BYTES per
+    // scratch slot, context-owned; their per-period maxima add [dc_nq][BLOCK]
+    // double2 to the scan's LDS
+    const int dc_nq = (T->max_dc_periods > 0 && T->max_dc_periods <= DCP) ? T->max_dc_periods : DCP;
+    bool dcr_on = dc && n_scratch > 0 && c->battery && c->cfg.batt_update_hours != 1 && c->dcr_enable;
+    if (dcr_on && (size_t)n_scratch * DCR_BYTES > c->dcr_cap) {
+        if (c->dcr_buf) HIP_TRY(hipFree(c->dcr_buf));
+        c->dcr_buf = nullptr;
+        c->dcr_cap = 0;
+        if (hipMalloc(&c->dcr_buf, (size_t)n_scratch * DCR_BYTES) != hipSuccess) {
+            c->dcr_buf = nullptr;   // no records: the staged pass over the plane
+            (void)hipGetLastError();
+        } else {
+            c->dcr_cap = (size_t)n_scratch * DCR_BYTES;
+        }
+    }
+    dcr_on = dcr_on && c->dcr_buf != nullptr;
+    char* const dcr = dcr_on ? reinterpret_cast<char*>(c->dcr_buf) : nullptr;
+    const size_t lds_dcr = dcr_on ? (size_t)16 * dc_nq * BLOCK : 0;
+    const size_t lds_nb = sizeof(double) * 4 * (size_t)lds_half(T->max_periods) * BLOCK + lds_dcr +
                           (size_t)(BLOCK / 64) * HB_DAY_BYTES;
     const bool nb_scan = n_scratch > 0 && c->nb_scan && c->battery && lds_nb <= 65536;
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK * (nb_scan ? 2 : 1) +
-                       (size_t)(BLOCK / 64) * HB_DAY_BYTES;
+                       lds_dcr + (size_t)(BLOCK / 64) * HB_DAY_BYTES;
+    const int rep_mask = (nb_scan ? 1 : 0) | (dcr_on ? 2 : 0);
     // two agents per wave when every analysis period fits 32 lanes, unless the
     // build guard withdrew that kernel's 32-lane instantiation (DGEN_NO2_*)
     const bool fits32 = A->max_years >= 1 && A->max_years <= 32;
@@ -4298,12 +4509,19 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
 #define DGEN_HB_LAUNCH_R(H, F, REP, R)                                                            \
     do {                                                                                          \
-        if (nb_scan && !(REP))                                                                    \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, true, R>), grid, block, lds, s2, *T, *A, *O, c->cfg, \
-                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0);      \
+        if (nb_scan && !(REP) && dcr_on && !(R))                                                  \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, true>), grid, block, lds, s2, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, dcr, dc_nq, c->dcr_enable); \
+        else if (nb_scan && !(REP))                                                               \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, true, R, false>), grid, block, lds, s2, *T, *A, *O, c->cfg, \
+                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0); \
+        else if (!(REP) && dcr_on && !(R))                                                        \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false, false, true>), grid, block, lds, s2, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, 0, dcr, dc_nq, c->dcr_enable); \
         else                                                                                      \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, false, R>), grid, block, lds, s2, *T, *A, *O,      \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? 1 : 0); \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false, R, false>), grid, block, lds, s2, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? rep_mask : 0, \
+                               (REP) ? dcr : nullptr, 0, 0);                                      \
     } while (0)
 #define DGEN_HB_LAUNCH(H, F, REP)                                                                 \
     do {                                                                                          \
@@ -4314,8 +4532,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             else if (hourly) DGEN_HB_LAUNCH(true, false, false);
             else DGEN_HB_LAUNCH(false, false, false);
         }
-        // repair pass (agents whose scan-built split overflowed: their plane)
-        for (int m0 = 0; nb_scan && m0 < 12; m0 += c->hb_months) {
+        // repair pass (agents whose scan-built split or demand record
+        // overflowed: their plane)
+        for (int m0 = 0; rep_mask && m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
             if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, true);
             else if (hourly) DGEN_HB_LAUNCH(true, false, true);
@@ -4330,34 +4549,34 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
 #if !DGEN_NO2_FIN
             if (net)
                 hipLaunchKernelGGL((k_batt_finance_w<32, false, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
             else
                 hipLaunchKernelGGL((k_batt_finance_w<32, false, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
 #endif
         } else if (lpa_f == 32 && !pk) {
 #if !DGEN_NO2_FIN_DC
             hipLaunchKernelGGL((k_batt_finance_w<32, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                               *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+                               *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
 #endif
         } else if (lpa_f == 32) {
 #if !DGEN_NO2_FIN_PK
             hipLaunchKernelGGL((k_batt_finance_w<32, true, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                               *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+                               *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
 #endif
         } else if (!dc) {
             if (net)
                 hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
             else
                 hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
-                                   *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+                                   *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
         } else if (!pk) {
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
-                               *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+                               *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
         } else {
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
-                               *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan);
+                               *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
         }
         HIP_TRY(hipEventRecord(e[4], s2));
     }
@@ -4373,6 +4592,15 @@ int32_t dgen_set_hourly_segment(dgen_ctx* c, int32_t months) {
         return DGEN_E_ARG;
     }
     c->hb_months = months;
+    return DGEN_OK;
+}
+
+int32_t dgen_set_dc_records(dgen_ctx* c, int32_t cap) {
+    if (!c || cap < 0 || cap > DCR_CAP) {
+        set_err("dgen_set_dc_records: cap must be in [0, %d]", DCR_CAP);
+        return DGEN_E_ARG;
+    }
+    c->dcr_enable = cap;
     return DGEN_OK;
 }
 

@@ -157,6 +157,7 @@ class Engine:
         if int(recs["dc"].max()) > dem.size or int(recs["dc"].min()) < 0:
             raise ValueError("tariff dc index outside the demand table")
         self.tables.n_demand = int(dem.size)
+        self.tables.max_dc_periods = (int(max(dem["wkday"].max(), dem["wkend"].max())) + 1) if dem.size else 0
         self.tables.demand = None
         self._keep.pop("demand", None)
         if dem.size:
@@ -335,6 +336,15 @@ class Engine:
         variant, dgen_set_battery)."""
         _lib.check(self.lib.dgen_set_battery(self.ctx, int(bool(on))), "dgen_set_battery")
         self.battery = bool(on)
+
+    def set_dc_records(self, cap=True):
+        """Battery-case demand records built in the hourly scan
+        (dgen_set_dc_records): True = DGEN_DCR_CAP kept hours per agent (the
+        default), an int = that capacity (an agent beyond it falls back), False
+        = the finance kernel's staged pass over all 8760 hours of the
+        system-output plane.  Results are bit-identical."""
+        c = _lib.DCR_CAP if cap is True else int(cap)
+        _lib.check(self.lib.dgen_set_dc_records(self.ctx, c), "dgen_set_dc_records")
 
     def kernel_times(self):
         """Average per-launch device time (ms) of the three sizing kernels over

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 7
+#define DGEN_ABI_VERSION 8
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_NH    8760   /* hours per year                                    */
@@ -48,6 +48,7 @@ extern "C" {
 #define DGEN_MAXT  6      /* tiers                                              */
 #define DGEN_MAXY  50     /* analysis years                                     */
 #define DGEN_DCP   8      /* demand-charge TOU periods (extension mode)         */
+#define DGEN_DCR_CAP 1024 /* kept hours per battery-case demand record          */
 #define DGEN_DCT   4      /* demand-charge tiers (extension mode)               */
 
 /* error codes */
@@ -168,6 +169,9 @@ typedef struct {
     int32_t peak_units;            /* 1: some tariff bills its tiers in kWh/kW (unit */
                                    /* codes 1, 3): the year-lane kernels keep month  */
                                    /* peaks per lane (see dgen_tariff.unit)          */
+    int32_t max_dc_periods;        /* 1 + the largest period in the demand records' */
+                                   /* schedules (sizes LDS; 0 = DGEN_DCP)           */
+    int32_t pad_t;
 } dgen_tables;
 
 /* Agent batch, structure of arrays (device pointers, length n).  Column
@@ -545,6 +549,18 @@ int32_t dgen_set_battery(dgen_ctx* ctx, int32_t on);
  * bins then fit 64 KB of LDS per block); others build in k_batt_finance.
  * Range [0, DGEN_NB_CAPM].  Replaces nothing in the reference.            */
 int32_t dgen_set_nb_scan(dgen_ctx* ctx, int32_t cap);
+
+/* Battery-case demand records holding at most cap kept hours per agent
+ * (default and maximum DGEN_DCR_CAP), or none (0).  With demand charges
+ * billed (or kWh/kW tier peaks) and the daily plan, k_hourly_batt's scan keeps
+ * per (month, demand period) the max load and a lower bound of every analysis
+ * year's peak import, and the hours that can raise some year's peak above it
+ * (a context-owned buffer per scratch slot); k_batt_finance's battery-case
+ * demand pass then stages those hours only, instead of all 8760 hours of the
+ * system-output plane.  Results are bit-identical (peaks are maxima of the
+ * same values).  An agent whose kept hours overflow the record falls back to
+ * the plane.  Replaces nothing in the reference.                            */
+int32_t dgen_set_dc_records(dgen_ctx* ctx, int32_t cap);
 
 #ifdef __cplusplus
 }

@@ -102,3 +102,38 @@ def test_reference_mode_ignores_demand_records(engine, engine_dc):
         assert np.array_equal(o_ref[k], o_plain[k]), k
     o_dc = _run(engine_dc, pop, pop.demand)
     assert (o_dc["first_without"] > o_ref["first_without"]).all()
+
+
+def _run_records(eng, pop, demand, cap):
+    eng.set_dc_records(cap)
+    try:
+        return _run(eng, pop, demand)
+    finally:
+        eng.set_dc_records(True)
+
+
+@pytest.mark.parametrize("net_billing,long_life", [(False, False), (True, False), (True, True)])
+def test_demand_records_bit_identical(engine_dc, net_billing, long_life):
+    """The battery-case demand pass over the scan's records (default), over the
+    system-output plane (records off) and with records that overflow a small
+    capacity (those agents fall back to the plane) give bit-identical outputs:
+    the peaks are maxima of the same imports."""
+    pop = _pop(160, net_billing, seed=11, long_life=long_life)
+    on = _run_records(engine_dc, pop, pop.demand, True)
+    off = _run_records(engine_dc, pop, pop.demand, False)
+    small = _run_records(engine_dc, pop, pop.demand, 24)
+    for k in ("system_kw", "npv", "npv_pv_batt", "first_without", "bill_w_batt", "bill_wo_batt",
+              "cfev_batt", "batt_kwh", "net_with_batt"):
+        assert np.array_equal(on[k], off[k], equal_nan=True), k
+        assert np.array_equal(small[k], off[k], equal_nan=True), k
+
+
+def test_kwh_per_kw_records_bit_identical(engine):
+    """kWh/kW tier peaks (reference mode, the PK kernels) from the records equal
+    the staged pass over the plane, bit for bit."""
+    pop = make_population("com_kwkw", 192, seed=20260000 + 21, n_res_shapes=16, n_com_shapes=32,
+                          n_cf=32, n_counties=16, n_tariffs=24)
+    on = _run_records(engine, pop, pop.demand, True)
+    off = _run_records(engine, pop, pop.demand, False)
+    for k in ("system_kw", "npv", "npv_pv_batt", "bill_w_batt", "bill_wo_batt", "status"):
+        assert np.array_equal(on[k], off[k], equal_nan=True), k
