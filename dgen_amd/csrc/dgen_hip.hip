@@ -501,6 +501,8 @@ struct NbRec {
 };
 // cnt[12]: 1 when k_hourly_batt built the battery case's split into the record
 __device__ __forceinline__ int& nbr_flag(char* p) { return reinterpret_cast<int*>(p + NB_SUMS_BYTES)[12]; }
+// cnt[13]: 1 + the tariff k_nb_env built the PV-only search's split for (0: none)
+__device__ __forceinline__ int& nbr_tag(char* p) { return reinterpret_cast<int*>(p + NB_SUMS_BYTES)[13]; }
 __device__ __forceinline__ NbRec nb_rec(char* p) {
     NbRec r;
     r.sums = reinterpret_cast<double*>(p);
@@ -2076,7 +2078,7 @@ __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const Y
             if (!with_gen) {                      // the no-system peaks: exact from the record
                 if (S.pk) S.pk[m * WAVE] = flat;
                 double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
-                for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
+                for (int q = 0; q < nq; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
                 total += c;
                 continue;
             }
@@ -2125,16 +2127,18 @@ __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const Y
 #pragma unroll
             for (int q = 0; q < DCP; q++) {
                 double v = S.at(q);
+                if (!REC) {
 #pragma unroll
-                for (int o = LPA / 2; o > 0; o >>= 1) {
-                    const double w = __shfl_xor(v, o, WAVE);
-                    v = w < v ? w : v;
+                    for (int o = LPA / 2; o > 0; o >>= 1) {
+                        const double w = __shfl_xor(v, o, WAVE);
+                        v = w < v ? w : v;
+                    }
                 }
                 thr[q] = v;
             }
 #pragma unroll
             for (int u = 0; u < HPL; u++) {
-                if (pv[u] >= 0) {
+                if (pv[u] >= 0 && !REC) {        // a record's kept hours passed this against lb
                     double t_u = thr[0];
 #pragma unroll
                     for (int q = 1; q < DCP; q++) t_u = pv[u] == q ? thr[q] : t_u;
@@ -2145,7 +2149,7 @@ __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const Y
             wave_lds_sync();                          // previous batch fully read
             int base_q = 0;
 #pragma unroll 1
-            for (int q = 0; q < DCP; q++) {
+            for (int q = 0; q < nq; q++) {
                 uint64_t b[HPL];
                 int cnt = 0;
 #pragma unroll
@@ -2163,9 +2167,9 @@ __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const Y
                 if (g.sl == 0) st->off[q] = base_q;
                 base_q += cnt;
             }
-            if (g.sl == 0) st->off[DCP] = base_q;
+            if (g.sl == 0) st->off[nq] = base_q;
             wave_lds_sync();
-            for (int q = 0; q < DCP; q++) {
+            for (int q = 0; q < nq; q++) {
                 const int lo = st->off[q], hi = st->off[q + 1];
                 if (lo == hi) continue;
                 double mx = -INFINITY;
@@ -2182,7 +2186,7 @@ __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const Y
         }
         if (S.pk) S.pk[m * WAVE] = flat;          // the month's peak import (kWh/kW tiers)
         double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
-        for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
+        for (int q = 0; q < nq; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
         total += c;
     }
     return total;
@@ -2209,8 +2213,9 @@ struct DcEnv {
     double2* lines;   // [12][DCP][DC_NL] (L, g)
     double* maxl;     // [12][DCP] max load (the no-system peak)
     int* cnt;         // [12][DCP] lines kept (0 = period absent from the month)
+    int* tag;         // 1 + the tariff k_dc_env built them for (0: none / overflow)
 };
-constexpr size_t DCW_BYTES = (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double) + sizeof(int));
+constexpr size_t DCW_BYTES = (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double) + sizeof(int)) + 16;
 
 __device__ __forceinline__ DcEnv dc_env_at(void* base, int64_t i) {
     char* b = reinterpret_cast<char*>(base) + (size_t)i * DCW_BYTES;
@@ -2218,6 +2223,7 @@ __device__ __forceinline__ DcEnv dc_env_at(void* base, int64_t i) {
     e.lines = reinterpret_cast<double2*>(b);
     e.maxl = reinterpret_cast<double*>(b + (size_t)12 * DCP * DC_NL * sizeof(double2));
     e.cnt = reinterpret_cast<int*>(b + (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double)));
+    e.tag = reinterpret_cast<int*>(b + (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double) + sizeof(int)));
     return e;
 }
 
@@ -3167,6 +3173,9 @@ struct YCtx {
     bool stg_ok;                // the current envelope is staged
     char* nb;                   // the agent's net-billing split record (or nullptr)
     bool nb_ok;                 // the split of the current (mo 2) tariff fits
+    int nb_tag;                 // 1 + the tariff the record holds the split of (0: none)
+    bool nb_pending;            // the current (mo 2) tariff's split is not formed yet
+    int env_tag;                // 1 + the tariff the envelopes are of (0: none)
     double tlo, thi;            // generation-scale range of the search
     int sw_cnt;
     int tariff, switched, status;
@@ -3185,6 +3194,29 @@ struct YCtx {
     bool active;
     __device__ explicit YCtx(int lane) : g(lane) {}
 };
+
+// The current tariff's demand envelopes, built here at the first evaluation
+// billed with the tariff (the segment's hour lanes, yl_dc_build_any).  With
+// DGEN_DC_PREBUILD, k_dc_env builds the first-evaluation tariff's ahead of
+// k_size (tag = 1 + tariff) and only other tariffs take the hourly pass
+// (yl_demand, exact).  A/B (C4 200k): k_size 35.7 ms in-kernel vs 41.4 ms
+// with the prebuild kernel (k_dc_env ran ~16 ms, and the evaluations read the
+// envelopes back from HBM instead of a build's warm L2 lines).
+#ifndef DGEN_DC_PREBUILD
+#define DGEN_DC_PREBUILD 0
+#endif
+#define DGEN_DC_INKERNEL (!DGEN_DC_PREBUILD)
+template <int LPA>
+__device__ __forceinline__ bool yl_dc_ready(YCtx<LPA>& c, const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
+    if (!E.lines) return false;
+    if (c.env_tag == c.tariff + 1) return true;
+    if (DGEN_DC_INKERNEL) {
+        const bool ok = yl_dc_build_any(c.dem, c.src, c.tlo, c.thi, E, st, g);
+        c.env_tag = ok ? c.tariff + 1 : 0;
+        return ok;
+    }
+    return false;
+}
 
 // NET: the batch may bill net (it has scratch slots, dgen_size_agents); the
 // NEM-only instantiation compiles the net-billing paths out, so the common
@@ -3213,7 +3245,7 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
             // kWh/kW tiers: the month peaks come before the energy bills, so
             // the envelopes are built and the no-system pass runs here (its
             // charge, when billed, joins the no-system bill below)
-            c.env_ok = c.env.lines && yl_dc_build_any(c.dem, c.src, c.tlo, c.thi, c.env, c.stg, c.g);
+            c.env_ok = yl_dc_ready(c, c.env, c.stg, c.g);
             c.stg_ok = c.env_ok && c.stg && yl_dc_stage(c.env, c.stg, c.g);
             const double v0 = c.env_ok ? yl_dc_eval(c.dem, c.env, 0.0, 1.0, false, c.S)
                                        : yl_demand(c.dem, c.src, 0.0, 1.0, false, c.S);
@@ -3230,15 +3262,14 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
         c.wo1 = yl_bill_nem_nosys(t, c.S, c.yearend, c.g);
         PH_ADD_KS(12, tn, c.g.sl == 0);        // NEM set_tariff (bins + no-system bill)
     } else if constexpr (NET) {
-        // net billing: the no-system bill from the load bins, then the split
-        // of the search's hours for this tariff's periods
+        // net billing: the no-system bill from the load bins
         wave_lds_sync();
         yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);
         c.wo1 = yl_bill_mo2_nogen_par(t, c.S, c.g);
-        PH_T0(tb);
-        c.nb_ok = c.nb && (DGEN_NB_SERIAL ? yl_nb_build_serial(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g) : yl_nb_build<false>(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g));
-        PH_ADD(1, tb, c.g.sl == 0);
-        PH_CNT(7, 1, c.g.sl == 0);
+        // the split is formed at the first evaluation billed with this tariff
+        // (an agent the rate switch moves at its first evaluation never needs
+        // its initial tariff's)
+        c.nb_pending = true;
     } else {
         c.status |= DGEN_ST_SCRATCH;
         c.wo1 = NAN;
@@ -3281,6 +3312,20 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
         wb = yl_bill_nem(t, c.S, c.s_y * kws, c.yearend);
         PH_ADD_KS(13, tn, c.g.sl == 0);        // NEM evaluation bill
     } else if constexpr (NET) {
+        if (c.nb_pending) {
+            // the first-evaluation tariff's split comes from k_nb_env (tag);
+            // any other is built here
+            PH_T0(tb);
+            if (c.nb && c.nb_tag != c.tariff + 1) {
+                const bool ok = DGEN_NB_SERIAL ? yl_nb_build_serial(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g)
+                                               : yl_nb_build<false>(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g);
+                c.nb_tag = ok ? c.tariff + 1 : 0;
+                PH_CNT(7, 1, c.g.sl == 0);
+            }
+            PH_ADD(1, tb, c.g.sl == 0);
+            c.nb_ok = c.nb && c.nb_tag == c.tariff + 1;
+            c.nb_pending = false;
+        }
         c.src.gen_scale = kws;
         PH_T0(te);
         wb = c.nb_ok ? yl_bill_nb(t, c.src, c.s_y, c.nb, c.S, c.g) : yl_bill_mo2(t, c.src, c.s_y, true, c.S);
@@ -3298,7 +3343,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
             c.src.gen_scale = kws;
             if (c.dem_wo_pending) {
                 PH_T0(tdb);
-                c.env_ok = c.env.lines && yl_dc_build_any(c.dem, c.src, c.tlo, c.thi, c.env, c.stg, c.g);
+                c.env_ok = yl_dc_ready(c, c.env, c.stg, c.g);
                 c.stg_ok = c.env_ok && c.stg && yl_dc_stage(c.env, c.stg, c.g);
                 PH_ADD(1, tdb, c.g.sl == 0);          // demand envelopes: build + stage
                 PH_CNT(7, 1, c.g.sl == 0);
@@ -3369,8 +3414,12 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.env.lines = nullptr;
     c.stg = nullptr;
     c.stg_ok = false;
+    c.env_tag = 0;
     if constexpr (DC) {
-        if (dcws) c.env = dc_env_at(dcws, i);
+        if (dcws) {
+            c.env = dc_env_at(dcws, i);
+            c.env_tag = DGEN_DC_PREBUILD ? *c.env.tag : 0;   // k_dc_env's, this step
+        }
         // the segment's envelope stage sits after the year-lane layout
         c.stg = reinterpret_cast<DcStage*>(reinterpret_cast<char*>(dyn_lds) +
                                            ylds_bytes(half, LPA, PK && T.peak_units != 0)) + lane / LPA;
@@ -3379,6 +3428,8 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         const int slot = A.scratch_slot[i];
         c.nb = (nbws && slot >= 0) ? nbws + (size_t)slot * NB_BYTES : nullptr;
         c.nb_ok = false;
+        c.nb_tag = c.nb ? nbr_tag(c.nb) : 0;  // k_nb_env's, this step
+        c.nb_pending = false;
     }
     c.sw_rows = T.switches + A.sw_solar_off[i];
     c.sw_cnt = A.sw_solar_cnt[i];
@@ -3501,6 +3552,129 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     }
     PH_ADD(0, t_all, sl == 0);
     PH_CNT(9, nfev, sl == 0);
+}
+
+// The tariff an agent bills its first Brent evaluation with: scipy's first
+// point a + golden_mean (b - a) (brent_bounded) through the solar rate switch
+// (yl_objective) -- the initial tariff, or the row the switch lands on, which
+// the rest of the narrow bracket almost always keeps.
+__device__ __forceinline__ int first_eval_tariff(const dgen_tables& T, const dgen_agents& A, int64_t i,
+                                                 double low, double high) {
+    const double x = low + 0.3819660112501051 * (high - low);
+    int t = A.tariff0[i];
+    if (x > 0.0) {
+        int nt;
+        (void)rate_switch(T.switches + A.sw_solar_off[i], A.sw_solar_cnt[i], x, &nt);
+        if (nt >= 0) t = nt;
+    }
+    return t;
+}
+
+// Demand envelopes of every agent's first-evaluation tariff (first_eval_tariff), built ahead of k_size on
+// the same stream (the PV-only search's demand pass, DC batches): two agents
+// per wave, the hour-lane build (yl_dc_build_coop) over the same bracket and
+// degradation range k_size evaluates.  In k_size the build was half the C4
+// search's cycles and its code held the two-agent DC kernel at 256 VGPRs with
+// spills; here it runs alone at a few waves per SIMD.  tag = 1 + the tariff
+// (0: no envelope -- no demand record, invalid agent, or a group over DC_NL
+// lines: k_size then takes the hourly pass).
+template <int LPA>
+__global__ void __launch_bounds__(WAVE)
+k_dc_env(dgen_tables T, dgen_agents A, dgen_cfg cfg, int64_t i0, int64_t i1, void* dcws) {
+    const int lane = threadIdx.x;
+    const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
+    if (i >= i1) return;
+    const Seg<LPA> g(lane);
+    const DcEnv E = dc_env_at(dcws, i);
+    const int lr = A.load_row[i], cr = A.cf_row[i];
+    const double kwh = A.load_kwh[i];
+    const double max_load = kwh / T.cf_naep[cr];                    // ff:440-444, as k_size
+    const double low = max_load * 0.8, high = max_load * 1.25;
+    const bool fin = isfinite(low) && isfinite(high);
+    const int t0 = fin ? first_eval_tariff(T, A, i, low, high) : -1;
+    int tag = 0;
+    if (t0 >= 0 && t0 < T.n_tariffs) {
+        const dgen_tariff& t = T.tariffs[t0];
+        // k_size's record for the tariff: the kWh/kW tier peaks' where the batch
+        // bills those (PK kernels), else the demand charges'
+        const dgen_demand* dem = (T.peak_units && peak_unit(t)) ? tariff_peaks(T.demand, T.n_demand, t)
+                                                                : tariff_demand(T, cfg, t);
+        const int N = A.econ_life[i];
+        if (dem && N >= 1 && N <= MAXY) {
+            const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+            const double sN = pow_seq(sys_base, N - 1);            // k_size's s_y of year N
+            const double s_lo = sN < 1.0 ? sN : 1.0, s_hi = sN > 1.0 ? sN : 1.0;
+            const double tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
+            const double thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
+            YSrc src;
+            src.shape = T.shapes + (int64_t)lr * NH;
+            src.cf = T.cfs + (int64_t)cr * NH;
+            src.sysgen = nullptr;
+            src.sys_stride = 0;
+            src.load_scale = kwh / T.shape_sum[lr];
+            src.gen_scale = 0.0;
+            src.ts = nullptr;
+            src.ts_mult = 0.0;
+            DcStage* const st = reinterpret_cast<DcStage*>(dyn_lds) + lane / LPA;
+            if (yl_dc_build_coop(dem, src, tlo, thi, E, st, g)) tag = t0 + 1;
+        }
+    }
+    PH_CNT(2, 1, g.sl == 0);                      // phase builds: agents / envelopes kept
+    PH_CNT(6, tag != 0, g.sl == 0);
+    if (g.sl == 0) *E.tag = tag;
+}
+
+// The PV-only search's net-billing split of every agent's first-evaluation
+// tariff (first_eval_tariff), built ahead of k_size on the same stream (yl_nb_build<false> over the same
+// range [tlo, thi]; k_size builds only for a tariff the rate switch moves to).
+// The build ran at k_size's occupancy with its registers; here it runs alone.
+// tag = 1 + the tariff (0: not built -- no slot, not billed net, or invalid).
+template <int LPA>
+__global__ void __launch_bounds__(WAVE)
+k_nb_env(dgen_tables T, dgen_agents A, int64_t i0, int64_t i1, char* nbws) {
+    const int lane = threadIdx.x;
+    const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
+    if (i >= i1) return;
+    const int slot = A.scratch_slot[i];
+    if (slot < 0) return;
+    const Seg<LPA> g(lane);
+    char* const nbp = nbws + (size_t)slot * NB_BYTES;
+    const int lr = A.load_row[i], cr = A.cf_row[i];
+    const double kwh = A.load_kwh[i];
+    const double max_load = kwh / T.cf_naep[cr];                    // ff:440-444, as k_size
+    const double low = max_load * 0.8, high = max_load * 1.25;
+    const bool fin = isfinite(low) && isfinite(high);
+    const int t0 = fin ? first_eval_tariff(T, A, i, low, high) : -1;
+    int tag = 0;
+    if (t0 >= 0 && t0 < T.n_tariffs && net_hourly(T.tariffs[t0])) {
+        const dgen_tariff& t = T.tariffs[t0];
+        const int N = A.econ_life[i];
+        if (N >= 1 && N <= MAXY) {
+            const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+            const double sN = pow_seq(sys_base, N - 1);            // k_size's s_y of year N
+            const double s_lo = sN < 1.0 ? sN : 1.0, s_hi = sN > 1.0 ? sN : 1.0;
+            const double tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
+            const double thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
+            const bool is_ca = (A.flags[i] & 2) != 0;
+            const int wr = A.wholesale_row[i];
+            YSrc src;
+            src.shape = T.shapes + (int64_t)lr * NH;
+            src.cf = T.cfs + (int64_t)cr * NH;
+            src.sysgen = nullptr;
+            src.sys_stride = 0;
+            src.load_scale = kwh / T.shape_sum[lr];
+            src.gen_scale = 0.0;
+            src.ts = (t.mo == 2 && !is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
+            src.ts_mult = A.price_mult[i];
+            YLds S;                                   // the build's 4 LDS slots per lane
+            S.trf = nullptr;
+            S.L = S.G = S.pk = nullptr;
+            S.half = 0;
+            S.lane = dyn_lds + lane;
+            if (yl_nb_build<false>(t, src, tlo, thi, nbp, S, g)) tag = t0 + 1;
+        }
+    }
+    if (g.sl == 0) nbr_tag(nbp) = tag;
 }
 
 // Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
@@ -4462,6 +4636,14 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         const int64_t i0 = (int64_t)j * csz, i1 = (i0 + csz < n) ? i0 + csz : n, m = i1 - i0;
         hipEvent_t* e = c->ev[slot][j];
         HIP_TRY(hipEventRecord(e[0], s));
+        // net-billing splits and demand envelopes of the initial tariffs
+        // (counted in k_size's time)
+        if (n_scratch > 0)
+            hipLaunchKernelGGL((k_nb_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE), 4 * WAVE * sizeof(double), s,
+                               *T, *A, i0, i1, nbws);
+        if (DGEN_DC_PREBUILD && dc && c->dc_buf)
+            hipLaunchKernelGGL((k_dc_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE), 2 * DCS_BYTES, s, *T, *A,
+                               c->cfg, i0, i1, c->dc_buf);
         // agents per year-lane block: WAVE / lpa
         const dim3 ygrid_s((unsigned)((m + WAVE / lpa_s - 1) / (WAVE / lpa_s)));
         const dim3 ygrid_f((unsigned)((m + WAVE / lpa_f - 1) / (WAVE / lpa_f)));

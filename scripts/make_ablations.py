@@ -35,6 +35,10 @@ VARIANTS = {
     # whose whole need fits, wave-days where it fits for all lanes, saturated)
     "phase_day": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
                   ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1")],
+    # demand envelopes prebuilt by k_dc_env ahead of k_size (A/B: slower)
+    "dc_prebuild": [("#define DGEN_DC_PREBUILD 0", "#define DGEN_DC_PREBUILD 1")],
+    # phase timers only (DGEN_PHASE_PROF slots, see dgen_hip.hip)
+    "phase": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1")],
     # k_size builds the demand envelopes with the serial month lanes
     "dc_serial": [("#define DGEN_DC_SERIAL 0", "#define DGEN_DC_SERIAL 1")],
     # timing probes of the hour-lane envelope build (wrong results by construction)
