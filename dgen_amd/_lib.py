@@ -111,7 +111,7 @@ EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
     "dgen_kernel_times", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
-    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_set_dc_records", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
+    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_set_dc_records", "dgen_hourly_planes", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
     "dgen_finance_series", "dgen_year_inputs", "dgen_initial_market_shares",
 ]
 
@@ -166,6 +166,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.dgen_set_nb_scan.argtypes = [_vp, _i32]
     L.dgen_set_dc_records.restype = _i32
     L.dgen_set_dc_records.argtypes = [_vp, _i32]
+    L.dgen_hourly_planes.restype = _i32
+    L.dgen_hourly_planes.argtypes = L.dgen_size_agents.argtypes
     L.dgen_segment_sums.restype = _i32
     L.dgen_segment_sums.argtypes = [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _vp, _i64, _vp, _vp]
     if L.dgen_abi_version() != ABI_VERSION:

@@ -4768,6 +4768,51 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     return DGEN_OK;
 }
 
+int32_t dgen_hourly_planes(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A,
+                           const dgen_outputs* O, int64_t n, void* ws, size_t ws_bytes,
+                           int64_t n_scratch, void* stream) {
+    if (!c || !T || !A || !O) { set_err("dgen_hourly_planes: null argument"); return DGEN_E_ARG; }
+    if (n <= 0) return DGEN_OK;
+    if (!O->baseline || !O->net_pvonly || !O->net_with_batt) {
+        set_err("dgen_hourly_planes: the three hourly planes are required");
+        return DGEN_E_ARG;
+    }
+    if (!T->shapes || !T->shape_sum || !T->cfs || !T->tariffs || T->n_tariffs <= 0 ||
+        (T->n_demand > 0 && !T->demand)) {
+        set_err("dgen_hourly_planes: incomplete tables");
+        return DGEN_E_ARG;
+    }
+    if (n >= ((int64_t)1 << (O->hourly_f64 ? 27 : 28)) || n_scratch >= ((int64_t)1 << 28)) {
+        set_err("dgen_hourly_planes: batch too large (n < 2^28 with f32 planes, 2^27 with f64)");
+        return DGEN_E_ARG;
+    }
+    if (!ws || ws_bytes < dgen_workspace_bytes(n, n_scratch)) {
+        set_err("dgen_hourly_planes: workspace too small (%zu < %zu)", ws_bytes,
+                dgen_workspace_bytes(n, n_scratch));
+        return DGEN_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    // the scan alone (no split or demand records: nothing reads them after it);
+    // it re-derives the battery run from the sizing outputs, so every output it
+    // writes besides the planes is the value the sizing call wrote
+    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK +
+                       (size_t)(BLOCK / 64) * HB_DAY_BYTES;
+    const dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK)), block(BLOCK);
+    const bool roll = c->cfg.batt_update_hours == 1;
+    for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
+        const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
+#define DGEN_HP_LAUNCH(F, R)                                                                       \
+        hipLaunchKernelGGL((k_hourly_batt<true, F, false, R, false>), grid, block, lds, s, *T, *A, *O, c->cfg, \
+                           n, ws, n_scratch, (int64_t)0, n, m0, m1, c->battery, 0, 0, nullptr, 0, 0)
+        if (O->hourly_f64) { if (roll) DGEN_HP_LAUNCH(true, true); else DGEN_HP_LAUNCH(true, false); }
+        else { if (roll) DGEN_HP_LAUNCH(false, true); else DGEN_HP_LAUNCH(false, false); }
+#undef DGEN_HP_LAUNCH
+    }
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
 int32_t dgen_set_hourly_segment(dgen_ctx* c, int32_t months) {
     if (!c || months < 1 || months > 12) {
         set_err("dgen_set_hourly_segment: months must be in [1, 12]");

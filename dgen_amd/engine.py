@@ -321,6 +321,15 @@ class Engine:
                                              self.stream_handle()),
                    "dgen_size_agents")
 
+    def hourly_planes(self, batch: AgentBatch, c_out: _lib.Outputs):
+        """The hourly planes of `batch`, already sized with the outputs `c_out`
+        points to (async, dgen_hourly_planes): the 8760-h scan alone."""
+        _lib.check(self.lib.dgen_hourly_planes(self.ctx, ctypes.byref(self.tables),
+                                               ctypes.byref(batch.c_agents), ctypes.byref(c_out),
+                                               batch.n, _ptr(batch.workspace), batch.workspace.numel(),
+                                               batch.n_scratch, self.stream_handle()),
+                   "dgen_hourly_planes")
+
     def set_pipeline(self, chunks: int):
         """Chunk-pipeline depth of size() (dgen_set_pipeline; 1 = no overlap)."""
         _lib.check(self.lib.dgen_set_pipeline(self.ctx, int(chunks)), "dgen_set_pipeline")

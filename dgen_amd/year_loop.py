@@ -277,9 +277,10 @@ class YearLoop:
     engine: a loaded Engine (tables set); pop: synth.Population of this rank's
     agents; agents: loop_agents(pop, ...); hourly_export: per-state 8760-h sums
     each year; hourly_chunk: None sizes the shard once with hourly planes and
-    exports from them in place (105 KB / agent of HBM), an int re-sizes the
-    shard in chunks of that many agents with a reusable plane buffer for the
-    export (the 2.5M-agents-per-GPU national case)."""
+    exports from them in place (105 KB / agent of HBM), an int sizes the shard
+    without planes and re-runs only the 8760-h scan (dgen_hourly_planes) in
+    chunks of that many agents into a reusable plane buffer for the export
+    (the 2.5M-agents-per-GPU national case)."""
 
     def __init__(self, engine, pop, agents: Dict[str, np.ndarray], tables: LoopTables,
                  first_year: int = 2026, hourly_export: bool = True,
@@ -372,11 +373,8 @@ class YearLoop:
         whole = hourly_export and hourly_chunk is None
         self.out = engine.alloc_outputs(n, hourly=whole)
         self.c_out = engine.c_outputs(self.out)
-        self._chunk_out = None
         if hourly_export and hourly_chunk is not None:
             ch = min(int(hourly_chunk), max(n, 1))
-            self._chunk_out = engine.alloc_outputs(ch, hourly=False)
-            self._chunk_out = {k: v for k, v in self._chunk_out.items() if v is not None}
             self._chunk_planes = {k: torch.empty(_lib.NH * ch, dtype=torch.float32, device=dev)
                                   for k in _lib.OUTPUT_HOURLY}
         self.Ld, self.La = _bind_diff(engine.lib), _bind_attach(engine.lib)
@@ -467,11 +465,23 @@ class YearLoop:
         if self.hourly_chunk is None:
             planes = (self.out["baseline"], self.out["net_pvonly"], self.out["net_with_batt"])
             return state_hourly(eng, planes, w, self.s_dev_idx, self.s_off)
-        # chunked: re-size each chunk of device rows with hourly planes, sum
-        # its members per state (the planes depend only on the agent)
+        # chunked: each chunk of device rows gets its hourly planes from the
+        # scan alone (dgen_hourly_planes, from this year's sizing outputs:
+        # the chunk's slices of self.out), then its members are summed per
+        # state (the planes depend only on the agent)
         from .engine import AgentBatch
         S = len(self.local_states)
-        pos = {s: j for j, s in enumerate(self.local_states)}
+        if getattr(self, "_chunk_groups", None) is None:
+            # per chunk: its rows grouped by local state (fixed across years)
+            ls = np.asarray(self.local_states, np.int64)
+            pos = np.full(int(ls.max()) + 1 if ls.size else 1, -1, np.int64)
+            pos[ls] = np.arange(ls.size)
+            self._chunk_groups = []
+            for a in range(0, self.n, int(self.hourly_chunk)):
+                p = pos[self.state_dev_order[a:a + int(self.hourly_chunk)]]
+                cnt = np.bincount(p, minlength=S)
+                self._chunk_groups.append((np.argsort(p, kind="stable"),
+                                           np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)))
         acc = torch.zeros((S, _lib.NH), dtype=torch.float64, device=eng.dev)
         ch = int(self.hourly_chunk)
         B = self.batch
@@ -483,18 +493,15 @@ class YearLoop:
             ca.max_years = B.c_agents.max_years
             sub = AgentBatch(n=m, n_scratch=B.n_scratch, cols=cols, workspace=B.workspace,
                              c_agents=ca, nb_scan=B.nb_scan)
-            # prefixes of the chunk buffers: [m] scalars, [m][26] yearly, and the
-            # first 8760*m floats of each plane viewed as [2190][m][4] tiles
-            out = {k: v[:m] for k, v in self._chunk_out.items()}
+            # the chunk's rows of the sizing outputs, and the first 8760*m floats
+            # of each plane buffer viewed as [2190][m][4] tiles
+            out = {k: v[a:b] for k, v in self.out.items() if v is not None}
             out.update({k: v[:_lib.NH * m].view(_lib.NH // 4, m, 4)
                         for k, v in self._chunk_planes.items()})
             co = eng.c_outputs(out)
             planes = (out["baseline"], out["net_pvonly"], out["net_with_batt"])
-            eng.size(sub, None, co)
-            st = self.state_dev_order[a:b]
-            order = np.argsort(np.array([pos[s] for s in st], np.int64), kind="stable")
-            cnt = np.bincount(np.array([pos[s] for s in st], np.int64), minlength=S)
-            off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+            eng.hourly_planes(sub, co)
+            order, off = self._chunk_groups[a // ch]
             wc = tuple(x[a:b] for x in w)
             acc += state_hourly(eng, planes, wc, order, off)
         return acc

@@ -518,6 +518,19 @@ int32_t dgen_kernel_times(dgen_ctx* ctx, double* ms_size, double* ms_hourly, dou
  * Replaces nothing in the reference (its per-agent loop is serial, ff:1149). */
 int32_t dgen_set_pipeline(dgen_ctx* ctx, int32_t chunks);
 
+/* The hourly planes of a batch already sized by dgen_size_agents (same ctx
+ * settings, same tables / agents / workspace), without re-sizing it: the
+ * 8760-h scan alone, re-deriving the battery run from O's sizing outputs
+ * (system_kw, x_last, tariff_final, switched, status); every other output it
+ * writes gets the value the sizing call wrote.  For shards whose planes do not
+ * fit beside the batch (dgen_amd.year_loop's chunked per-state export): size
+ * the whole shard without planes, then call this per chunk of agents with the
+ * chunk's slices of O and a plane buffer.  Replaces nothing in the reference
+ * (its lists come out of the one sizing call, ff:505-539).                  */
+int32_t dgen_hourly_planes(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
+                           const dgen_outputs* outputs, int64_t n, void* workspace, size_t workspace_bytes,
+                           int64_t n_scratch, void* stream);
+
 /* Months of the year per k_hourly_batt launch (the sequential 8760-h scan of
  * dgen_size_agents): the year is swept in ceil(12 / months) launches, SOC and
  * the annual PV sum carried between them in the workspace, so that all
