@@ -37,6 +37,9 @@ VARIANTS = {
                   ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1")],
     # demand envelopes prebuilt by k_dc_env ahead of k_size (A/B: slower)
     "dc_prebuild": [("#define DGEN_DC_PREBUILD 0", "#define DGEN_DC_PREBUILD 1")],
+    # hour-lane envelope build: days of loads in flight per lane
+    "dcb16": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 16;")],
+    "dcb12": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 12;")],
     # phase timers only (DGEN_PHASE_PROF slots, see dgen_hip.hip)
     "phase": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1")],
     # k_size builds the demand envelopes with the serial month lanes
