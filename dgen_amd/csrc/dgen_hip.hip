@@ -2313,6 +2313,7 @@ constexpr int DCS_CAP = 128;                       // lines per agent (else the 
 constexpr int DCS_NG = 12 * DCP;
 struct DcStage {
     double2 lines[DCS_CAP];
+    double gen[DCS_CAP];     // the lines' generation at the current evaluation's kW (yl_dc_gen)
     uint16_t off[DCS_NG + 1];
     uint16_t pad[(8 - (DCS_NG + 1) % 8) % 8];
 };
@@ -2355,6 +2356,17 @@ __device__ __forceinline__ bool yl_dc_stage(const DcEnv& E, DcStage* st, const S
     if (g.sl == 0) st->off[DCS_NG] = (uint16_t)base;
     wave_lds_sync();
     return true;
+}
+
+// Each staged line's generation term at this evaluation's kW, ref_gen(g, kW):
+// the same for every year lane of the agent, so the segment's lanes form it
+// once per line (a division each) instead of every lane for every line.
+template <int LPA>
+__device__ __forceinline__ void yl_dc_gen(DcStage* st, double kw, const Seg<LPA>& g) {
+    const int n = st->off[DCS_NG];
+    wave_lds_sync();                                   // the previous evaluation's reads
+    for (int k = g.sl; k < n; k += LPA) st->gen[k] = ref_gen(st->lines[k].y, kw);
+    wave_lds_sync();
 }
 
 // The same envelopes built by the segment's hour lanes (k_size: the serial
@@ -2536,22 +2548,32 @@ __device__ __forceinline__ bool yl_dc_build_any(const dgen_demand* D, const YSrc
 // reference's operation order), or the no-system peaks (max load) when !with_gen.
 // st: the agent's staged lines (or nullptr: the global record).
 __device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& E, double kw, double s,
-                                             bool with_gen, const YLds& S, const DcStage* st = nullptr) {
+                                             bool with_gen, const YLds& S, const DcStage* st = nullptr,
+                                             int nq = DCP) {
+    // nq: the batch's demand periods (dgen_tables.max_dc_periods): a period no
+    // schedule uses has no hours, a zero peak and a zero charge
     double total = 0.0;
     for (int m = 0; m < 12; m++) {
         double flat = 0.0;
-        for (int q = 0; q < DCP; q++) {
+        for (int q = 0; q < nq; q++) {
             const int gk = m * DCP + q;
             const int o0 = (st && with_gen) ? st->off[gk] : 0;
             const int n_l = (st && with_gen) ? st->off[gk + 1] - o0 : E.cnt[gk];
             double pk = 0.0;
             if (n_l > 0) {
                 if (with_gen) {
-                    const double2* ln = st ? st->lines + o0 : E.lines + gk * DC_NL;
-                    for (int k = 0; k < n_l; k++) {
-                        const double2 v = ln[k];
-                        const double imp = v.x - ref_gen(v.y, kw) * s;
-                        pk = imp > pk ? imp : pk;
+                    if (st) {                  // the stage: generation formed by yl_dc_gen
+                        for (int k = 0; k < n_l; k++) {
+                            const double imp = st->lines[o0 + k].x - st->gen[o0 + k] * s;
+                            pk = imp > pk ? imp : pk;
+                        }
+                    } else {
+                        const double2* ln = E.lines + gk * DC_NL;
+                        for (int k = 0; k < n_l; k++) {
+                            const double2 v = ln[k];
+                            const double imp = v.x - ref_gen(v.y, kw) * s;
+                            pk = imp > pk ? imp : pk;
+                        }
                     }
                 } else {
                     pk = E.maxl[gk];
@@ -2562,7 +2584,7 @@ __device__ __forceinline__ double yl_dc_eval(const dgen_demand* D, const DcEnv& 
         }
         if (S.pk) S.pk[m * WAVE] = flat;          // the month's peak import (kWh/kW tiers)
         double c = dc_tier_charge(flat, D->flat_cap[m], D->flat_price[m], D->flat_nt[m]);
-        for (int q = 0; q < DCP; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
+        for (int q = 0; q < nq; q++) c += dc_tier_charge(S.at(q), D->tou_cap[q], D->tou_price[q], D->tou_nt[q]);
         total += c;
     }
     return total;
@@ -3036,7 +3058,7 @@ __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double
         // the month's 48 slot sums of both rows in batches of BB (2 BB loads
         // in flight, branch-free), then the period's slots added in slot order
         // (the oracle's order; a skipped slot is a select, not a + 0.0)
-        constexpr int BB = 4;
+        constexpr int BB = 8;
         const double* lm = lslots + m * 48;
         const double* gm = gslots + m * 48;
         for (int dt = 0; dt < 2; dt++) {
@@ -3174,6 +3196,7 @@ struct YCtx {
     char* nb;                   // the agent's net-billing split record (or nullptr)
     bool nb_ok;                 // the split of the current (mo 2) tariff fits
     int nb_tag;                 // 1 + the tariff the record holds the split of (0: none)
+    int dc_nq;                  // the batch's demand periods (dgen_tables.max_dc_periods)
     bool nb_pending;            // the current (mo 2) tariff's split is not formed yet
     int env_tag;                // 1 + the tariff the envelopes are of (0: none)
     double tlo, thi;            // generation-scale range of the search
@@ -3247,7 +3270,7 @@ __device__ __forceinline__ void yl_set_tariff(YCtx<LPA>& c, int tix) {
             // charge, when billed, joins the no-system bill below)
             c.env_ok = yl_dc_ready(c, c.env, c.stg, c.g);
             c.stg_ok = c.env_ok && c.stg && yl_dc_stage(c.env, c.stg, c.g);
-            const double v0 = c.env_ok ? yl_dc_eval(c.dem, c.env, 0.0, 1.0, false, c.S)
+            const double v0 = c.env_ok ? yl_dc_eval(c.dem, c.env, 0.0, 1.0, false, c.S, nullptr, c.dc_nq)
                                        : yl_demand(c.dem, c.src, 0.0, 1.0, false, c.S);
             wo_dem = c.dem_bill ? v0 : 0.0;
             c.dem_wo_pending = false;
@@ -3302,7 +3325,8 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
             // kWh/kW tiers: this evaluation's month peaks (and demand charge)
             // ahead of the energy bill, whose tier caps scale with them
             c.src.gen_scale = kws;
-            const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, c.s_y, true, c.S, c.stg_ok ? c.stg : nullptr)
+            if (c.env_ok && c.stg_ok) yl_dc_gen(c.stg, kw, c.g);
+            const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, c.s_y, true, c.S, c.stg_ok ? c.stg : nullptr, c.dc_nq)
                                       : yl_demand(c.dem, c.src, kw, c.s_y, true, c.S);
             v13 = c.dem_bill ? v : 0.0;
         }
@@ -3349,10 +3373,11 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
                 PH_CNT(7, 1, c.g.sl == 0);
             }
             PH_T0(tde);
+            if (c.env_ok && c.stg_ok) yl_dc_gen(c.stg, kw, c.g);
             for (int pass = c.dem_wo_pending ? 0 : 1; pass < 2; pass++) {
                 const bool wg = pass == 1;
                 const double s = wg ? c.s_y : 1.0;
-                const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, s, wg, c.S, c.stg_ok ? c.stg : nullptr)
+                const double v = c.env_ok ? yl_dc_eval(c.dem, c.env, kw, s, wg, c.S, c.stg_ok ? c.stg : nullptr, c.dc_nq)
                                           : yl_demand(c.dem, c.src, kw, s, wg, c.S);
                 if (wg) wb += v;
                 else c.wo1 += v;
@@ -3415,6 +3440,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.stg = nullptr;
     c.stg_ok = false;
     c.env_tag = 0;
+    c.dc_nq = (T.max_dc_periods > 0 && T.max_dc_periods <= DCP) ? T.max_dc_periods : DCP;
     if constexpr (DC) {
         if (dcws) {
             c.env = dc_env_at(dcws, i);

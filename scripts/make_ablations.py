@@ -37,6 +37,9 @@ VARIANTS = {
                   ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1")],
     # demand envelopes prebuilt by k_dc_env ahead of k_size (A/B: slower)
     "dc_prebuild": [("#define DGEN_DC_PREBUILD 0", "#define DGEN_DC_PREBUILD 1")],
+    # NEM bins build: slot-sum loads in flight per batch (4 = the product)
+    "bins_bb8": [("        constexpr int BB = 4;\n", "        constexpr int BB = 8;\n")],
+    "bins_bb12": [("        constexpr int BB = 4;\n", "        constexpr int BB = 12;\n")],
     # hour-lane envelope build: days of loads in flight per lane
     "dcb16": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 16;")],
     "dcb12": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 12;")],
