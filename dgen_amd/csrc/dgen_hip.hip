@@ -65,6 +65,7 @@ constexpr int MAXP = DGEN_MAXP;
 constexpr int MAXT = DGEN_MAXT;
 constexpr int MAXY = DGEN_MAXY;
 constexpr int NBIN = 12 * MAXP;
+constexpr int PREG = 4;   // periods whose NEM month recursion runs in registers
 constexpr int DCP = DGEN_DCP;
 constexpr int DCT = DGEN_DCT;
 constexpr int BLOCK = 128;   // threads per block for the per-agent kernels
@@ -797,6 +798,20 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
     }
 }
 
+// The battery case's bills and cash flow for a NEM agent, in the scan's tail
+// (defined after the year-lane engine; see hb_finance_nem).  Off by default:
+// A/B on C3 1M (DGEN_FIN_FOLD=1) k_hourly_batt 24.9 -> 31.3 ms against the
+// 3.9 ms k_batt_finance it replaces -- the year-lane kernel is VALU-bound,
+// not launch-bound, and one thread's 25 sequential years cost as much VALU
+// per agent as the lanes' (every wave runs the union of its agents' periods
+// and tiers) while lengthening the last month segment.
+__device__ __forceinline__ void hb_finance_nem(const dgen_tariff& t, const dgen_agents& A, const dgen_outputs& O,
+                                               const dgen_cfg& cfg, int64_t i, const double2* lg, double kw,
+                                               double bank, double otc, bool same_tariff);
+#ifndef DGEN_FIN_FOLD
+#define DGEN_FIN_FOLD 0
+#endif
+
 // F64: the hourly planes as doubles (the reference's fp64 lists) instead of
 // floats: the same values the scan computes, 32 B per lane per hour quad.
 // NB: the batch has net-billing scratch slots; the scan then also builds the
@@ -825,7 +840,7 @@ template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR>
 __global__ void __launch_bounds__(BLOCK, ROLL ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
-              int repair, char* dcr, int dc_nq, int dcr_cap) {
+              int repair, char* dcr, int dc_nq, int dcr_cap, int fin) {
     // agents [i0, i1) of a batch of n (row stride of every plane stays n),
     // months [m_lo, m_hi) of the year: the year is swept in month segments,
     // one launch each, so that every resident wave works on the same weeks
@@ -1297,7 +1312,17 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // battery run on the PV run's tariff: k_batt_finance reuses its no-system
     // bill (same load, same tariff -> the same bill, as in the oracle)
     if (!repair) {   // the repair pass starts from the already switched tariff
-        W.aux[i] = (tariff != O.tariff_final[i]) ? 1.0 : 0.0;
+        const bool same = tariff == O.tariff_final[i];
+        // DGEN_FIN_FOLD: the battery-case finance of a NEM agent (bins, no
+        // demand record, first-tier prices in registers) runs here and
+        // k_batt_finance skips it (aux 2)
+        const int N = A.econ_life[i];
+        const bool fold = DGEN_FIN_FOLD && fin && batt_on && !unsized && !mo2 && !has_dc && t.mo == 0 &&
+                          t.P <= PREG && !peak_unit(t) && N >= 1 && N <= MAXY &&
+                          !(status & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH |
+                                      DGEN_ST_UNIT));
+        if (fold) hb_finance_nem(t, A, O, cfg, i, W.LGb + (int64_t)i * NBIN, kw_star, bank, otc, same);
+        W.aux[i] = fold ? 2.0 : (same ? 0.0 : 1.0);
         O.tariff_final[i] = tariff;
         O.switched[i] = switched;
     }
@@ -1553,7 +1578,6 @@ __device__ __forceinline__ double yl_bill_mo0(const dgen_tariff& t, const YLds& 
 // Same bill with the per-period credits and billed kWh in registers (P <= 4,
 // the common case): loops run to the compile-time bound under the uniform
 // guard p < P, so the order of every sum is the LDS version's.
-constexpr int PREG = 4;
 __device__ __forceinline__ double yl_bill_mo0_reg(const dgen_tariff& t, const YLds& S, double gscale,
                                                   double yearend) {
     const int P = t.P, T = t.T, half = S.half;
@@ -3172,6 +3196,151 @@ __device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev
     return f;
 }
 
+// k_batt_finance_w's NEM branch for one agent in one thread (the tail of
+// k_hourly_batt): the same per-year arithmetic -- yl_bill_mo0_reg's month
+// recursion on the agent's (load, system) bins, the year's escalation and
+// degradation factors by sequential products (pow_seq), yl_make_loan and
+// yl_cashflow's per-year terms -- with the NPV summed in year order instead of
+// the lanes' butterfly (npv_pv_batt within rounding of the year-lane form;
+// every per-year output bit-identical).
+constexpr int TH_MB = 3;    // months of bins loaded together in the tail's bill
+__device__ __forceinline__ double th_bill_mo0(const dgen_tariff& t, const double2* lg, double gscale,
+                                              double yearend) {
+    const int P = t.P, T = t.T;
+    const double fixed = t.fixed;
+    double b0[PREG], credit[PREG], u[PREG];
+#pragma unroll
+    for (int p = 0; p < PREG; p++) { b0[p] = p < P ? t.buy[p][0] : 0.0; credit[p] = 0.0; u[p] = 0.0; }
+    double total = 0.0;
+#pragma unroll 1
+    for (int m0 = 0; m0 < 12; m0 += TH_MB) {
+        // TH_MB months of (load, system) bins in flight together (L2-resident:
+        // the scan wrote them), static register indices
+        double2 bv[TH_MB][PREG];
+#pragma unroll
+        for (int k = 0; k < TH_MB; k++)
+#pragma unroll
+            for (int p = 0; p < PREG; p++)
+                bv[k][p] = p < P ? lg[(m0 + k) * P + p] : make_double2(0.0, 0.0);
+#pragma unroll
+        for (int k = 0; k < TH_MB; k++) {
+            const int m = m0 + k;
+#pragma unroll
+            for (int p = 0; p < PREG; p++) {
+                if (p < P) {
+                    double nn = bv[k][p].x - gscale * bv[k][p].y;
+                    double use = nn < credit[p] ? nn : credit[p];
+                    double un = nn - use;
+                    double cn = credit[p] - use;
+                    const bool pos = nn >= 0.0;
+                    u[p] = pos ? un : 0.0;
+                    credit[p] = pos ? cn : credit[p] + -nn;
+                }
+            }
+            double U = 0.0;
+#pragma unroll
+            for (int p = 0; p < PREG; p++)
+                if (p < P) U += u[p];
+            double charge = 0.0;
+            if (U > 0.0) {
+                if (T == 1) {
+#pragma unroll
+                    for (int p = 0; p < PREG; p++)
+                        if (p < P) charge += u[p] * b0[p];
+                } else {
+                    double fr[PREG];
+#pragma unroll
+                    for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
+                    const double scale = tier_scale(t, m, nullptr);
+                    double prev = 0.0;
+                    for (int kk = 0; kk < T; kk++) {
+                        double hi = (kk == T - 1) ? INFINITY : t.cap[kk] * scale;
+                        double top = U < hi ? U : hi;
+                        double amt = top - prev;
+                        if (amt < 0.0) amt = 0.0;
+                        if (hi > prev) prev = hi;
+#pragma unroll
+                        for (int p = 0; p < PREG; p++)
+                            if (p < P) charge += fr[p] * amt * (kk == 0 ? b0[p] : t.buy[p][kk]);
+                    }
+                }
+            }
+            double bill = fixed + charge;
+            if (m == 11) {
+                double cc = 0.0;
+#pragma unroll
+                for (int p = 0; p < PREG; p++)
+                    if (p < P) cc += credit[p];
+                bill -= cc * yearend;
+            }
+            total += bill;
+        }
+    }
+    return total;
+}
+
+__device__ __forceinline__ void hb_finance_nem(const dgen_tariff& t, const dgen_agents& A, const dgen_outputs& O,
+                                               const dgen_cfg& cfg, int64_t i, const double2* lg, double kw,
+                                               double bank, double otc, bool same_tariff) {
+
+    const bool is_res = (A.flags[i] & 1) != 0;
+    const int N = A.econ_life[i];
+    const double rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
+    const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+    const double system_costs = (kw > 0.0) ? A.capex_combined[i] * kw : A.capex[i] * kw;   // ff:203-216
+    const double batt_costs = A.batt_capex_kwh[i] * bank * 0.7;                           // ff:219
+    const double C = ((system_costs + batt_costs) * A.ccm[i]) + 0.0 + otc;
+    const double vor = A.vor[i];
+    const double yearend = cfg.nm_yearend_sell_rate;
+    const double wo1 = same_tariff ? O.first_without[i] : th_bill_mo0(t, lg, 0.0, yearend);
+    // yl_cashflow's agent-level terms
+    const YLoan L1 = yl_make_loan(A, cfg, i, N, is_res, 1);
+    const double debt = L1.debt_frac * C;
+    double pmt = 0.0;
+    if (L1.term > 0 && debt != 0.0) {
+        if (L1.r_loan != 0.0) pmt = debt * L1.r_loan / (1.0 - 1.0 / L1.loan_f);
+        else pmt = debt / (double)L1.term;
+    }
+    double itc = L1.itc_pct * 0.01 * C;
+    if (itc > L1.itc_max) itc = L1.itc_max;
+    const double basis = C - 0.5 * itc;
+    const int64_t row = i * (MAXY + 1);
+    O.cfev_batt[row] = 0.0;
+    O.bill_w_batt[row] = 0.0;
+    O.bill_wo_batt[row] = 0.0;
+    double r_y = 1.0, s_y = 1.0, npv_sum = 0.0;
+    for (int y = 1; y <= N; y++) {
+        if (y > 1) { r_y = r_y * rate_base; s_y = s_y * sys_base; }        // pow_seq(·, y - 1)
+        const YLoan L = yl_make_loan(A, cfg, i, N, is_res, y);
+        const double wb = th_bill_mo0(t, lg, s_y, yearend);
+        const double w = wb * r_y;
+        const double wo = wo1 * r_y;
+        const double ev = (wo - w) + vor;                                  // ff:275
+        const double oe = (L.ins_rate * C) * L.ins_esc;
+        const bool paying = y <= L.term && pmt != 0.0;
+        const double payment = paying ? pmt : 0.0;
+        const double itc_y = (y == 1) ? itc : 0.0;
+        double sta_tax = 0.0, fed_tax = 0.0;
+        if (L.market != 0) {
+            double bal = debt;
+            const int kend = min(min(y, L.term + 1), L.N + 1);
+            if (pmt != 0.0)
+                for (int k = 1; k < kend; k++) bal = bal - (pmt - bal * L.r_loan);
+            const double interest = paying ? bal * L.r_loan : 0.0;
+            const double dep = depr_frac(L.depr_type, y, L.sl_years) * basis;
+            sta_tax = L.sta * (ev - oe - interest - dep);
+            fed_tax = L.fed * (ev - oe - interest - dep - sta_tax);
+        }
+        const double taxsav = itc_y - sta_tax - fed_tax;
+        const double atcf = ev - oe - payment + taxsav;
+        npv_sum += atcf * L.df;
+        O.cfev_batt[row + y] = ev;
+        O.bill_w_batt[row + y] = w;
+        O.bill_wo_batt[row + y] = wo;
+    }
+    O.npv_pv_batt[i] = -(C - debt) + npv_sum;
+}
+
 struct YLast {   // per-lane results of the most recent evaluation
     double total, ev, w, wo;
     YFlow flow;
@@ -3713,6 +3882,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     if (i >= i1) return;
     const int st = O.status[i];
     if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH | DGEN_ST_UNIT)) return;
+    if (ws_layout(ws, n).aux[i] == 2.0) return;   // its finance ran in k_hourly_batt's tail
     PH_T0(t_all);
     const Seg<LPA> g(lane);
     const int y = g.sl + 1;
@@ -4719,17 +4889,17 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     do {                                                                                          \
         if (nb_scan && !(REP) && dcr_on && !(R))                                                  \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, true>), grid, block, lds, s2, *T, *A, *O, \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, dcr, dc_nq, c->dcr_enable); \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, dcr, dc_nq, c->dcr_enable, m1 == 12); \
         else if (nb_scan && !(REP))                                                               \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true, R, false>), grid, block, lds, s2, *T, *A, *O, c->cfg, \
-                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0); \
+                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0, m1 == 12); \
         else if (!(REP) && dcr_on && !(R))                                                        \
             hipLaunchKernelGGL((k_hourly_batt<H, F, false, false, true>), grid, block, lds, s2, *T, *A, *O, \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, 0, dcr, dc_nq, c->dcr_enable); \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, 0, dcr, dc_nq, c->dcr_enable, m1 == 12); \
         else                                                                                      \
             hipLaunchKernelGGL((k_hourly_batt<H, F, false, R, false>), grid, block, lds, s2, *T, *A, *O, \
                                c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? rep_mask : 0, \
-                               (REP) ? dcr : nullptr, 0, 0);                                      \
+                               (REP) ? dcr : nullptr, 0, 0, (REP) ? 0 : (m1 == 12));                                      \
     } while (0)
 #define DGEN_HB_LAUNCH(H, F, REP)                                                                 \
     do {                                                                                          \
@@ -4830,7 +5000,7 @@ int32_t dgen_hourly_planes(dgen_ctx* c, const dgen_tables* T, const dgen_agents*
         const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
 #define DGEN_HP_LAUNCH(F, R)                                                                       \
         hipLaunchKernelGGL((k_hourly_batt<true, F, false, R, false>), grid, block, lds, s, *T, *A, *O, c->cfg, \
-                           n, ws, n_scratch, (int64_t)0, n, m0, m1, c->battery, 0, 0, nullptr, 0, 0)
+                           n, ws, n_scratch, (int64_t)0, n, m0, m1, c->battery, 0, 0, nullptr, 0, 0, 0)
         if (O->hourly_f64) { if (roll) DGEN_HP_LAUNCH(true, true); else DGEN_HP_LAUNCH(true, false); }
         else { if (roll) DGEN_HP_LAUNCH(false, true); else DGEN_HP_LAUNCH(false, false); }
 #undef DGEN_HP_LAUNCH
