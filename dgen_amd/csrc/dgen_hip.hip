@@ -833,6 +833,21 @@ __device__ __forceinline__ void hb_finance_nem(const dgen_tariff& t, const dgen_
 // lane), so the network appears once per hour of the day (~27k instructions),
 // and the form runs one wave per SIMD: the window, its sorted copy and both
 // days' raw values need ~400 registers.
+// XCD-aware block order (DGEN_XCD_REMAP): the hardware deals consecutive
+// blocks round-robin to the 8 XCDs, each with its own L2; consecutive agents
+// (load-major device order) share profile rows, so logical block k goes to the
+// hardware slot that keeps runs of consecutive blocks on one XCD.  A bijection
+// on [0, nb).
+#ifndef DGEN_XCD_REMAP
+#define DGEN_XCD_REMAP 0
+#endif
+__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned nb) {
+    if (!DGEN_XCD_REMAP) return b;
+    constexpr unsigned X = 8;
+    const unsigned q = nb / X, r = nb % X, x = b % X, k = b / X;
+    return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
 // DCR: the batch bills demand charges (or kWh/kW tier peaks) and has room for
 // the battery-case demand records (dcr: DCR_BYTES per scratch slot, dc_nq the
 // batch's demand periods, which size the scan's per-period LDS maxima).
@@ -846,7 +861,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // one launch each, so that every resident wave works on the same weeks
     // and the profile-row slices they read stay in L2 / MALL (SOC and the
     // running annual PV sum carry between launches in W.carry)
-    int64_t i = i0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    int64_t i = i0 + (int64_t)xcd_block(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     if (i >= i1) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
     // repair pass: only the agents whose scan-built split (repair bit 1) or

@@ -45,6 +45,8 @@ VARIANTS = {
     "dcb12": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 12;")],
     # battery-case NEM finance in k_hourly_batt's tail (A/B: slower)
     "fin_fold": [("#define DGEN_FIN_FOLD 0", "#define DGEN_FIN_FOLD 1")],
+    # XCD-aware block order in k_hourly_batt
+    "xcd": [("#define DGEN_XCD_REMAP 0", "#define DGEN_XCD_REMAP 1")],
     # phase timers only (DGEN_PHASE_PROF slots, see dgen_hip.hip)
     "phase": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1")],
     # k_size builds the demand envelopes with the serial month lanes

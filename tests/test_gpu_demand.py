@@ -49,7 +49,7 @@ def _xatol(load_kwh, naep):
     return max(2.0, float(int(max(hi_lo, 1.0) * 1e-3)))
 
 
-def _check(o, ref, life, pop):
+def _check(o, ref, life, pop, max_flips=0):
     """Demand charges make the objective piecewise linear in kW; at its kinks a
     Brent comparison can flip on the last-bit rounding difference between the
     device's and the oracle's import arithmetic (one agent in 160 observed).
@@ -75,9 +75,10 @@ def _check(o, ref, life, pop):
                          ("cash_flow", "cash_flow")):
             assert np.allclose(o[k_o][i, :N1], r[k_r], rtol=1e-6, atol=1e-5), (i, k_o)
     print(f"demand-charge Brent path flips: {flipped} of {len(ref)}", flush=True)
-    # measured: 0, 0 and 1 of 160 (the net-billing long-life case, whose energy
-    # bills re-associate the split sums); each flipped agent is held to xatol above
-    assert flipped <= 1, flipped
+    # measured: 0, 0 and 1 of 160; a flip is allowed only where the energy bill
+    # re-associates the net-billing split sums over 33-50-year lanes (the
+    # long-life net-billing case), and the flipped agent is held to xatol above
+    assert flipped <= max_flips, flipped
 
 
 @pytest.mark.parametrize("net_billing,long_life", [(False, False), (True, False), (True, True)])
@@ -87,7 +88,8 @@ def test_demand_charges_match_oracle(engine_dc, net_billing, long_life):
     o = _run(engine_dc, pop, pop.demand)
     opop = helpers.oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs,
                                      pop.wholesale, demand=pop.demand)
-    _check(o, opop.run(orc.make_cfg()), pop.cols["econ_life"], pop)
+    _check(o, opop.run(orc.make_cfg()), pop.cols["econ_life"], pop,
+           max_flips=1 if (net_billing and long_life) else 0)
 
 
 def test_reference_mode_ignores_demand_records(engine, engine_dc):
