@@ -768,6 +768,18 @@ __device__ __forceinline__ void day_read(uint32_t a, DayRaw& r) {
     }
 }
 
+// One hour of the day buffer (ROLL: tomorrow's hour hh, after its DMA landed):
+// shape at chunk hh / 4, cf at chunk 6 + hh / 4 (compile-time offsets).
+__device__ __forceinline__ void day_hour(uint32_t a, int hh, float& s, int32_t& c) {
+    const uint32_t o = (uint32_t)(hh >> 2) * 1024u + (uint32_t)(hh & 3) * 4u;
+    asm volatile("ds_read_b32 %0, %2\n\t"
+                 "ds_read_b32 %1, %3\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(s), "=&v"(c)
+                 : "v"(a + o), "v"(a + o + 6144u)
+                 : "memory");
+}
+
 // Read the day buffer again (no vmcnt wait: it already landed).
 __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
     f32x4 s0, s1, s2, s3, s4, s5;
@@ -1046,9 +1058,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     day_dma(d_lo);
     const int d_last = c_month_start_day[m_hi] - 1;
     DayRaw r;
-    DayRaw r2;                     // ROLL: tomorrow's raw values
     double win[24];                // ROLL: the 24-hour window's deficits by hour of day
-    (void)r2;
     (void)win;
     double2* const bins2 = bins + (size_t)lds_half(T.max_periods) * BLOCK;   // NB: export sums
     for (int m = m_lo; m < m_hi; m++) {
@@ -1106,7 +1116,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 for (int hh = 0; hh < 24; hh++)
                     win[hh] = fmax((double)r.s[hh] * ls - (double)r.c[hh] * cs6, 0.0);
                 day_dma(d + 1 < 365 ? d + 1 : 0);
-                day_read<0>(dlane, r2);                    // vmcnt(0): tomorrow has landed
+                // tomorrow's values are read from the buffer hour by hour
+                // (below): wait here until its DMA has landed
+                __builtin_amdgcn_s_waitcnt(0x0f70);        // vmcnt(0)
             } else if (has_batt) {
                 // the day's deficits d_h = max(load_h - pv_h, 0), sorted; the raw
                 // registers are dead meanwhile and re-read from the LDS buffer
@@ -1167,8 +1179,12 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 }
                 HourStep st = batt_hour(nn, pv, target, power, bank, soc, cfg, inv_eta_in,
                                         in_per_bank, out_per_bank);
-                if constexpr (ROLL)     // the window moves on: tomorrow's hour hh comes in
-                    win[hh] = fmax((double)r2.s[hh] * ls - (double)r2.c[hh] * cs6, 0.0);
+                if constexpr (ROLL) {   // the window moves on: tomorrow's hour hh comes in
+                    float ts;
+                    int32_t tc;
+                    day_hour(dlane, hh, ts, tc);
+                    win[hh] = fmax((double)ts * ls - (double)tc * cs6, 0.0);
+                }
                 if constexpr (HOURLY) {
                     const double dn = ld - pl;
                     qb[hh & 3] = (PT)ld;
