@@ -33,43 +33,88 @@ NH = 8760
 ROW_BYTES = NH * 4              # one f32 load-shape row or one i32 cf row
 PLANE_BYTES = NH * 4            # one f32 hourly output plane per agent
 SYS_BYTES = NH * 8              # the battery case's f64 system-output plane per agent
-NB_BYTES = 59968                # net-billing split record per scratch slot (DGEN_NB_BYTES)
 
 
-def algorithmic_bytes(cols, hourly: bool, battery: bool):
+MAXP, DCP = 12, 8                 # include/dgen_hip.h DGEN_MAXP / DGEN_DCP
+DCR_HEAD = 2 * 12 * DCP * 8 + 64  # a demand record's per-(month, period) max load + lower bound
+
+
+def scratch_paths(cols, recs, tariff_final, *, battery=True, skip_dc=True, nb_scan=True,
+                  dcr_on=True, has_wholesale=True):
+    """Which scratch-slot agents move the battery case's f64 system-output
+    plane and which hand k_batt_finance a compact record instead, per agent in
+    the order of `cols` (dgen_hip.hip k_hourly_batt: put_sys / put_nb / put_dcr
+    / skip_plane).  `tariff_final` is the battery case's tariff (after the
+    storage switch, outputs["tariff_final"]); `recs` the engine's tariff
+    records (Engine.tariff_records).  Returns (plane, nb_rec, dcr_rec, mo2, P)
+    boolean / int arrays.  Agents whose record overflowed (the repair pass
+    writes their plane) are counted as record agents: a lower bound."""
+    tf = np.asarray(tariff_final, np.int64)
+    sl = np.asarray(cols["scratch_slot"]) >= 0
+    mo, dc, unit = recs["mo"][tf], recs["dc"][tf], recs["unit"][tf]
+    P = recs["P"][tf].astype(np.int64)
+    mo2 = (mo == 2) | (mo == 3)
+    has_dc = (dc > 0) & ((not skip_dc) | (unit == 1) | (unit == 3))
+    ca = (np.asarray(cols["flags"]) & 2) != 0
+    ts_on = (mo == 2) & ~ca & (np.asarray(cols["wholesale_row"]) >= 0) & bool(has_wholesale)
+    put_sys = (mo2 | has_dc) & sl & bool(battery)
+    put_nb = put_sys & mo2 & ~ts_on & bool(nb_scan)
+    put_dcr = put_sys & has_dc & bool(dcr_on)
+    skip = (put_nb & ~has_dc) | (put_dcr & ~mo2)
+    return put_sys & ~skip, put_nb, put_dcr, mo2, P
+
+
+def algorithmic_bytes(cols, hourly: bool, battery: bool, paths=None, recs=None):
     """ALGORITHMIC HBM bytes per step of each sizing kernel for this population
     (DESIGN.md section 5): the bytes the step cannot avoid moving.  Profile
-    rows are shared: every distinct load-shape / cf row the batch uses must be
-    read once (not once per agent -- per-agent row reads that hit in L2 / MALL
-    are not HBM traffic); per-agent inputs and outputs are moved once each.
+    rows are shared: every distinct load-shape / cf row the batch uses is read
+    once (a per-agent re-read that hits L2 / MALL is not HBM traffic);
+    per-agent inputs and outputs are moved once each.
       k_size          the distinct rows' 576 (month, daytype, hour) slot sums
                       (f64, both tables), ~24 scalars and 4 yearly output
-                      arrays of N+1 f64 per agent; agents that bill hourly
-                      imports (net billing / demand charges: the scratch-slot
-                      agents) also need their distinct rows and write the
-                      split record
-      k_hourly_batt   the distinct rows, the (month, period) bins + scalars per
-                      agent, the three f32 hourly planes when requested, and
-                      the f64 system-output plane of the scratch-slot agents
-      k_batt_finance  bins + scalars + 3 yearly arrays per agent; the
-                      scratch-slot agents read their system-output plane and
-                      their distinct load rows"""
+                      arrays of N+1 f64 per agent; the agents whose search
+                      bills hourly imports (net billing, demand charges) also
+                      read their distinct rows once.  Intermediate records
+                      (the search's net-billing split, the demand envelopes)
+                      are not counted: they are this implementation's, not
+                      the algorithm's
+      k_hourly_batt   the distinct rows, the agent's 12 x P (load, system)
+                      bin pairs (NEM agents) + scalars, the three f32 hourly
+                      planes when requested; the f64 system-output plane only
+                      for the agents that write it (`scratch_paths`), and the
+                      (month, period) sums / maxima of the compact records for
+                      the agents that hand one to the finance kernel instead
+                      (their variable hour entries are not counted: a lower
+                      bound)
+      k_batt_finance  bins + scalars + 3 yearly arrays per agent; the plane
+                      agents read their plane and their distinct load rows,
+                      the record agents their record's sums / maxima
+    `paths` = scratch_paths(...) after a run; without it every scratch-slot
+    agent is taken to write and read the plane (an upper bound)."""
     n = len(cols["load_kwh"])
     lr, cr = np.asarray(cols["load_row"]), np.asarray(cols["cf_row"])
     yearly = 8.0 * (np.asarray(cols["econ_life"], np.int64) + 1).sum()
     sl = np.asarray(cols["scratch_slot"]) >= 0
-    nh = int(sl.sum())
+    if paths is None:
+        plane, nbr, dcr, mo2 = sl, np.zeros(n, bool), np.zeros(n, bool), sl
+        P = np.full(n, MAXP, np.int64)
+    else:
+        plane, nbr, dcr, mo2, P = paths
+    distinct = lambda m, a: np.unique(a[m]).size if m.any() else 0
     rows = (np.unique(lr).size + np.unique(cr).size) * ROW_BYTES
-    rows_h = (np.unique(lr[sl]).size + np.unique(cr[sl]).size) * ROW_BYTES if nh else 0
+    # the search bills hourly imports for the scratch-slot agents (initial tariff)
+    rows_h = (distinct(sl, lr) + distinct(sl, cr)) * ROW_BYTES
     slots = (np.unique(lr).size + np.unique(cr).size) * 576 * 8
-    k_size = slots + n * 24 * 8 + 4 * yearly + rows_h + nh * NB_BYTES
-    k_hourly = rows + n * (2 * 144 * 8 + 16 * 8)
+    k_size = slots + n * 24 * 8 + 4 * yearly + rows_h
+    bins = float((12 * P * 16)[~mo2].sum())              # NEM agents' (load, system) pairs
+    recb = float((12 * P * 4 * 8)[nbr].sum() + 64 * nbr.sum() + DCR_HEAD * dcr.sum())
+    k_hourly = rows + n * 16 * 8 + bins + recb
     if hourly:
         k_hourly += n * 3 * PLANE_BYTES
     if battery:
-        k_hourly += nh * SYS_BYTES
-    k_fin = (n * (2 * 144 * 8 + 24 * 8) + 3 * yearly + nh * SYS_BYTES +
-             (np.unique(lr[sl]).size * ROW_BYTES if nh else 0)) if battery else 0.0
+        k_hourly += plane.sum() * SYS_BYTES
+    k_fin = (n * 24 * 8 + bins + 3 * yearly + recb + plane.sum() * SYS_BYTES +
+             distinct(plane, lr) * ROW_BYTES) if battery else 0.0
     return {"k_size": float(k_size), "k_hourly_batt": float(k_hourly), "k_batt_finance": float(k_fin)}
 
 
@@ -100,7 +145,9 @@ def parse():
     ap.add_argument("--config", default="res_1m_nem_tou")
     ap.add_argument("--no-hourly", action="store_true", help="on-device reduction mode")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="OpenMP threads of the CPU baseline (0 = every core this process may run on, "
+                         "capped by OMP_NUM_THREADS when the environment sets it: the GPU box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--chunks", type=int, default=None,
                     help="size() pipeline depth (default: the library's DGEN_DEFAULT_CHUNKS)")
@@ -138,7 +185,9 @@ def cpu_baseline(pop, seconds: float, threads: int, replan_hours: int = 24):
         avail = len(os.sched_getaffinity(0))
     except Exception:
         avail = os.cpu_count() or 1
-    threads = max(1, min(threads, avail))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    share = min(avail, omp) if omp > 0 else avail
+    threads = share if threads <= 0 else max(1, min(threads, avail))
     chunk = max(64, 32 * threads)
     n_take = min(pop.cols["load_kwh"].size, 200_000)
     sub = {k: v[:n_take] for k, v in pop.cols.items()}
@@ -153,6 +202,7 @@ def cpu_baseline(pop, seconds: float, threads: int, replan_hours: int = 24):
         if el >= seconds or done >= n_take:
             break
     return {"value": done / el, "unit": "agents/s", "cores": threads, "kind": "port",
+            "host_cpus": os.cpu_count(), "affinity_cpus": avail, "omp_num_threads_env": omp or None,
             "sample": f"{done} agents of the same synthetic workload ({pop.config}), "
                       f"oracle/orc.c full per-agent driver, OpenMP x{threads}, {el:.1f} s"}
 
@@ -237,7 +287,18 @@ def main():
     total_agents = args.agents * ws * args.steps
     value = total_agents / el
 
-    nbytes = algorithmic_bytes(pop.cols, not args.no_hourly, not args.no_batt)
+    # which scratch-slot agents moved the f64 system-output plane and which a
+    # compact record (the battery case's final tariff, the batch's switches)
+    dcols = pop.cols if batch.perm is None else {k: np.asarray(v)[batch.perm] for k, v in pop.cols.items()}
+    recs = eng.tariff_records
+    dc_batch = eng.tables.n_demand > 0 and (not pop.skip_demand_charges or eng.tables.peak_units != 0)
+    hp = max(1, min(int(recs["P"].max()), 12))
+    nb_lds = 8 * 4 * hp * 128 + (16 * (eng.tables.max_dc_periods or 8) * 128 if dc_batch else 0) + 2 * 12 * 1024   # dgen_size_agents' gate
+    paths = scratch_paths(dcols, recs, out["tariff_final"].cpu().numpy(), battery=not args.no_batt,
+                          skip_dc=pop.skip_demand_charges, nb_scan=batch.nb_scan and nb_lds <= 65536,
+                          dcr_on=dc_batch and args.replan_hours != 1,
+                          has_wholesale=bool(eng.tables.wholesale))
+    nbytes = algorithmic_bytes(dcols, not args.no_hourly, not args.no_batt, paths)
     traffic_pa, valu_busy, traffic_src = pmc_traffic(args.pmc_dir, args.config)
     # launches per step: k_hourly_batt sweeps the year in month-segment launches
     # per pipeline chunk; the year-lane kernels launch once per chunk

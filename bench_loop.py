@@ -2,12 +2,16 @@
 """Benchmark of the device model-year loop (BASELINE config C5: national
 synthetic population, 2026-2050 diffusion loop with RCCL state totals).
 
-Per model year, on every rank's resident shard of WHOLE states: per-year
-inputs, dgen_size_agents (Brent PV sizing + PV+battery run), max market share,
-Bass diffusion, largest-remainder battery attachment, per-state 8760-h export
-(in place from the sizing planes, or by re-sizing chunks with --hourly-chunk
-for shards whose planes do not fit), per-state totals, and one all-reduce of
-the [51 x 5] totals + [51 x 8760] hourly rows (RCCL over xGMI for N > 1).
+Per model year, on every rank's resident shard (state pieces of one national
+population, dgen_amd.partition: cut to equal predicted device cost, a state
+split across ranks where balance needs it): per-year inputs, dgen_size_agents
+(Brent PV sizing + PV+battery run), max market share, Bass diffusion,
+largest-remainder battery attachment (split states' groups gathered and
+allocated whole), per-state 8760-h export (in place from the sizing planes,
+or by re-running the scan in chunks with --hourly-chunk for shards whose
+planes do not fit), per-state totals, and one all-reduce of the per-state
+totals + 8760-h rows (RCCL over xGMI for N > 1).  The line reports every
+rank's measured time and sizing device time.
 
 Launch like bench.py (python bench_loop.py, or torch.distributed.run with one
 rank per GPU).  Weak scaling: --agents per GPU.  Prints ONE JSON line on rank 0:
@@ -59,43 +63,46 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+    from dgen_amd import partition as P
     from dgen_amd.engine import Engine
-    from dgen_amd.synth import STATE_HOUSEHOLDS_M, STATES, make_population
-    from dgen_amd.year_loop import LoopTables, YearLoop, loop_agents, population_work, rank_states
+    from dgen_amd.synth import STATES, make_population, national_tables, shard_population, split_state_members
+    from dgen_amd.year_loop import LoopTables, YearLoop, loop_agents
 
     t_setup = time.perf_counter()
     cnum = 1 if args.config == "de_res" else 5
     n_global = args.agents * ws
+    plan = None
     if args.config == "de_res":
-        pool, n_rank, mix = [STATES.index("DE")], args.agents, "uniform"
+        pop = make_population(args.config, args.agents, seed=20260000 + cnum + 7919 * rank,
+                              state_pool=[STATES.index("DE")])
+        ag = loop_agents(pop, agent_id0=rank * 2 * args.agents)
+        sg = None
+        n_rank = args.agents
     else:
-        # national population with census state sizes; whole states per rank,
-        # balanced by predicted work: every rank derives the same
-        # partition from the same census sample, then generates its own states'
-        # agents (its share of the global population by households)
-        sample = make_population(args.config, 50_000, seed=20260000 + cnum, n_res_shapes=256,
-                                 n_com_shapes=128, n_cf=256, n_counties=64, n_tariffs=32,
-                                 state_mix="census")
-        sw = np.bincount(sample.state_ix.astype(np.int64), weights=population_work(sample),
-                         minlength=len(STATES))
-        del sample
-        pool = rank_states(rank, ws, state_work=sw)
-        hh = STATE_HOUSEHOLDS_M
-        n_rank = int(round(n_global * hh[pool].sum() / hh.sum())) if ws > 1 else args.agents
-        mix = "census"
-        part = [rank_states(r, ws, state_work=sw) for r in range(ws)]
-        part_load = [float(sw[p_].sum()) for p_ in part]
-    pop = make_population(args.config, n_rank, seed=20260000 + cnum + 7919 * rank, state_pool=pool,
-                          state_mix=mix)
+        # national population by pieces (dgen_amd.partition): census state
+        # sizes, the states cut into equal measured device cost per rank (the
+        # per-path cost model over a per-state sample; a state is split across
+        # ranks where balance needs it), every rank drawing its own pieces
+        T = national_tables(args.config)
+        naep_row = T.cfs.astype(np.float64).sum(axis=1) / 1e6
+        sizes = P.census_sizes(n_global)
+        cost = np.zeros(len(STATES))
+        for s in range(len(STATES)):
+            smp = make_population(args.config, 2000, tables=T, agent_seed=20268000 + s, state_pool=[s])
+            cost[s] = P.cost_per_agent(smp.cols, naep_row[smp.cols["cf_row"]]).mean()
+        plan = P.plan_partition(sizes, cost, ws)
+        pop, ag = shard_population(T, plan, rank)
+        secs, ids = split_state_members(args.config, plan)
+        sg = P.split_groups(plan, rank, secs, ids)
+        n_rank = len(ag["agent_id"])
     eng = Engine(local if ws > 1 else 0)
     if args.no_batt:
         eng.set_battery(False)
     eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
     eng.set_tariffs(pop.tariffs)
     eng.set_switches(pop.switches)
-    loop = YearLoop(eng, pop, loop_agents(pop, agent_id0=rank * 2 * args.agents), LoopTables.synthetic(),
-                    first_year=args.first_year, hourly_export=not args.no_export,
-                    hourly_chunk=args.hourly_chunk)
+    loop = YearLoop(eng, pop, ag, LoopTables.synthetic(), first_year=args.first_year,
+                    hourly_export=not args.no_export, hourly_chunk=args.hourly_chunk, plan=plan, split=sg)
     del pop
     setup_s = time.perf_counter() - t_setup
     for k in range(args.warmup):
@@ -109,10 +116,15 @@ def main():
     t0 = time.perf_counter()
     res = [loop.run_year(y) for y in years]
     torch.cuda.synchronize()
+    own = time.perf_counter() - t0                  # this rank's own time, before the barrier
     if ws > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    ms_size, ms_hourly, ms_fin, cnt = eng.kernel_times()
+    # sizing device time per year of this rank (HIP events of the sizing kernels)
+    dev_ms = (ms_size + ms_hourly + ms_fin) * (cnt / max(len(years), 1) if cnt else 0.0)
     n_total = n_rank
+    per_rank = [[own, dev_ms, float(n_rank)]]
     if ws > 1:
         dev = eng.dev if backend == "nccl" else "cpu"
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -121,7 +133,10 @@ def main():
         c = torch.tensor([float(n_rank)], dtype=torch.float64, device=dev)
         dist.all_reduce(c)
         n_total = int(c.item())
-    ms_size, ms_hourly, ms_fin, cnt = eng.kernel_times()
+        g = torch.zeros((ws, 3), dtype=torch.float64, device=dev)
+        g[rank] = torch.tensor(per_rank[0], dtype=torch.float64, device=dev)
+        dist.all_reduce(g)
+        per_rank = g.cpu().tolist()
     last = res[-1].totals.cpu().numpy()
     if rank == 0:
         line = {
@@ -136,13 +151,18 @@ def main():
                        "population": args.config, "year_step": args.step, "battery_run": not args.no_batt,
                        "agents_per_gpu": args.agents,
                        "global_agents": n_total, "years": [years[0], years[-1]],
-                       "state_mix": mix,
-                       "rank_partition": (None if args.config == "de_res" else
-                                          {"states_per_rank": [len(p_) for p_ in part],
-                                           "predicted_work_max_over_mean":
-                                               max(part_load) / (sum(part_load) / len(part_load))}),
+                       "state_mix": "census" if plan is not None else "DE",
+                       "rank_partition": (None if plan is None else
+                                          {"pieces_per_rank": [len(p_) for p_ in plan.pieces],
+                                           "split_states": [STATES[s_] for s_ in plan.split_states()],
+                                           "predicted_cost_max_over_mean": plan.imbalance()}),
+                       "per_rank": {"seconds": [r_[0] for r_ in per_rank],
+                                    "sizing_device_ms_per_year": [r_[1] for r_ in per_rank],
+                                    "agents": [int(r_[2]) for r_ in per_rank],
+                                    "measured_max_over_mean": (max(r_[0] for r_ in per_rank) /
+                                                               (sum(r_[0] for r_ in per_rank) / len(per_rank)))},
                        "state_export": not args.no_export, "hourly_chunk": args.hourly_chunk,
-                       "parallelism": f"dp{ws} (whole states per rank; one all-reduce per year)"},
+                       "parallelism": f"dp{ws} (state pieces per rank; split groups gathered, one all-reduce of state rows per year)"},
             "sizing_kernel_ms_per_call": {"k_size": ms_size, "k_hourly_batt": ms_hourly,
                                           "k_batt_finance": ms_fin, "launch_samples": cnt},
             "final_year": {"adopters": float(last[:, 3].sum()), "system_mw": float(last[:, 0].sum() / 1e3),

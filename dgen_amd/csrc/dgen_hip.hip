@@ -810,20 +810,6 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
     }
 }
 
-// The battery case's bills and cash flow for a NEM agent, in the scan's tail
-// (defined after the year-lane engine; see hb_finance_nem).  Off by default:
-// A/B on C3 1M (DGEN_FIN_FOLD=1) k_hourly_batt 24.9 -> 31.3 ms against the
-// 3.9 ms k_batt_finance it replaces -- the year-lane kernel is VALU-bound,
-// not launch-bound, and one thread's 25 sequential years cost as much VALU
-// per agent as the lanes' (every wave runs the union of its agents' periods
-// and tiers) while lengthening the last month segment.
-__device__ __forceinline__ void hb_finance_nem(const dgen_tariff& t, const dgen_agents& A, const dgen_outputs& O,
-                                               const dgen_cfg& cfg, int64_t i, const double2* lg, double kw,
-                                               double bank, double otc, bool same_tariff);
-#ifndef DGEN_FIN_FOLD
-#define DGEN_FIN_FOLD 0
-#endif
-
 // F64: the hourly planes as doubles (the reference's fp64 lists) instead of
 // floats: the same values the scan computes, 32 B per lane per hour quad.
 // NB: the batch has net-billing scratch slots; the scan then also builds the
@@ -845,21 +831,6 @@ __device__ __forceinline__ void hb_finance_nem(const dgen_tariff& t, const dgen_
 // lane), so the network appears once per hour of the day (~27k instructions),
 // and the form runs one wave per SIMD: the window, its sorted copy and both
 // days' raw values need ~400 registers.
-// XCD-aware block order (DGEN_XCD_REMAP): the hardware deals consecutive
-// blocks round-robin to the 8 XCDs, each with its own L2; consecutive agents
-// (load-major device order) share profile rows, so logical block k goes to the
-// hardware slot that keeps runs of consecutive blocks on one XCD.  A bijection
-// on [0, nb).
-#ifndef DGEN_XCD_REMAP
-#define DGEN_XCD_REMAP 0
-#endif
-__device__ __forceinline__ unsigned xcd_block(unsigned b, unsigned nb) {
-    if (!DGEN_XCD_REMAP) return b;
-    constexpr unsigned X = 8;
-    const unsigned q = nb / X, r = nb % X, x = b % X, k = b / X;
-    return x < r ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
-}
-
 // DCR: the batch bills demand charges (or kWh/kW tier peaks) and has room for
 // the battery-case demand records (dcr: DCR_BYTES per scratch slot, dc_nq the
 // batch's demand periods, which size the scan's per-period LDS maxima).
@@ -867,13 +838,13 @@ template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR>
 __global__ void __launch_bounds__(BLOCK, ROLL ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
-              int repair, char* dcr, int dc_nq, int dcr_cap, int fin) {
+              int repair, char* dcr, int dc_nq, int dcr_cap) {
     // agents [i0, i1) of a batch of n (row stride of every plane stays n),
     // months [m_lo, m_hi) of the year: the year is swept in month segments,
     // one launch each, so that every resident wave works on the same weeks
     // and the profile-row slices they read stay in L2 / MALL (SOC and the
     // running annual PV sum carry between launches in W.carry)
-    int64_t i = i0 + (int64_t)xcd_block(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    int64_t i = i0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= i1) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
     // repair pass: only the agents whose scan-built split (repair bit 1) or
@@ -1200,7 +1171,10 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 if constexpr (DCR) {
                     if (put_dcr) {
                         int q = (int)((dsch[hh >> 3] >> (8 * (hh & 7))) & 0xffu);
-                        q = q < DCP ? q : 0;
+                        // dc_nq (dgen_tables.max_dc_periods) sizes the per-period
+                        // LDS maxima: a schedule beyond it is a malformed table
+                        // (flagged, never written past the region)
+                        if (q >= dc_nq) { status |= DGEN_ST_DEMAND; q = 0; }
                         if (q != dq) {
                             dcb[dq * BLOCK] = dacc;
                             dq = q;
@@ -1316,6 +1290,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     if (m_hi < 12) {
         W.carry[i] = soc;
         W.carry[n + i] = annual;
+        if (DCR && (status & DGEN_ST_DEMAND)) O.status[i] = status;   // the next segment reloads it
         return;
     }
     // 1: the record holds every kept hour; 2: it overflowed and the plane was
@@ -1344,16 +1319,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // bill (same load, same tariff -> the same bill, as in the oracle)
     if (!repair) {   // the repair pass starts from the already switched tariff
         const bool same = tariff == O.tariff_final[i];
-        // DGEN_FIN_FOLD: the battery-case finance of a NEM agent (bins, no
-        // demand record, first-tier prices in registers) runs here and
-        // k_batt_finance skips it (aux 2)
-        const int N = A.econ_life[i];
-        const bool fold = DGEN_FIN_FOLD && fin && batt_on && !unsized && !mo2 && !has_dc && t.mo == 0 &&
-                          t.P <= PREG && !peak_unit(t) && N >= 1 && N <= MAXY &&
-                          !(status & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH |
-                                      DGEN_ST_UNIT));
-        if (fold) hb_finance_nem(t, A, O, cfg, i, W.LGb + (int64_t)i * NBIN, kw_star, bank, otc, same);
-        W.aux[i] = fold ? 2.0 : (same ? 0.0 : 1.0);
+        W.aux[i] = same ? 0.0 : 1.0;
         O.tariff_final[i] = tariff;
         O.switched[i] = switched;
     }
@@ -2268,7 +2234,6 @@ struct DcEnv {
     double2* lines;   // [12][DCP][DC_NL] (L, g)
     double* maxl;     // [12][DCP] max load (the no-system peak)
     int* cnt;         // [12][DCP] lines kept (0 = period absent from the month)
-    int* tag;         // 1 + the tariff k_dc_env built them for (0: none / overflow)
 };
 constexpr size_t DCW_BYTES = (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double) + sizeof(int)) + 16;
 
@@ -2278,7 +2243,6 @@ __device__ __forceinline__ DcEnv dc_env_at(void* base, int64_t i) {
     e.lines = reinterpret_cast<double2*>(b);
     e.maxl = reinterpret_cast<double*>(b + (size_t)12 * DCP * DC_NL * sizeof(double2));
     e.cnt = reinterpret_cast<int*>(b + (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double)));
-    e.tag = reinterpret_cast<int*>(b + (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double) + sizeof(int)));
     return e;
 }
 
@@ -2588,13 +2552,10 @@ __device__ __forceinline__ bool yl_dc_build_coop(const dgen_demand* D, const YSr
 }
 
 // k_size's build: the hour-lane form when the segment has its stage
-#ifndef DGEN_DC_SERIAL
-#define DGEN_DC_SERIAL 0
-#endif
 template <int LPA>
 __device__ __forceinline__ bool yl_dc_build_any(const dgen_demand* D, const YSrc& src, double tlo, double thi,
                                                 const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
-    if (!DGEN_DC_SERIAL && st) return yl_dc_build_coop(D, src, tlo, thi, E, st, g);
+    if (st) return yl_dc_build_coop(D, src, tlo, thi, E, st, g);
     return yl_dc_build(D, src, tlo, thi, E, g);
 }
 
@@ -2684,80 +2645,6 @@ __device__ __forceinline__ double nb_weight(const YSrc& src, int h) { return (do
 // first -- a fixed order, a re-association of the serial hour sums.  The
 // mixed hours are appended in hour order (ballot rank within the day).
 // Returns true when every month's M hours fit (segment-uniform).
-#ifndef DGEN_NB_SERIAL
-#define DGEN_NB_SERIAL 0
-#endif
-// Month lane m < 12 of the segment builds month m (accumulators in its LDS
-// column, at(4 p + q), 4 P <= 4 half).  Returns true when every month's M
-// hours fit (segment-uniform).
-template <int LPA>
-__device__ bool yl_nb_build_serial(const dgen_tariff& t, const YSrc& src, double tlo, double thi, char* nbp,
-                            const YLds& S, const Seg<LPA>& g) {
-    bool ok = true;
-    const int m = g.sl;
-    const NbRec R = nb_rec(nbp);
-    if (m < 12) {
-        const int P = t.P;
-        for (int k = 0; k < 4 * P; k++) S.at(k) = 0.0;
-        int n_m = 0;
-        NbEnt* ent = R.ent + m * NB_CAPM;
-        for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
-            const uint8_t* sc = ((d % 7) >= 5) ? t.wkend[m] : t.wkday[m];
-#pragma unroll 1
-            for (int c0 = 0; c0 < 24; c0 += 4) {
-                const int h = d * 24 + c0;
-                const uint32_t pq = *reinterpret_cast<const uint32_t*>(sc + c0);
-                const float4 sv = *reinterpret_cast<const float4*>(src.shape + h);
-                const float shv[4] = {sv.x, sv.y, sv.z, sv.w};
-                // per-kW PV output (search) or the battery case's system output
-                double gq[4];
-                if (src.sysgen) {
-                    sys_quad(src, h, gq);
-                } else {
-                    const int4 cv = *reinterpret_cast<const int4*>(src.cf + h);
-                    gq[0] = cf_per_kw(cv.x); gq[1] = cf_per_kw(cv.y);
-                    gq[2] = cf_per_kw(cv.z); gq[3] = cf_per_kw(cv.w);
-                }
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const int p = (int)((pq >> (8 * k)) & 0xffu);
-                    const double L = (double)shv[k] * src.load_scale;
-                    const double gk = gq[k];
-                    const double vlo = L - gk * tlo, vhi = L - gk * thi;
-                    const double slack = 1e-10 * (fabs(L) + fabs(gk) * thi);
-                    if (fmin(vlo, vhi) > slack) {               // imports at every t
-                        S.at(4 * p) += L;
-                        S.at(4 * p + 1) += gk;
-                    } else if (fmax(vlo, vhi) < -slack) {       // exports at every t
-                        const double w = nb_weight(src, h + k);
-                        S.at(4 * p + 2) += gk * w;
-                        S.at(4 * p + 3) += L * w;
-                    } else {
-                        if (n_m < NB_CAPM) {
-                            NbEnt e;
-                            e.L = L;
-                            e.g = gk;
-                            e.w = nb_weight_f(src, h + k);
-                            e.p = p;
-                            ent[n_m] = e;
-                        }
-                        n_m++;
-                    }
-                }
-            }
-        }
-        ok = n_m <= NB_CAPM;
-        R.cnt[m] = n_m;
-        for (int p = 0; p < P; p++)
-            for (int q = 0; q < 4; q++) R.sums[(m * MAXP + p) * 4 + q] = S.at(4 * p + q);
-    }
-    // hand-off to the other lanes through global memory, as yl_dc_build
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    return g.first(!ok) < 0;
-}
-
 // days per load batch: the battery case's f64 system output takes twice the
 // registers of the cf row, and k_batt_finance stays at 3 waves with 4; the
 // search's cf build measured 2 / 3 / 4 / 6 / 8 / 12 days: 21.2 / 20.3 / 20.0 /
@@ -3227,151 +3114,6 @@ __device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev
     return f;
 }
 
-// k_batt_finance_w's NEM branch for one agent in one thread (the tail of
-// k_hourly_batt): the same per-year arithmetic -- yl_bill_mo0_reg's month
-// recursion on the agent's (load, system) bins, the year's escalation and
-// degradation factors by sequential products (pow_seq), yl_make_loan and
-// yl_cashflow's per-year terms -- with the NPV summed in year order instead of
-// the lanes' butterfly (npv_pv_batt within rounding of the year-lane form;
-// every per-year output bit-identical).
-constexpr int TH_MB = 3;    // months of bins loaded together in the tail's bill
-__device__ __forceinline__ double th_bill_mo0(const dgen_tariff& t, const double2* lg, double gscale,
-                                              double yearend) {
-    const int P = t.P, T = t.T;
-    const double fixed = t.fixed;
-    double b0[PREG], credit[PREG], u[PREG];
-#pragma unroll
-    for (int p = 0; p < PREG; p++) { b0[p] = p < P ? t.buy[p][0] : 0.0; credit[p] = 0.0; u[p] = 0.0; }
-    double total = 0.0;
-#pragma unroll 1
-    for (int m0 = 0; m0 < 12; m0 += TH_MB) {
-        // TH_MB months of (load, system) bins in flight together (L2-resident:
-        // the scan wrote them), static register indices
-        double2 bv[TH_MB][PREG];
-#pragma unroll
-        for (int k = 0; k < TH_MB; k++)
-#pragma unroll
-            for (int p = 0; p < PREG; p++)
-                bv[k][p] = p < P ? lg[(m0 + k) * P + p] : make_double2(0.0, 0.0);
-#pragma unroll
-        for (int k = 0; k < TH_MB; k++) {
-            const int m = m0 + k;
-#pragma unroll
-            for (int p = 0; p < PREG; p++) {
-                if (p < P) {
-                    double nn = bv[k][p].x - gscale * bv[k][p].y;
-                    double use = nn < credit[p] ? nn : credit[p];
-                    double un = nn - use;
-                    double cn = credit[p] - use;
-                    const bool pos = nn >= 0.0;
-                    u[p] = pos ? un : 0.0;
-                    credit[p] = pos ? cn : credit[p] + -nn;
-                }
-            }
-            double U = 0.0;
-#pragma unroll
-            for (int p = 0; p < PREG; p++)
-                if (p < P) U += u[p];
-            double charge = 0.0;
-            if (U > 0.0) {
-                if (T == 1) {
-#pragma unroll
-                    for (int p = 0; p < PREG; p++)
-                        if (p < P) charge += u[p] * b0[p];
-                } else {
-                    double fr[PREG];
-#pragma unroll
-                    for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
-                    const double scale = tier_scale(t, m, nullptr);
-                    double prev = 0.0;
-                    for (int kk = 0; kk < T; kk++) {
-                        double hi = (kk == T - 1) ? INFINITY : t.cap[kk] * scale;
-                        double top = U < hi ? U : hi;
-                        double amt = top - prev;
-                        if (amt < 0.0) amt = 0.0;
-                        if (hi > prev) prev = hi;
-#pragma unroll
-                        for (int p = 0; p < PREG; p++)
-                            if (p < P) charge += fr[p] * amt * (kk == 0 ? b0[p] : t.buy[p][kk]);
-                    }
-                }
-            }
-            double bill = fixed + charge;
-            if (m == 11) {
-                double cc = 0.0;
-#pragma unroll
-                for (int p = 0; p < PREG; p++)
-                    if (p < P) cc += credit[p];
-                bill -= cc * yearend;
-            }
-            total += bill;
-        }
-    }
-    return total;
-}
-
-__device__ __forceinline__ void hb_finance_nem(const dgen_tariff& t, const dgen_agents& A, const dgen_outputs& O,
-                                               const dgen_cfg& cfg, int64_t i, const double2* lg, double kw,
-                                               double bank, double otc, bool same_tariff) {
-
-    const bool is_res = (A.flags[i] & 1) != 0;
-    const int N = A.econ_life[i];
-    const double rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
-    const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
-    const double system_costs = (kw > 0.0) ? A.capex_combined[i] * kw : A.capex[i] * kw;   // ff:203-216
-    const double batt_costs = A.batt_capex_kwh[i] * bank * 0.7;                           // ff:219
-    const double C = ((system_costs + batt_costs) * A.ccm[i]) + 0.0 + otc;
-    const double vor = A.vor[i];
-    const double yearend = cfg.nm_yearend_sell_rate;
-    const double wo1 = same_tariff ? O.first_without[i] : th_bill_mo0(t, lg, 0.0, yearend);
-    // yl_cashflow's agent-level terms
-    const YLoan L1 = yl_make_loan(A, cfg, i, N, is_res, 1);
-    const double debt = L1.debt_frac * C;
-    double pmt = 0.0;
-    if (L1.term > 0 && debt != 0.0) {
-        if (L1.r_loan != 0.0) pmt = debt * L1.r_loan / (1.0 - 1.0 / L1.loan_f);
-        else pmt = debt / (double)L1.term;
-    }
-    double itc = L1.itc_pct * 0.01 * C;
-    if (itc > L1.itc_max) itc = L1.itc_max;
-    const double basis = C - 0.5 * itc;
-    const int64_t row = i * (MAXY + 1);
-    O.cfev_batt[row] = 0.0;
-    O.bill_w_batt[row] = 0.0;
-    O.bill_wo_batt[row] = 0.0;
-    double r_y = 1.0, s_y = 1.0, npv_sum = 0.0;
-    for (int y = 1; y <= N; y++) {
-        if (y > 1) { r_y = r_y * rate_base; s_y = s_y * sys_base; }        // pow_seq(·, y - 1)
-        const YLoan L = yl_make_loan(A, cfg, i, N, is_res, y);
-        const double wb = th_bill_mo0(t, lg, s_y, yearend);
-        const double w = wb * r_y;
-        const double wo = wo1 * r_y;
-        const double ev = (wo - w) + vor;                                  // ff:275
-        const double oe = (L.ins_rate * C) * L.ins_esc;
-        const bool paying = y <= L.term && pmt != 0.0;
-        const double payment = paying ? pmt : 0.0;
-        const double itc_y = (y == 1) ? itc : 0.0;
-        double sta_tax = 0.0, fed_tax = 0.0;
-        if (L.market != 0) {
-            double bal = debt;
-            const int kend = min(min(y, L.term + 1), L.N + 1);
-            if (pmt != 0.0)
-                for (int k = 1; k < kend; k++) bal = bal - (pmt - bal * L.r_loan);
-            const double interest = paying ? bal * L.r_loan : 0.0;
-            const double dep = depr_frac(L.depr_type, y, L.sl_years) * basis;
-            sta_tax = L.sta * (ev - oe - interest - dep);
-            fed_tax = L.fed * (ev - oe - interest - dep - sta_tax);
-        }
-        const double taxsav = itc_y - sta_tax - fed_tax;
-        const double atcf = ev - oe - payment + taxsav;
-        npv_sum += atcf * L.df;
-        O.cfev_batt[row + y] = ev;
-        O.bill_w_batt[row + y] = w;
-        O.bill_wo_batt[row + y] = wo;
-    }
-    O.npv_pv_batt[i] = -(C - debt) + npv_sum;
-}
-
 struct YLast {   // per-lane results of the most recent evaluation
     double total, ev, w, wo;
     YFlow flow;
@@ -3419,26 +3161,16 @@ struct YCtx {
 };
 
 // The current tariff's demand envelopes, built here at the first evaluation
-// billed with the tariff (the segment's hour lanes, yl_dc_build_any).  With
-// DGEN_DC_PREBUILD, k_dc_env builds the first-evaluation tariff's ahead of
-// k_size (tag = 1 + tariff) and only other tariffs take the hourly pass
-// (yl_demand, exact).  A/B (C4 200k): k_size 35.7 ms in-kernel vs 41.4 ms
-// with the prebuild kernel (k_dc_env ran ~16 ms, and the evaluations read the
-// envelopes back from HBM instead of a build's warm L2 lines).
-#ifndef DGEN_DC_PREBUILD
-#define DGEN_DC_PREBUILD 0
-#endif
-#define DGEN_DC_INKERNEL (!DGEN_DC_PREBUILD)
+// billed with the tariff (the segment's hour lanes, yl_dc_build_any).  A
+// separate prebuild kernel ahead of k_size measured slower (C4 200k: k_size
+// 35.7 -> 41.4 ms) and was removed.
 template <int LPA>
 __device__ __forceinline__ bool yl_dc_ready(YCtx<LPA>& c, const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
     if (!E.lines) return false;
     if (c.env_tag == c.tariff + 1) return true;
-    if (DGEN_DC_INKERNEL) {
-        const bool ok = yl_dc_build_any(c.dem, c.src, c.tlo, c.thi, E, st, g);
-        c.env_tag = ok ? c.tariff + 1 : 0;
-        return ok;
-    }
-    return false;
+    const bool ok = yl_dc_build_any(c.dem, c.src, c.tlo, c.thi, E, st, g);
+    c.env_tag = ok ? c.tariff + 1 : 0;
+    return ok;
 }
 
 // NET: the batch may bill net (it has scratch slots, dgen_size_agents); the
@@ -3541,8 +3273,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
             // any other is built here
             PH_T0(tb);
             if (c.nb && c.nb_tag != c.tariff + 1) {
-                const bool ok = DGEN_NB_SERIAL ? yl_nb_build_serial(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g)
-                                               : yl_nb_build<false>(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g);
+                const bool ok = yl_nb_build<false>(t, c.src, c.tlo, c.thi, c.nb, c.S, c.g);
                 c.nb_tag = ok ? c.tariff + 1 : 0;
                 PH_CNT(7, 1, c.g.sl == 0);
             }
@@ -3642,10 +3373,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.env_tag = 0;
     c.dc_nq = (T.max_dc_periods > 0 && T.max_dc_periods <= DCP) ? T.max_dc_periods : DCP;
     if constexpr (DC) {
-        if (dcws) {
-            c.env = dc_env_at(dcws, i);
-            c.env_tag = DGEN_DC_PREBUILD ? *c.env.tag : 0;   // k_dc_env's, this step
-        }
+        if (dcws) c.env = dc_env_at(dcws, i);
         // the segment's envelope stage sits after the year-lane layout
         c.stg = reinterpret_cast<DcStage*>(reinterpret_cast<char*>(dyn_lds) +
                                            ylds_bytes(half, LPA, PK && T.peak_units != 0)) + lane / LPA;
@@ -3796,60 +3524,6 @@ __device__ __forceinline__ int first_eval_tariff(const dgen_tables& T, const dge
     return t;
 }
 
-// Demand envelopes of every agent's first-evaluation tariff (first_eval_tariff), built ahead of k_size on
-// the same stream (the PV-only search's demand pass, DC batches): two agents
-// per wave, the hour-lane build (yl_dc_build_coop) over the same bracket and
-// degradation range k_size evaluates.  In k_size the build was half the C4
-// search's cycles and its code held the two-agent DC kernel at 256 VGPRs with
-// spills; here it runs alone at a few waves per SIMD.  tag = 1 + the tariff
-// (0: no envelope -- no demand record, invalid agent, or a group over DC_NL
-// lines: k_size then takes the hourly pass).
-template <int LPA>
-__global__ void __launch_bounds__(WAVE)
-k_dc_env(dgen_tables T, dgen_agents A, dgen_cfg cfg, int64_t i0, int64_t i1, void* dcws) {
-    const int lane = threadIdx.x;
-    const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
-    if (i >= i1) return;
-    const Seg<LPA> g(lane);
-    const DcEnv E = dc_env_at(dcws, i);
-    const int lr = A.load_row[i], cr = A.cf_row[i];
-    const double kwh = A.load_kwh[i];
-    const double max_load = kwh / T.cf_naep[cr];                    // ff:440-444, as k_size
-    const double low = max_load * 0.8, high = max_load * 1.25;
-    const bool fin = isfinite(low) && isfinite(high);
-    const int t0 = fin ? first_eval_tariff(T, A, i, low, high) : -1;
-    int tag = 0;
-    if (t0 >= 0 && t0 < T.n_tariffs) {
-        const dgen_tariff& t = T.tariffs[t0];
-        // k_size's record for the tariff: the kWh/kW tier peaks' where the batch
-        // bills those (PK kernels), else the demand charges'
-        const dgen_demand* dem = (T.peak_units && peak_unit(t)) ? tariff_peaks(T.demand, T.n_demand, t)
-                                                                : tariff_demand(T, cfg, t);
-        const int N = A.econ_life[i];
-        if (dem && N >= 1 && N <= MAXY) {
-            const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
-            const double sN = pow_seq(sys_base, N - 1);            // k_size's s_y of year N
-            const double s_lo = sN < 1.0 ? sN : 1.0, s_hi = sN > 1.0 ? sN : 1.0;
-            const double tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
-            const double thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
-            YSrc src;
-            src.shape = T.shapes + (int64_t)lr * NH;
-            src.cf = T.cfs + (int64_t)cr * NH;
-            src.sysgen = nullptr;
-            src.sys_stride = 0;
-            src.load_scale = kwh / T.shape_sum[lr];
-            src.gen_scale = 0.0;
-            src.ts = nullptr;
-            src.ts_mult = 0.0;
-            DcStage* const st = reinterpret_cast<DcStage*>(dyn_lds) + lane / LPA;
-            if (yl_dc_build_coop(dem, src, tlo, thi, E, st, g)) tag = t0 + 1;
-        }
-    }
-    PH_CNT(2, 1, g.sl == 0);                      // phase builds: agents / envelopes kept
-    PH_CNT(6, tag != 0, g.sl == 0);
-    if (g.sl == 0) *E.tag = tag;
-}
-
 // The PV-only search's net-billing split of every agent's first-evaluation
 // tariff (first_eval_tariff), built ahead of k_size on the same stream (yl_nb_build<false> over the same
 // range [tlo, thi]; k_size builds only for a tariff the rate switch moves to).
@@ -3913,7 +3587,6 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     if (i >= i1) return;
     const int st = O.status[i];
     if (st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS | DGEN_ST_SCRATCH | DGEN_ST_UNIT)) return;
-    if (ws_layout(ws, n).aux[i] == 2.0) return;   // its finance ran in k_hourly_batt's tail
     PH_T0(t_all);
     const Seg<LPA> g(lane);
     const int y = g.sl + 1;
@@ -4013,8 +3686,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
                 const NbRec R = nb_rec(nbp);
                 nb_ok = g.first(g.sl < 12 && R.cnt[g.sl] > NB_CAPM) < 0;
             } else {
-                nb_ok = DGEN_NB_SERIAL ? yl_nb_build_serial(t, src, s_lo, s_hi, nbp, S, g)
-                                       : yl_nb_build<true>(t, src, s_lo, s_hi, nbp, S, g);
+                nb_ok = yl_nb_build<true>(t, src, s_lo, s_hi, nbp, S, g);
             }
             PH_ADD(5, tb, g.sl == 0);
             PH_T0(te);
@@ -4112,6 +3784,21 @@ k_segment_sums(const V* __restrict__ v1, const double* __restrict__ w1, const V*
     if (threadIdx.x == 0) out[s * k + j] = red[0];
 }
 
+
+// Rows of each segment summed in row order: out[s][j] = ((in[r0][j] + in[r0+1][j])
+// + ...) for the rows r of [seg_off[s], seg_off[s+1]).  The model-year loop's
+// per-state rows are sums of per-chunk partials (fixed 8192-agent chunks of
+// each state's members, dgen_amd/partition.py) taken in chunk order, so a
+// state whose chunks sit on several ranks sums to the same bits as on one.
+__global__ void k_rows_seq_sum(const double* __restrict__ in, int64_t k, const int64_t* __restrict__ seg_off,
+                               int64_t n_seg, double* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t s = blockIdx.y;
+    if (j >= k || s >= n_seg) return;
+    double acc = 0.0;
+    for (int64_t r = seg_off[s]; r < seg_off[s + 1]; r++) acc += in[r * k + j];
+    out[s * k + j] = acc;
+}
 
 // ---------------------------------------------------------------------------
 // Diffusion step, thread per agent
@@ -4868,9 +4555,6 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         if (n_scratch > 0)
             hipLaunchKernelGGL((k_nb_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE), 4 * WAVE * sizeof(double), s,
                                *T, *A, i0, i1, nbws);
-        if (DGEN_DC_PREBUILD && dc && c->dc_buf)
-            hipLaunchKernelGGL((k_dc_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE), 2 * DCS_BYTES, s, *T, *A,
-                               c->cfg, i0, i1, c->dc_buf);
         // agents per year-lane block: WAVE / lpa
         const dim3 ygrid_s((unsigned)((m + WAVE / lpa_s - 1) / (WAVE / lpa_s)));
         const dim3 ygrid_f((unsigned)((m + WAVE / lpa_f - 1) / (WAVE / lpa_f)));
@@ -4920,17 +4604,17 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     do {                                                                                          \
         if (nb_scan && !(REP) && dcr_on && !(R))                                                  \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, true>), grid, block, lds, s2, *T, *A, *O, \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, dcr, dc_nq, c->dcr_enable, m1 == 12); \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, dcr, dc_nq, c->dcr_enable); \
         else if (nb_scan && !(REP))                                                               \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true, R, false>), grid, block, lds, s2, *T, *A, *O, c->cfg, \
-                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0, m1 == 12); \
+                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0); \
         else if (!(REP) && dcr_on && !(R))                                                        \
             hipLaunchKernelGGL((k_hourly_batt<H, F, false, false, true>), grid, block, lds, s2, *T, *A, *O, \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, 0, dcr, dc_nq, c->dcr_enable, m1 == 12); \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, 0, dcr, dc_nq, c->dcr_enable); \
         else                                                                                      \
             hipLaunchKernelGGL((k_hourly_batt<H, F, false, R, false>), grid, block, lds, s2, *T, *A, *O, \
                                c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? rep_mask : 0, \
-                               (REP) ? dcr : nullptr, 0, 0, (REP) ? 0 : (m1 == 12));                                      \
+                               (REP) ? dcr : nullptr, 0, 0);                                                               \
     } while (0)
 #define DGEN_HB_LAUNCH(H, F, REP)                                                                 \
     do {                                                                                          \
@@ -5031,7 +4715,7 @@ int32_t dgen_hourly_planes(dgen_ctx* c, const dgen_tables* T, const dgen_agents*
         const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
 #define DGEN_HP_LAUNCH(F, R)                                                                       \
         hipLaunchKernelGGL((k_hourly_batt<true, F, false, R, false>), grid, block, lds, s, *T, *A, *O, c->cfg, \
-                           n, ws, n_scratch, (int64_t)0, n, m0, m1, c->battery, 0, 0, nullptr, 0, 0, 0)
+                           n, ws, n_scratch, (int64_t)0, n, m0, m1, c->battery, 0, 0, nullptr, 0, 0)
         if (O->hourly_f64) { if (roll) DGEN_HP_LAUNCH(true, true); else DGEN_HP_LAUNCH(true, false); }
         else { if (roll) DGEN_HP_LAUNCH(false, true); else DGEN_HP_LAUNCH(false, false); }
 #undef DGEN_HP_LAUNCH
@@ -5055,6 +4739,12 @@ int32_t dgen_set_dc_records(dgen_ctx* c, int32_t cap) {
         return DGEN_E_ARG;
     }
     c->dcr_enable = cap;
+    if (cap == 0 && c->dcr_buf) {   // records off: release their HBM (n_scratch x DCR_BYTES)
+        HIP_TRY(hipStreamSynchronize(c->s2));
+        HIP_TRY(hipFree(c->dcr_buf));
+        c->dcr_buf = nullptr;
+        c->dcr_cap = 0;
+    }
     return DGEN_OK;
 }
 
@@ -5121,6 +4811,20 @@ int32_t dgen_segment_sums(dgen_ctx* c, const void* v1, const double* w1, const v
     else
         hipLaunchKernelGGL(k_segment_sums<double>, grid, block, 0, (hipStream_t)stream,
                            (const double*)v1, w1, (const double*)v2, w2, k, n, seg_off, n_seg, out);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_rows_seq_sum(dgen_ctx* c, const double* in, int64_t k, const int64_t* seg_off, int64_t n_seg,
+                          double* out, void* stream) {
+    if (!c || !in || !seg_off || !out || k <= 0 || n_seg < 0 || n_seg > 65535) {
+        set_err("dgen_rows_seq_sum: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n_seg == 0) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    dim3 grid((unsigned)((k + 255) / 256), (unsigned)n_seg), block(256);
+    hipLaunchKernelGGL(k_rows_seq_sum, grid, block, 0, (hipStream_t)stream, in, k, seg_off, n_seg, out);
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
 }

@@ -41,8 +41,20 @@ class AgentBatch:
     nb_scan: bool = True
 
 
+def path_class(cols: Dict[str, np.ndarray]) -> np.ndarray:
+    """The battery case's billing path per agent, from its columns: 0 = bins
+    only (NEM, no scratch slot), 1 = hourly imports billed from the split the
+    scan builds (a scratch slot, no TS sell rate: CA or no wholesale row), 2 =
+    the other scratch-slot agents (TS sell rate, demand charges).  k_hourly_batt
+    runs one agent per lane, and the paths' per-hour work differs (bins vs
+    classification vs plane stores): grouped, a wave runs one of them."""
+    sl = np.asarray(cols["scratch_slot"]) >= 0
+    ts = (np.asarray(cols["wholesale_row"]) >= 0) & ((np.asarray(cols["flags"]) & 2) == 0)
+    return np.where(~sl, 0, np.where(ts, 2, 1)).astype(np.int8)
+
+
 def profile_order(cols: Dict[str, np.ndarray], major: str = "load",
-                  group: Optional[np.ndarray] = None) -> np.ndarray:
+                  group: Optional[np.ndarray] = None, by_path: bool = True) -> np.ndarray:
     """Device order for a batch: agents grouped by (load_row, cf_row)
     (major="cf": by (cf_row, load_row)).
 
@@ -54,12 +66,17 @@ def profile_order(cols: Dict[str, np.ndarray], major: str = "load",
     38.0 ms cf-major, 45.3 ms caller order).  The
     reference's agent order carries no meaning (size_chunk returns rows keyed
     by agent_id, ff:1149-1218), so the host columnarizer is free to choose it.
-    group (optional) is an outer key: the model-year loop passes the state so
-    each state's members are one contiguous column range of the hourly planes
-    and k_state_hourly streams them coalesced.  Stable, so ties keep caller
+    by_path: the battery case's billing path (path_class) is the next key
+    out, so a wave's lanes run one path of the scan (and the scan-built
+    net-billing split is decided per agent, not per batch).  group (optional)
+    is the outermost key: the model-year loop passes the state so each state's
+    members are one contiguous column range of the hourly planes and
+    k_state_hourly streams them coalesced.  Stable, so ties keep caller
     order."""
     lr, cr = np.asarray(cols["load_row"]), np.asarray(cols["cf_row"])
     keys = (lr, cr) if major == "cf" else (cr, lr)
+    if by_path:
+        keys = keys + (path_class(cols),)
     if group is not None:
         keys = keys + (np.asarray(group),)
     return np.lexsort(keys).astype(np.int64)
@@ -229,34 +246,17 @@ class Engine:
         return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order,
                           nb_scan=self._nb_scan_pays(cols, n, n_scratch))
 
-    NB_SCAN_MIN_SHARE = 0.25
-
     def _nb_scan_pays(self, cols, n: int, n_scratch: int) -> bool:
-        """dgen_set_nb_scan per batch: the scan-side split pays off when a large
-        share of the batch bills net without a TS sell rate (initial tariff).
-        The share is a cost heuristic, but the two split builds re-associate
-        the battery case's net-billing sums differently: npv_pv_batt,
-        bill_w_batt, bill_wo_batt and cfev_batt of such agents can differ by
-        about 1e-9 relative between the forms (every other output and every
-        discrete decision is identical; test_nb_scan_split_equals_finance_build),
-        so these four outputs depend on the batch composition (and on the
-        at-most-10-periods LDS gate) at that level."""
+        """dgen_set_nb_scan: the battery case's net-billing split is built in
+        the hourly scan for every agent that bills net without a TS sell rate
+        (the scan decides per agent; profile_order groups those agents into
+        their own waves), so an agent's battery-case outputs do not depend on
+        the batch it is sized in.  DGEN_NB_SCAN=0 turns it off (A/B: the
+        finance kernel's build over the system-output plane; the two builds
+        re-associate the split's sums, ~1e-9 relative on the battery-case
+        bills and NPV)."""
         import os
-        force = os.environ.get("DGEN_NB_SCAN")          # "0" / "1" override the heuristic
-        if force in ("0", "1"):
-            return force == "1"
-        mo_t = getattr(self, "_tariff_mo", None)
-        if n == 0 or n_scratch == 0 or mo_t is None:
-            return True
-        try:
-            sl = np.asarray(cols["scratch_slot"])
-            mo = mo_t[np.asarray(cols["tariff0"], np.int64)]
-            ts = (mo == 2) & ((np.asarray(cols["flags"]) & 2) == 0) & (np.asarray(cols["wholesale_row"]) >= 0)
-        except Exception:          # device-tensor columns: keep the default
-            return True
-        if not self.tables.wholesale:
-            ts[:] = False
-        return bool(((sl >= 0) & ((mo == 2) | (mo == 3)) & ~ts).mean() >= self.NB_SCAN_MIN_SHARE)
+        return os.environ.get("DGEN_NB_SCAN", "1") != "0"
 
     def validate_agents(self, dev, n):
         """Host-side bounds checks before any kernel indexes a table."""
@@ -390,6 +390,23 @@ class Engine:
                    "dgen_segment_sums")
         torch.cuda.current_stream(self.dev).synchronize()
         del keep
+        return out
+
+    def rows_seq_sum(self, rows, seg_off):
+        """[R, k] float64 device rows -> [S, k]: each segment's rows added in row
+        order (dgen_rows_seq_sum; async on the current stream)."""
+        torch = _torch()
+        if rows.dtype != torch.float64 or rows.dim() != 2:
+            raise TypeError("rows_seq_sum: rows must be a [R, k] float64 tensor")
+        so = self._to_dev(np.asarray(seg_off, np.int64), torch.int64)
+        S = so.numel() - 1
+        if S < 0 or (S > 0 and (int(so[0].item()) < 0 or int(so[-1].item()) > rows.shape[0])):
+            raise ValueError("segment offsets outside the rows")
+        r = rows.contiguous()
+        out = torch.empty((max(S, 0), rows.shape[1]), dtype=torch.float64, device=self.dev)
+        _lib.check(self.lib.dgen_rows_seq_sum(self.ctx, _ptr(r), int(rows.shape[1]), _ptr(so), S, _ptr(out),
+                                              self.stream_handle()), "dgen_rows_seq_sum")
+        self._keep["_seq"] = (r, so)          # alive until the next call (stream order)
         return out
 
     def brent_selftest(self, lo, hi, xatol, c2, x0, c1, maxn=64):

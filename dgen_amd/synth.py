@@ -198,33 +198,112 @@ STATE_HOUSEHOLDS_M = np.array([
     0.73, 2.37, 0.23, 0.29, 0.25, 0.46])
 
 
-def make_population(config: str, n_agents: int, seed: Optional[int] = None,
-                    n_res_shapes: int = 4096, n_com_shapes: int = 2048, n_cf: int = 2048,
-                    n_counties: int = 3100, n_tariffs: int = 256,
-                    state_pool: Optional[np.ndarray] = None,
-                    state_mix: str = "uniform") -> Population:
-    """Synthetic population of `config` (SURVEY 8d).  `state_pool` (indices into
-    STATES) restricts the agents' states, e.g. to the states one rank of the
-    model-year loop owns (year_loop.rank_states); CA agents take the NEM3 path.
-    state_mix (mixed configs): "uniform" (every state equally likely, the
-    default stream) or "census" (states drawn in proportion to
-    STATE_HOUSEHOLDS_M, renormalised over the pool)."""
-    if config not in CONFIGS:
-        raise KeyError(f"unknown config {config!r}; one of {sorted(CONFIGS)}")
-    cnum, sector, metering, _ = CONFIGS[config]
-    rng = np.random.default_rng(20260000 + cnum if seed is None else seed)
-    n = int(n_agents)
+@dataclass
+class PopTables:
+    """The tables a population's agents index (profiles, wholesale rows,
+    compiled tariffs, DG switch rows), shared by every agent drawn against them
+    (national_tables / make_population(tables=...)): one national population
+    generated state by state, each rank drawing only its own pieces."""
+    config: str
+    shapes: np.ndarray
+    cfs: np.ndarray
+    wholesale: np.ndarray
+    tt: object                       # TariffTable
+    base_idx: np.ndarray
+    ca_idx: np.ndarray
+    n_res_shapes: int
+    n_com_shapes: int
+    n_cf: int
+    n_counties: int
+    n_tariffs: int
+    switches: Optional[np.ndarray] = None
+    sw_first: Optional[np.ndarray] = None     # [n_util, is_res, is_ca] -> switch row (-1: none)
 
+
+N_UTIL = 3000
+
+
+def _switch_rows(rng, n_tariffs: int, base_idx, ca_idx):
+    """10 % of (utility, sector) get one DG rate-switch row (solar)."""
+    has_dg = rng.random((N_UTIL, 2)) < 0.10
+    sw = []
+    first = np.full((N_UTIL, 2, 2), -1, dtype=np.int64)   # [util, is_res, is_ca] -> switch index
+    for u in range(N_UTIL):
+        for r in range(2):
+            if not has_dg[u, r]:
+                continue
+            lim = 10.0 if r == 1 else 200.0
+            k = int(rng.integers(0, n_tariffs))
+            otc = float(rng.uniform(0.0, 500.0))
+            for c in range(2):
+                rec = np.zeros((), dtype=SWITCH_DTYPE)
+                rec["min_kw"], rec["max_kw"], rec["one_time_charge"] = 0.0, lim, otc
+                rec["tariff"] = ca_idx[k] if c else base_idx[k]
+                first[u, r, c] = len(sw)
+                sw.append(rec)
+    switches = np.stack(sw).astype(SWITCH_DTYPE) if sw else np.zeros(0, dtype=SWITCH_DTYPE)
+    return switches, first
+
+
+def _tables(rng, config: str, n_res_shapes: int, n_com_shapes: int, n_cf: int, n_counties: int,
+            n_tariffs: int) -> PopTables:
+    _, _, metering, _ = CONFIGS[config]
     res_shapes = load_shapes(rng, n_res_shapes, commercial=False)
     com_shapes = load_shapes(rng, n_com_shapes, commercial=True)
     shapes = np.concatenate([res_shapes, com_shapes])
     cfs = solar_cfs(rng, n_cf)
     wholesale = wholesale_rows(rng, n_counties)
-
     tt = TariffTable(skip_demand_charges=False if metering == "nem_dc" else None)
     raw = random_tariffs(rng, n_tariffs, "nem" if metering in ("nem", "ca") else metering)
     base_idx = np.array([tt.add(d, False) for d in raw], dtype=np.int32)
     ca_idx = np.array([tt.add(d, True) for d in raw], dtype=np.int32)
+    return PopTables(config=config, shapes=shapes, cfs=cfs, wholesale=wholesale, tt=tt, base_idx=base_idx,
+                     ca_idx=ca_idx, n_res_shapes=n_res_shapes, n_com_shapes=n_com_shapes, n_cf=n_cf,
+                     n_counties=n_counties, n_tariffs=n_tariffs)
+
+
+def national_tables(config: str = "national_mixed", seed: Optional[int] = None,
+                    n_res_shapes: int = 4096, n_com_shapes: int = 2048, n_cf: int = 2048,
+                    n_counties: int = 3100, n_tariffs: int = 256) -> PopTables:
+    """The shared tables of a population generated piece by piece
+    (make_population(..., tables=T, agent_seed=...)): profiles and tariffs
+    from the config's stream, the DG switch rows from their own stream."""
+    cnum = CONFIGS[config][0]
+    s0 = 20260000 + cnum if seed is None else seed
+    T = _tables(np.random.default_rng(s0), config, n_res_shapes, n_com_shapes, n_cf, n_counties, n_tariffs)
+    T.switches, T.sw_first = _switch_rows(np.random.default_rng(s0 + 2), n_tariffs, T.base_idx, T.ca_idx)
+    return T
+
+
+def make_population(config: str, n_agents: int, seed: Optional[int] = None,
+                    n_res_shapes: int = 4096, n_com_shapes: int = 2048, n_cf: int = 2048,
+                    n_counties: int = 3100, n_tariffs: int = 256,
+                    state_pool: Optional[np.ndarray] = None,
+                    state_mix: str = "uniform", tables: Optional[PopTables] = None,
+                    agent_seed: Optional[int] = None) -> Population:
+    """Synthetic population of `config` (SURVEY 8d).  `state_pool` (indices into
+    STATES) restricts the agents' states, e.g. to the states one rank of the
+    model-year loop owns (year_loop.rank_states); CA agents take the NEM3 path.
+    state_mix (mixed configs): "uniform" (every state equally likely, the
+    default stream) or "census" (states drawn in proportion to
+    STATE_HOUSEHOLDS_M, renormalised over the pool).  tables (with
+    agent_seed): draw the agents alone, from their own stream, against shared
+    tables (national_tables; the table-size arguments are then ignored)."""
+    if config not in CONFIGS:
+        raise KeyError(f"unknown config {config!r}; one of {sorted(CONFIGS)}")
+    cnum, sector, metering, _ = CONFIGS[config]
+    if tables is None:
+        rng = np.random.default_rng(20260000 + cnum if seed is None else seed)
+        T = _tables(rng, config, n_res_shapes, n_com_shapes, n_cf, n_counties, n_tariffs)
+    else:
+        if agent_seed is None or tables.config != config:
+            raise ValueError("shared tables need their own config and an agent_seed")
+        T = tables
+        rng = np.random.default_rng(agent_seed)
+    n = int(n_agents)
+    n_res_shapes, n_com_shapes, n_cf = T.n_res_shapes, T.n_com_shapes, T.n_cf
+    n_counties, n_tariffs = T.n_counties, T.n_tariffs
+    base_idx, ca_idx = T.base_idx, T.ca_idx
 
     if sector == "res":
         is_res = np.ones(n, dtype=bool)
@@ -278,31 +357,17 @@ def make_population(config: str, n_agents: int, seed: Optional[int] = None,
     cols["ccm"] = rng.uniform(0.9, 1.2, n)
     cols["vor"] = np.where(rng.random(n) < 0.2, rng.uniform(0.0, 300.0, n), 0.0)
 
-    # 10 % of (utility, sector) get one DG rate-switch row (solar)
-    n_util = 3000
-    util = rng.integers(0, n_util, n)
-    has_dg = rng.random((n_util, 2)) < 0.10
-    sw = []
-    first = np.full((n_util, 2, 2), -1, dtype=np.int64)   # [util, is_res, is_ca] -> switch index
-    for u in range(n_util):
-        for r in range(2):
-            if not has_dg[u, r]:
-                continue
-            lim = 10.0 if r == 1 else 200.0
-            k = int(rng.integers(0, n_tariffs))
-            otc = float(rng.uniform(0.0, 500.0))
-            for c in range(2):
-                rec = np.zeros((), dtype=SWITCH_DTYPE)
-                rec["min_kw"], rec["max_kw"], rec["one_time_charge"] = 0.0, lim, otc
-                rec["tariff"] = ca_idx[k] if c else base_idx[k]
-                first[u, r, c] = len(sw)
-                sw.append(rec)
-    switches = np.stack(sw).astype(SWITCH_DTYPE) if sw else np.zeros(0, dtype=SWITCH_DTYPE)
+    util = rng.integers(0, N_UTIL, n)
+    if T.switches is None:           # one stream: the switch rows follow the agents' draws
+        switches, first = _switch_rows(rng, n_tariffs, base_idx, ca_idx)
+    else:
+        switches, first = T.switches, T.sw_first
     idx = first[util, is_res.astype(int), is_ca.astype(int)]
     cols["sw_solar_off"] = np.where(idx >= 0, idx, 0).astype(np.int32)
     cols["sw_solar_cnt"] = (idx >= 0).astype(np.int32)
     cols["sw_storage_off"] = np.zeros(n, dtype=np.int32)
     cols["sw_storage_cnt"] = np.zeros(n, dtype=np.int32)
+    tt = T.tt
     tariffs = tt.array()
     n_scratch = assign_scratch(cols, tariffs, switches)
     if not (sector == "mixed" or metering == "mixed"):
@@ -314,7 +379,7 @@ def make_population(config: str, n_agents: int, seed: Optional[int] = None,
         if metering == "ca":
             pool = np.asarray([STATES.index("CA")])
         state_ix = pool[srng.integers(0, len(pool), n)]
-    return Population(shapes=shapes, cfs=cfs, wholesale=wholesale, tariffs=tariffs,
+    return Population(shapes=T.shapes, cfs=T.cfs, wholesale=T.wholesale, tariffs=tariffs,
                       switches=switches, cols=cols, n_scratch=n_scratch, config=config,
                       state_ix=state_ix.astype(np.int16),
                       demand=tt.demand_array() if metering == "nem_dc" else None,
@@ -392,3 +457,85 @@ def reference_frame(n: int, seed: int = 20260811, n_load: int = 512, n_cf: int =
                              "res_com": rc, "min_kw_limit": 0.0, "max_kw_limit": 10.0 if rc == "R" else 200.0,
                              "one_time_charge": float(rng.uniform(0, 500))})
     return df, store, pd.DataFrame(rows)
+
+
+# ------------------------------------------------ national population by pieces
+STATE_SEED0 = 20265000          # agents of state s: default_rng(STATE_SEED0 + 7919 * s)
+CUST_SEED0 = 20266000           # customers in bin of state s: default_rng(CUST_SEED0 + 7919 * s)
+
+
+def _state_seed(s: int, seed0: int) -> int:
+    return int(seed0) + 7919 * int(s)
+
+
+def state_member_sectors(config: str, s: int, n_s: int, seed0: int = STATE_SEED0) -> np.ndarray:
+    """Sector code (0 res, 1 com) of every member of state s of a national
+    population by pieces: the first draw of the state's agent stream, so any
+    rank can know a split state's groups without generating its agents."""
+    sector = CONFIGS[config][1]
+    if sector == "res":
+        return np.zeros(int(n_s), np.int64)
+    if sector == "com":
+        return np.ones(int(n_s), np.int64)
+    return np.where(np.random.default_rng(_state_seed(s, seed0)).random(int(n_s)) < 0.75, 0, 1).astype(np.int64)
+
+
+def state_id_base(sizes) -> np.ndarray:
+    """First agent_id of each state (ids are state-major, members in order)."""
+    sizes = np.asarray(sizes, np.int64)
+    return np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+
+
+def shard_population(tables: PopTables, plan, rank: int, seed0: int = STATE_SEED0,
+                     cust_seed0: int = CUST_SEED0):
+    """One rank's agents of a national population by pieces (partition.
+    ShardPlan): state s's agents are make_population(state_pool=[s]) drawn
+    from their own stream against the shared tables, sliced to the rank's
+    member range.  Returns (Population, loop agent columns: agent_id (state-
+    major global ids), state, sector, county, customers_in_bin, member)."""
+    sizes = np.asarray(plan.sizes, np.int64)
+    base = state_id_base(sizes)
+    cols, county, st, mem, cust, aid = [], [], [], [], [], []
+    for s, lo, hi in plan.pieces[rank]:
+        n_s = int(sizes[s])
+        p = make_population(tables.config, n_s, tables=tables, agent_seed=_state_seed(s, seed0),
+                            state_pool=[s], state_mix="uniform")
+        sl = slice(lo, hi)
+        cols.append({k: np.asarray(v)[sl] for k, v in p.cols.items()})
+        county.append(np.asarray(p.county_ix)[sl])
+        st.append(np.full(hi - lo, s, np.int64))
+        mem.append(np.arange(lo, hi, dtype=np.int64))
+        aid.append(base[s] + np.arange(lo, hi, dtype=np.int64))
+        is_res = (np.asarray(p.cols["flags"]) & 1).astype(bool)
+        crng = np.random.default_rng(_state_seed(s, cust_seed0))
+        c = np.where(is_res, crng.lognormal(np.log(400.0), 0.5, n_s), crng.lognormal(np.log(40.0), 0.5, n_s))
+        cust.append(c[sl])
+    keys = list(cols[0].keys()) if cols else list(empty_columns(0).keys())
+    merged = {k: np.concatenate([c[k] for c in cols]) if cols else empty_columns(0)[k] for k in keys}
+    tariffs = tables.tt.array()
+    n_scratch = assign_scratch(merged, tariffs, tables.switches)
+    state = np.concatenate(st) if st else np.zeros(0, np.int64)
+    metering = CONFIGS[tables.config][2]
+    pop = Population(shapes=tables.shapes, cfs=tables.cfs, wholesale=tables.wholesale, tariffs=tariffs,
+                     switches=tables.switches, cols=merged, n_scratch=n_scratch, config=tables.config,
+                     state_ix=state.astype(np.int16),
+                     demand=tables.tt.demand_array() if metering == "nem_dc" else None,
+                     county_ix=np.concatenate(county) if county else np.zeros(0, np.int32))
+    sector = np.where((np.asarray(merged["flags"]) & 1) != 0, 0, 1).astype(np.int64)
+    agents = {"agent_id": np.concatenate(aid) if aid else np.zeros(0, np.int64), "state": state,
+              "sector": sector, "county": np.asarray(pop.county_ix, np.int64),
+              "customers_in_bin": np.concatenate(cust) if cust else np.zeros(0),
+              "member": np.concatenate(mem) if mem else np.zeros(0, np.int64)}
+    return pop, agents
+
+
+def split_state_members(config: str, plan, seed0: int = STATE_SEED0):
+    """({s: member sectors}, {s: member agent ids}) of every split state of
+    the plan (partition.split_groups' inputs), the same on every rank."""
+    base = state_id_base(plan.sizes)
+    sec, ids = {}, {}
+    for s in plan.split_states():
+        n_s = int(plan.sizes[s])
+        sec[s] = state_member_sectors(config, s, n_s, seed0)
+        ids[s] = base[s] + np.arange(n_s, dtype=np.int64)
+    return sec, ids

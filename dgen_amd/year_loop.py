@@ -31,11 +31,19 @@ the next:
                          adopters, market value and cumulative PV / battery
                          capacity stay on device as the next year's inputs
 
-Sharding: a rank owns WHOLE states (`rank_states`), so the (state, sector)
-groups of the largest-remainder attachment and the per-state hourly sums are
-rank-local, exactly as in the single-process reference; the only exchange is
-the per-state totals (and per-state hourly rows) all-reduce at the end of each
-year.  Nothing here runs on the CPU except index bookkeeping done once.
+Sharding: a rank owns pieces of states -- whole states (`rank_states`, or a
+dgen_amd.partition.ShardPlan) or member ranges of a state split across ranks
+for balance (plan_partition).  Per-state totals and 8760-h rows are sums of
+fixed 8192-member chunk partials in chunk order (bit-identical however the
+states are cut), merged by ONE all-reduce per year; a split state's
+(state, sector) attachment groups gather their new adopters (one more
+all-reduce of disjoint positions) and are allocated whole on every rank that
+holds a piece (the reference allocates on the gathered frame,
+dgen_model.py:408-427).  The first model year gathers the split groups'
+developable weights the same way for the initial market shares.  A year is a
+generator of exchange requests (`year_steps`): run_year drives it with the
+process group's all-reduce, `run_lockstep` with an in-process sum over shards
+(tests).  Nothing here runs on the CPU except index bookkeeping done once.
 
 Synthetic stand-ins (the DB tables are not available offline): Bass
 parameters per (state, sector), the max-market-share curves, storage
@@ -62,6 +70,7 @@ from .attachment import export_weights, state_hourly, string_ranks
 from .diffusion import DIFF_IN, DIFF_OUT, DiffIn, DiffOut, MmsTable, mms_table
 from .diffusion import _bind as _bind_diff
 from .dist import allreduce_sum
+from .partition import REDUCE_CHUNK, ChunkLayout, SplitGroups, chunk_layout
 from .synth import STATES
 
 SECTORS = ("res", "com")
@@ -284,7 +293,8 @@ class YearLoop:
 
     def __init__(self, engine, pop, agents: Dict[str, np.ndarray], tables: LoopTables,
                  first_year: int = 2026, hourly_export: bool = True,
-                 hourly_chunk: Optional[int] = None, order: Optional[np.ndarray] = None):
+                 hourly_chunk: Optional[int] = None, order: Optional[np.ndarray] = None,
+                 plan=None, split: Optional[SplitGroups] = None):
         import torch
         from .engine import profile_order
         self.eng, self.tables = engine, tables
@@ -292,7 +302,23 @@ class YearLoop:
         self.hourly_export, self.hourly_chunk = bool(hourly_export), hourly_chunk
         n = len(pop.cols["load_kwh"])
         self.n = n
-        perm = (profile_order(pop.cols, group=np.asarray(agents["state"])) if order is None
+        st_all = np.asarray(agents["state"], np.int64)
+        # member index of each agent within its state (caller order); a shard
+        # of whole states numbers them itself, a piece of a split state gets
+        # them from the plan (agents["member"])
+        if "member" in agents:
+            member = np.asarray(agents["member"], np.int64)
+        else:
+            member = np.zeros(n, np.int64)
+            for s in np.unique(st_all):
+                ix = np.flatnonzero(st_all == s)
+                member[ix] = np.arange(ix.size)
+        # device order: by (state, reduction chunk), then billing path and
+        # profile rows (profile_order): each chunk is one contiguous, canonical
+        # run of device rows
+        self.chunk = int(plan.chunk) if plan is not None else REDUCE_CHUNK
+        gkey = st_all * (1 << 32) + member // self.chunk
+        perm = (profile_order(pop.cols, group=gkey) if order is None
                 else np.asarray(order, np.int64))
         self.perm = perm
         inv = np.empty(n, np.int64)
@@ -316,6 +342,7 @@ class YearLoop:
         self.frame = frame
         st, sec = agents["state"], agents["sector"]
         self.state_caller = st
+        self.sector_caller = sec
         # per-agent Bass parameters (the reference's merge on (state, sector), :41-44)
         b = tables.bass[tables.bass["tech"] == "solar"].set_index(["state_abbr", "sector_abbr"])
         keys = [(STATES[s], SECTORS[c]) for s, c in zip(st, sec)]
@@ -335,36 +362,58 @@ class YearLoop:
                                factor_min=fmin, pad=0, min_pb=min_pb, max_pb=max_pb)
         self.mms_row = torch.as_tensor(np.array([rows.get(SECTORS[c], -1) for c in sec],
                                                 np.int32)[perm], device=dev)
-        # (state, sector) attachment groups in caller (reference row) order
+        # (state, sector) attachment groups in caller (reference row) order;
+        # the groups of split states are allocated whole from a gather (split)
+        self.split = split
+        split_states = set(plan.split_states()) if plan is not None else set()
         g_keys = list(zip(st.tolist(), sec.tolist()))
         g_first: Dict = {}
         for i, k in enumerate(g_keys):
+            if k[0] in split_states:
+                continue
             g_first.setdefault(k, []).append(i)
-        g_idx = np.concatenate([np.asarray(v, np.int64) for v in g_first.values()]) if n else \
+        g_idx = np.concatenate([np.asarray(v, np.int64) for v in g_first.values()]) if g_first else \
             np.zeros(0, np.int64)
-        g_off = np.concatenate([[0], np.cumsum([len(v) for v in g_first.values()])]).astype(np.int64)
+        g_off = [0] + np.cumsum([len(v) for v in g_first.values()]).tolist()
+        g_rate = [tables.attach_rate[k[0]] for k in g_first]
+        aid_local = string_ranks(agents["agent_id"])[g_idx] if g_idx.size else np.zeros(0, np.int64)
+        # split groups this rank holds members of: the whole group is allocated
+        # here; own members sit at [own_off, own_off + own_cnt) of the group
+        self.sg = []          # (buffer offset, group size, own offset, own device rows [torch])
+        aid_parts, pos = [aid_local], int(g_idx.size)
+        self.m_local = int(g_idx.size)
+        if split is not None:
+            for j, (key, G) in enumerate(zip(split.keys, split.size)):
+                cnt = int(split.own_cnt[j])
+                if cnt == 0:
+                    continue
+                s_, c_ = key
+                own = np.flatnonzero((st == s_) & (sec == c_))           # caller order = member order
+                if own.size != cnt:
+                    raise ValueError(f"split group {key}: {own.size} members here, plan says {cnt}")
+                self.sg.append((int(split.buf_off[j]), int(G), int(split.own_off[j]),
+                                torch.as_tensor(inv[own], device=dev), pos))
+                aid_parts.append(split.aid_rank[j])
+                g_off.append(g_off[-1] + int(G))
+                g_rate.append(tables.attach_rate[s_])
+                pos += int(G)
+        self.m_attach = pos
         self.g_dev = torch.as_tensor(inv[g_idx], device=dev)
-        self.g_off = torch.as_tensor(g_off, device=dev)
-        self.g_n = len(g_first)
-        self.g_rate = torch.as_tensor(np.array([tables.attach_rate[k[0]] for k in g_first],
-                                               np.float64), device=dev)
-        self.aid_rank = torch.as_tensor(string_ranks(agents["agent_id"])[g_idx], device=dev)
-        # state segments (first-appearance order, like the export's groupby)
-        s_first: Dict = {}
-        for i, s in enumerate(st.tolist()):
-            s_first.setdefault(s, []).append(i)
-        self.local_states = list(s_first.keys())
-        s_idx = np.concatenate([np.asarray(v, np.int64) for v in s_first.values()]) if n else \
-            np.zeros(0, np.int64)
-        self.s_off = np.concatenate([[0], np.cumsum([len(v) for v in s_first.values()])]).astype(np.int64)
-        # device column of each state member, ascending within the state: with
-        # the state-major device order each state is one contiguous range and
-        # the export's plane reads are coalesced (the sum order is the
-        # kernel's own fixed order either way)
-        self.s_dev_idx = np.concatenate([np.sort(inv[np.asarray(v, np.int64)]) for v in s_first.values()]) \
-            if n else np.zeros(0, np.int64)
+        self.g_off = torch.as_tensor(np.asarray(g_off, np.int64), device=dev)
+        self.g_n = len(g_off) - 1
+        self.g_rate = torch.as_tensor(np.asarray(g_rate, np.float64), device=dev)
+        self.aid_rank = torch.as_tensor(np.concatenate(aid_parts).astype(np.int64), device=dev)
+        self.n_buf = split.n_buf if split is not None else 0
+        # reduction chunks (dgen_amd.partition): fixed 8192-member chunks of each
+        # state, device rows ascending within a chunk; per-state rows are the
+        # chunk partials summed in chunk order
+        self.state_dev_order = st_all[perm]                   # state of each device row
+        self.layout: ChunkLayout = chunk_layout(self.state_dev_order, member[perm], len(STATES), plan,
+                                                chunk=self.chunk)
+        self.s_dev_idx = self.layout.seg_dev
+        self.s_off = self.layout.seg_off
         self.s_dev = torch.as_tensor(self.s_dev_idx, device=dev)
-        self.state_dev_order = np.asarray(st, np.int64)[perm]   # state of each device row
+        self.local_states = sorted(set(self.state_dev_order.tolist()))
         # carry (market_last_year), device order
         z = lambda: torch.zeros(n, dtype=torch.float64, device=dev)
         self.carry = {k: z() for k in ("market_share_last_year", "adopters_cum_last_year",
@@ -389,21 +438,68 @@ class YearLoop:
         # form); the chunked export's sub-batches copy it from here
         self.batch.c_agents.max_years = self.year_inputs.max_years(year)
 
-    def initial_market(self):
+    def _initial_market_steps(self):
         """First model year: elec.estimate_initial_market_shares (elec.py:701-765)
-        on device from the state starting capacities, into the carry."""
+        on device from the state starting capacities, into the carry.  Its
+        per-(state, sector, tech) group sums need whole groups: a split group's
+        developable weights are gathered (exchange) and the group is computed
+        whole here, own members' rows kept (a generator: yields the gather)."""
+        import torch
         from .market import initial_market_shares
         caps = self.tables.caps if self.tables.caps is not None else pd.DataFrame(
             columns=["state_abbr", "sector_abbr", "system_mw", "batt_mw", "batt_mwh", "pv_systems_count",
                      "batt_systems_count"])
         st, sec = self.caller_frame          # pandas' group sums visit the frame (caller) order
-        ini = initial_market_shares(self.eng, st, sec, ["solar"] * self.n, self.dev_w,
-                                    self.batch.cols["capex"], caps, dev_index=self.inv)
+        n = self.n
+        w, cx = self.dev_w, self.batch.cols["capex"]
+        if self.split is None or self.n_buf == 0:
+            ini = initial_market_shares(self.eng, st, sec, ["solar"] * n, w, cx, caps, dev_index=self.inv)
+        else:
+            buf = torch.zeros(self.n_buf, dtype=torch.float64, device=self.eng.dev)
+            for b0, G, o, rows, _ in self.sg:
+                buf[b0 + o:b0 + o + rows.numel()] = w.index_select(0, rows)
+            buf = yield buf
+            # extended frame: this rank's rows outside split groups, then every
+            # split group it holds members of, whole, in group (caller) order
+            split_keys = {(k[0], k[1]) for k in self.split.keys}
+            stc = np.asarray(self.state_caller, np.int64)
+            seco = np.asarray(self.sector_caller, np.int64)
+            keep = np.array([(a, b) not in split_keys for a, b in zip(stc.tolist(), seco.tolist())], bool)
+            rows_local = np.flatnonzero(keep)
+            fst = [st[i] for i in rows_local]
+            fsec = [sec[i] for i in rows_local]
+            dev_index = [self.inv[rows_local]]
+            vals_w, vals_c = [w], [cx]
+            ext = n
+            take = []
+            for (b0, G, o, rows, _), key in zip(self.sg, [k for k, c in zip(self.split.keys, self.split.own_cnt)
+                                                          if c > 0]):
+                fst += [STATES[key[0]]] * G
+                fsec += [SECTORS[key[1]]] * G
+                dev_index.append(np.arange(ext, ext + G, dtype=np.int64))
+                vals_w.append(buf[b0:b0 + G])
+                cg = torch.zeros(G, dtype=torch.float64, device=self.eng.dev)
+                cg[o:o + rows.numel()] = cx.index_select(0, rows)
+                vals_c.append(cg)
+                take.append((ext + o, rows))
+                ext += G
+            ini = initial_market_shares(self.eng, fst, fsec, ["solar"] * len(fst), torch.cat(vals_w),
+                                        torch.cat(vals_c), caps, dev_index=np.concatenate(dev_index))
+            for k in list(ini.keys()):
+                v = ini[k]
+                if isinstance(v, torch.Tensor) and v.dim() == 1 and v.numel() == ext:
+                    own = v[:n].clone()
+                    for e0, rows in take:
+                        own.index_copy_(0, rows, v[e0:e0 + rows.numel()])
+                    ini[k] = own
         c = self.carry
         for k in ("market_share_last_year", "adopters_cum_last_year", "market_value_last_year",
                   "system_kw_cum_last_year", "batt_kw_cum_last_year", "batt_kwh_cum_last_year"):
             c[k].copy_(ini[k])
         return ini
+
+    def initial_market(self, exchange=None):
+        return _drive(self._initial_market_steps(), exchange or allreduce_sum)
 
     def _max_market_share(self):
         import torch
@@ -435,16 +531,38 @@ class YearLoop:
                                           int(first), eng.stream_handle()), "dgen_diffusion")
         return outs
 
-    def _attach(self, new_adopters):
+    def _attach_steps(self, new_adopters):
+        """Largest-remainder battery adopters per (state, sector) group
+        (k_batt_attach).  Split groups: the members' new adopters are gathered
+        (yield) and each group is allocated whole, own members' results kept."""
         import torch
         eng, n, g = self.eng, self.n, self.g_dev
-        src = {"new_adopters": new_adopters.index_select(0, g), "aid_rank": self.aid_rank,
-               "batt_kw": self.out["batt_kw"].index_select(0, g),
-               "batt_kwh": self.out["batt_kwh"].index_select(0, g),
-               "batt_kw_cum_last_year": self.carry["batt_kw_cum_last_year"].index_select(0, g),
-               "batt_kwh_cum_last_year": self.carry["batt_kwh_cum_last_year"].index_select(0, g)}
-        grp = {k: torch.empty(n, dtype=torch.int64 if k == "added" else torch.float64,
-                              device=eng.dev) for k in ATTACH_OUT}
+        dev = eng.dev
+        gathered = None
+        if self.n_buf:
+            buf = torch.zeros(self.n_buf, dtype=torch.float64, device=dev)
+            for b0, G, o, rows, _ in self.sg:
+                buf[b0 + o:b0 + o + rows.numel()] = new_adopters.index_select(0, rows)
+            gathered = yield buf
+        M = self.m_attach
+
+        def col(v, gather=None):
+            x = torch.zeros(M, dtype=torch.float64, device=dev)
+            if self.m_local:
+                x[:self.m_local] = v.index_select(0, g)
+            for b0, G, o, rows, p0 in self.sg:
+                if gather is not None:
+                    x[p0:p0 + G] = gather[b0:b0 + G]
+                else:
+                    x[p0 + o:p0 + o + rows.numel()] = v.index_select(0, rows)
+            return x
+
+        src = {"new_adopters": col(new_adopters, gathered), "aid_rank": self.aid_rank,
+               "batt_kw": col(self.out["batt_kw"]), "batt_kwh": col(self.out["batt_kwh"]),
+               "batt_kw_cum_last_year": col(self.carry["batt_kw_cum_last_year"]),
+               "batt_kwh_cum_last_year": col(self.carry["batt_kwh_cum_last_year"])}
+        grp = {k: torch.empty(M, dtype=torch.int64 if k == "added" else torch.float64,
+                              device=dev) for k in ATTACH_OUT}
         ci = AttachIn(**{k: src[k].data_ptr() for k in ATTACH_IN})
         co = AttachOut(**{k: grp[k].data_ptr() for k in ATTACH_OUT})
         if self.g_n:
@@ -453,61 +571,75 @@ class YearLoop:
                                                 self.g_n, eng.stream_handle()), "dgen_batt_attach")
         res = {}
         for k, v in grp.items():                    # group order -> device order
-            d = torch.empty_like(v)
-            d.index_copy_(0, g, v)
+            d = torch.empty(n, dtype=v.dtype, device=dev)
+            if self.m_local:
+                d.index_copy_(0, g, v[:self.m_local])
+            for b0, G, o, rows, p0 in self.sg:
+                d.index_copy_(0, rows, v[p0 + o:p0 + o + rows.numel()])
             res[k] = d
         return res
 
     def _state_hourly(self, w):
-        """[S_local, 8760] MW in local_states order."""
+        """[C_local, 8760] MW: each reduction chunk's partial, chunks in layout
+        order (combined per state by partition.combine_rows)."""
         import torch
         eng = self.eng
         if self.hourly_chunk is None:
             planes = (self.out["baseline"], self.out["net_pvonly"], self.out["net_with_batt"])
             return state_hourly(eng, planes, w, self.s_dev_idx, self.s_off)
-        # chunked: each chunk of device rows gets its hourly planes from the
-        # scan alone (dgen_hourly_planes, from this year's sizing outputs:
-        # the chunk's slices of self.out), then its members are summed per
-        # state (the planes depend only on the agent)
+        # chunked: runs of device rows get their hourly planes from the scan
+        # alone (dgen_hourly_planes, from this year's sizing outputs: the run's
+        # slices of self.out), then each reduction chunk's members are summed.
+        # Reduction chunks are contiguous device-row ranges; a run ends on a
+        # chunk boundary, so every chunk partial comes from one run.
         from .engine import AgentBatch
-        S = len(self.local_states)
-        if getattr(self, "_chunk_groups", None) is None:
-            # per chunk: its rows grouped by local state (fixed across years)
-            ls = np.asarray(self.local_states, np.int64)
-            pos = np.full(int(ls.max()) + 1 if ls.size else 1, -1, np.int64)
-            pos[ls] = np.arange(ls.size)
-            self._chunk_groups = []
-            for a in range(0, self.n, int(self.hourly_chunk)):
-                p = pos[self.state_dev_order[a:a + int(self.hourly_chunk)]]
-                cnt = np.bincount(p, minlength=S)
-                self._chunk_groups.append((np.argsort(p, kind="stable"),
-                                           np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)))
-        acc = torch.zeros((S, _lib.NH), dtype=torch.float64, device=eng.dev)
-        ch = int(self.hourly_chunk)
+        if getattr(self, "_runs", None) is None:
+            off = self.s_off
+            starts = np.asarray([int(self.s_dev_idx[off[j]]) for j in range(len(off) - 1)], np.int64)
+            ends = np.asarray([int(self.s_dev_idx[off[j + 1] - 1]) + 1 for j in range(len(off) - 1)], np.int64)
+            if np.any(ends - starts != np.diff(off)):
+                raise RuntimeError("reduction chunks are not contiguous device-row ranges")
+            runs, j0 = [], 0
+            ch = int(self.hourly_chunk)
+            while j0 < len(starts):
+                j1 = j0 + 1
+                while j1 < len(starts) and ends[j1] - starts[j0] <= ch:
+                    j1 += 1
+                a, b = int(starts[j0]), int(ends[j1 - 1])
+                seg = [(int(s0) - a, int(e0) - a) for s0, e0 in zip(starts[j0:j1], ends[j0:j1])]
+                idx = np.concatenate([np.arange(s0, e0) for s0, e0 in seg]).astype(np.int64)
+                so = np.concatenate([[0], np.cumsum([e0 - s0 for s0, e0 in seg])]).astype(np.int64)
+                runs.append((a, b, idx, so))
+                j0 = j1
+            self._runs = runs
+            mx = max((b - a for a, b, _, _ in runs), default=0)
+            self._chunk_planes = {k: torch.empty(_lib.NH * max(mx, 1), dtype=torch.float32, device=eng.dev)
+                                  for k in _lib.OUTPUT_HOURLY}
         B = self.batch
-        for a in range(0, self.n, ch):
-            b = min(a + ch, self.n)
+        parts = []
+        for a, b, idx, so in self._runs:
             m = b - a
             cols = {k: v[a:b] for k, v in B.cols.items()}
             ca = _lib.Agents(**{name: cols[name].data_ptr() for name, _ in _lib.AGENT_COLUMNS})
             ca.max_years = B.c_agents.max_years
             sub = AgentBatch(n=m, n_scratch=B.n_scratch, cols=cols, workspace=B.workspace,
                              c_agents=ca, nb_scan=B.nb_scan)
-            # the chunk's rows of the sizing outputs, and the first 8760*m floats
-            # of each plane buffer viewed as [2190][m][4] tiles
             out = {k: v[a:b] for k, v in self.out.items() if v is not None}
             out.update({k: v[:_lib.NH * m].view(_lib.NH // 4, m, 4)
                         for k, v in self._chunk_planes.items()})
             co = eng.c_outputs(out)
             planes = (out["baseline"], out["net_pvonly"], out["net_with_batt"])
             eng.hourly_planes(sub, co)
-            order, off = self._chunk_groups[a // ch]
             wc = tuple(x[a:b] for x in w)
-            acc += state_hourly(eng, planes, wc, order, off)
-        return acc
+            parts.append(state_hourly(eng, planes, wc, idx, so))
+        return torch.cat(parts) if parts else torch.zeros((0, _lib.NH), dtype=torch.float64, device=eng.dev)
 
-    def run_year(self, year: int, keep_per_agent: bool = False) -> YearResult:
+    def year_steps(self, year: int, keep_per_agent: bool = False):
+        """One model year as a generator: it yields the tensors to be summed over
+        the ranks (the split groups' gathers, the per-state table) and receives
+        the sums; returns the YearResult (run_year / run_lockstep drive it)."""
         import torch
+        from .partition import rows_finish, rows_table
         eng = self.eng
         first = year == self.first_year
         torch.cuda.synchronize(eng.dev)
@@ -516,25 +648,29 @@ class YearLoop:
         eng.size(self.batch, self.out, self.c_out)
         mms = self._max_market_share()
         if first:
-            self.initial_market()
+            yield from self._initial_market_steps()
         d = self._diffusion(mms, first)
-        att = self._attach(d["new_adopters"])
+        att = yield from self._attach_steps(d["new_adopters"])
         hourly_local = None
         if self.hourly_export:
             # the export reads the frame's last-year battery cumulative (:185)
             w = export_weights(eng, self.cust, d["number_of_adopters"],
                                self.carry["batt_kw_cum_last_year"], self.out["batt_kw"], att["added"])
             hourly_local = self._state_hourly(w)
-        # per-state totals (dgen_model.py:437-440) on device, one all-reduce
+        # per-chunk totals (dgen_model.py:437-440), then per-state rows of totals
+        # and hourly sums through one all-reduce (partition.rows_table)
         sd = self.s_dev
         cols = torch.stack([d["system_kw_cum"].index_select(0, sd), att["batt_kw_cum"].index_select(0, sd),
                             att["batt_kwh_cum"].index_select(0, sd),
                             d["number_of_adopters"].index_select(0, sd),
                             torch.ones(self.n, dtype=torch.float64, device=eng.dev)])
-        loc = eng.segment_sums(cols, self.s_off)                     # [S_local, 5]
-        totals = merge_state_rows(loc, self.local_states, len(STATES))
-        hourly = (merge_state_rows(hourly_local, self.local_states, len(STATES))
-                  if hourly_local is not None else None)
+        loc = eng.segment_sums(cols, self.s_off)                     # [C_local, 5]
+        rows = loc if hourly_local is None else torch.cat([loc, hourly_local], dim=1)
+        table = rows_table(rows, self.layout, eng.rows_seq_sum)
+        table = yield table
+        merged = rows_finish(table, self.layout, eng.rows_seq_sum)
+        totals = merged[:, :5].contiguous()
+        hourly = merged[:, 5:].contiguous() if hourly_local is not None else None
         per_agent = {}
         if keep_per_agent:
             per_agent = {"max_market_share": mms, **d, **att,
@@ -551,6 +687,11 @@ class YearLoop:
         return YearResult(year=year, totals=totals, hourly=hourly,
                           seconds=time.perf_counter() - t0, per_agent=per_agent)
 
+    def run_year(self, year: int, keep_per_agent: bool = False, exchange=None) -> YearResult:
+        """One model year; exchange(t) sums t over the ranks (default: the
+        process group's all-reduce, identity without one)."""
+        return _drive(self.year_steps(year, keep_per_agent), exchange or allreduce_sum)
+
     def reset(self):
         """Back to an empty market (before the first model year)."""
         for v in self.carry.values():
@@ -558,3 +699,38 @@ class YearLoop:
 
     def run(self, years: Sequence[int]) -> List[YearResult]:
         return [self.run_year(int(y)) for y in years]
+
+
+def _drive(gen, exchange):
+    """Run a year_steps-style generator, answering each yielded tensor with
+    exchange(tensor); returns the generator's value."""
+    try:
+        req = next(gen)
+        while True:
+            req = gen.send(exchange(req))
+    except StopIteration as e:
+        return e.value
+
+
+def run_lockstep(loops: Sequence["YearLoop"], year: int, keep_per_agent: bool = False):
+    """The shards of one model year run in one process, their exchanges summed
+    here in shard order (what the all-reduce over their ranks returns): the
+    multi-rank loop by construction on one GPU (tests)."""
+    import torch
+    gens = [lp.year_steps(year, keep_per_agent) for lp in loops]
+    reqs = [next(g) for g in gens]
+    while True:
+        tot = reqs[0].clone()
+        for r in reqs[1:]:
+            tot += r
+        done, nxt = [], []
+        for g in gens:
+            try:
+                nxt.append(g.send(tot.clone()))
+            except StopIteration as e:
+                done.append(e.value)
+        if done:
+            if len(done) != len(gens):
+                raise RuntimeError("shards disagree on the year's exchanges")
+            return done
+        reqs = nxt

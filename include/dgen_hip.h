@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 8
+#define DGEN_ABI_VERSION 9
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_NH    8760   /* hours per year                                    */
@@ -303,6 +303,15 @@ int32_t dgen_brent_selftest(dgen_ctx* ctx, const double* lo, const double* hi,
 int32_t dgen_segment_sums(dgen_ctx* ctx, const void* v1, const double* w1, const void* v2,
                           const double* w2, int32_t values_f32, int32_t k, int64_t n,
                           const int64_t* seg_off, int64_t n_seg, double* out, void* stream);
+
+/* Sequential sum of row segments (ABI 9): out[s * k + j] = the rows
+ * r in [seg_off[s], seg_off[s+1]) of in[r * k + j] added in row order
+ * (((r0 + r1) + r2) + ...).  The model-year loop forms each state's totals and
+ * 8760-h rows as the sum of fixed-size member chunks' partials in chunk order
+ * (dgen_amd/partition.py), so a state split across ranks sums to the same bits
+ * as on one rank.  n_seg <= 65535.                                           */
+int32_t dgen_rows_seq_sum(dgen_ctx* ctx, const double* in, int64_t k, const int64_t* seg_off,
+                          int64_t n_seg, double* out, void* stream);
 
 /* ------------------------------------------------------------------------
  * Diffusion step: the per-agent arithmetic of

@@ -35,22 +35,14 @@ VARIANTS = {
     # whose whole need fits, wave-days where it fits for all lanes, saturated)
     "phase_day": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
                   ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1")],
-    # demand envelopes prebuilt by k_dc_env ahead of k_size (A/B: slower)
-    "dc_prebuild": [("#define DGEN_DC_PREBUILD 0", "#define DGEN_DC_PREBUILD 1")],
     # NEM bins build: slot-sum loads in flight per batch (4 = the product)
     "bins_bb8": [("        constexpr int BB = 4;\n", "        constexpr int BB = 8;\n")],
     "bins_bb12": [("        constexpr int BB = 4;\n", "        constexpr int BB = 12;\n")],
     # hour-lane envelope build: days of loads in flight per lane
     "dcb16": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 16;")],
     "dcb12": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 12;")],
-    # battery-case NEM finance in k_hourly_batt's tail (A/B: slower)
-    "fin_fold": [("#define DGEN_FIN_FOLD 0", "#define DGEN_FIN_FOLD 1")],
-    # XCD-aware block order in k_hourly_batt
-    "xcd": [("#define DGEN_XCD_REMAP 0", "#define DGEN_XCD_REMAP 1")],
     # phase timers only (DGEN_PHASE_PROF slots, see dgen_hip.hip)
     "phase": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1")],
-    # k_size builds the demand envelopes with the serial month lanes
-    "dc_serial": [("#define DGEN_DC_SERIAL 0", "#define DGEN_DC_SERIAL 1")],
     # timing probes of the hour-lane envelope build (wrong results by construction)
     "dcb_nopass2": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
                     ("        // pass 2: the lines above the bound, per day type\n        for (int dt = 0; dt < 2; dt++) {",

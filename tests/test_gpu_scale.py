@@ -184,3 +184,46 @@ def test_c5_loop_2p5m_sample_vs_oracle(engine):
                          pa["system_kw_cum_last_year_in"], y == 2026)
         for k in ("market_share", "new_adopters", "number_of_adopters", "system_kw_cum"):
             assert np.allclose(pa[k], d[k], rtol=1e-12, atol=1e-12), (y, k)
+
+
+def test_rank_shards_balanced_on_measured_device_time(engine):
+    """The 8 rank shards of a 2.5M-agent census national population (the C5
+    per-GPU scale: 20M over 8 GPUs would be 8x each shard), cut by the
+    partition's per-path cost model with states split where balance needs it,
+    sized one after the other on this GPU: measured device time (HIP events
+    of the sizing kernels) max / mean <= 1.15."""
+    from dgen_amd import partition as P
+    from dgen_amd.synth import STATES, national_tables, shard_population
+    T = national_tables()
+    engine.load_profiles(T.shapes, T.cfs, T.wholesale)
+    engine.set_tariffs(T.tt.array())
+    engine.set_switches(T.switches)
+    naep_row = T.cfs.astype(np.float64).sum(axis=1) / 1e6
+    sizes = P.census_sizes(2_500_000)
+    cost = np.zeros(len(STATES))
+    for s in range(len(STATES)):
+        smp = make_population("national_mixed", 2000, tables=T, agent_seed=20268000 + s, state_pool=[s])
+        cost[s] = P.cost_per_agent(smp.cols, naep_row[smp.cols["cf_row"]]).mean()
+    plan = P.plan_partition(sizes, cost, 8)
+    times, counts = [], []
+    for r in range(8):
+        pop, _ = shard_population(T, plan, r)
+        batch = engine.upload_agents(pop.cols, pop.n_scratch, order=profile_order(pop.cols))
+        out = engine.alloc_outputs(batch.n, hourly=True)
+        co = engine.c_outputs(out)
+        engine.size(batch, out, co)
+        torch.cuda.synchronize()
+        engine.kernel_times()
+        for _ in range(3):
+            engine.size(batch, out, co)
+        torch.cuda.synchronize()
+        ks, kh, kf, cnt = engine.kernel_times()
+        times.append(ks + kh + kf)
+        counts.append(batch.n)
+        del batch, out, co
+        torch.cuda.empty_cache()
+    t = np.asarray(times)
+    print(f"\nrank shards: agents {counts}, device ms {np.round(t, 2).tolist()}, "
+          f"predicted max/mean {plan.imbalance():.3f}, measured max/mean {t.max() / t.mean():.3f}, "
+          f"split states {[STATES[s] for s in plan.split_states()]}")
+    assert t.max() / t.mean() <= 1.15

@@ -340,3 +340,36 @@ def test_hourly_replan_matches_oracle(engine_hourly_plan, cfg, n):
             moved += not np.allclose(daily[i]["adopter_net_hourly_with_batt"], ref_h)
     assert moved > 0                 # the re-plan interval changes the dispatch
     assert last_eval <= 1, last_eval
+
+
+def test_battery_case_independent_of_batch(engine):
+    """The battery case's net-billing split is built in the scan for every
+    agent that bills net without a TS sell rate (decided per agent, not per
+    batch): an agent's battery-case outputs are bit-identical whether it is
+    sized in the national batch, in a batch of its own state's (CA) agents or
+    alone."""
+    from dgen_amd.engine import profile_order
+    pop = _small_pop("national_mixed", 1500)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    keys = ("npv_pv_batt", "bill_w_batt", "bill_wo_batt", "cfev_batt", "npv", "system_kw", "batt_kwh")
+
+    def run(idx):
+        cols = {k: np.asarray(v)[idx] for k, v in pop.cols.items()}
+        batch = engine.upload_agents(cols, order=profile_order(cols))
+        out = engine.alloc_outputs(batch.n, hourly=False)
+        engine.size(batch, out)
+        torch.cuda.synchronize()
+        return outputs_to_host(out, batch.perm)
+
+    ca = np.flatnonzero((pop.cols["flags"] & 2) != 0)
+    assert ca.size >= 20
+    full = run(np.arange(1500))
+    part = run(ca)
+    for k in keys:
+        assert np.array_equal(full[k][ca], part[k], equal_nan=True), k
+    for j in list(ca[:4]) + [int(np.flatnonzero((pop.cols["flags"] & 2) == 0)[0])]:
+        one = run(np.array([j]))
+        for k in keys:
+            assert np.array_equal(full[k][j], one[k][0], equal_nan=True), (j, k)

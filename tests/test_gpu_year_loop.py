@@ -201,3 +201,54 @@ def test_lifetime_raised_by_year_table_reaches_the_kernels(engine):
     # year 40's cash flow is live, year 41's is not
     cf = loop.out["cash_flow"].cpu().numpy()
     assert np.abs(cf[:, 40]).max() > 0 and not cf[:, 41:].any()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_state_shards_reproduce_one_pool(engine, world):
+    """States cut across ranks (partition.plan_partition with cuts inside
+    states): the shards run in lockstep on this GPU, their exchanges summed as
+    the all-reduce would (year_loop.run_lockstep), and reproduce the one-pool
+    loop bit for bit -- per-agent diffusion and battery allocation (split
+    (state, sector) groups allocated whole from the gather), the first year's
+    initial market, per-state totals and 8760-h rows (chunk partials summed in
+    chunk order)."""
+    from dgen_amd import partition as P
+    from dgen_amd.synth import national_tables, shard_population, split_state_members
+    from dgen_amd.year_loop import run_lockstep
+    T = national_tables(n_res_shapes=64, n_com_shapes=32, n_cf=32, n_counties=16, n_tariffs=48)
+    engine.load_profiles(T.shapes, T.cfs, T.wholesale)
+    engine.set_tariffs(T.tt.array())
+    engine.set_switches(T.switches)
+    tabs = LoopTables.synthetic()
+    sizes = P.census_sizes(3000)
+    chunk = 64
+    cost = np.ones(sizes.size)
+    cost[STATES.index("CA")] = 40.0                      # cuts inside CA (and others)
+    plan = P.plan_partition(sizes, cost, world, chunk=chunk, tol=0.0)
+    assert plan.split_states()
+    whole = P.whole_plan(sizes, chunk=chunk)
+    pop1, ag1 = shard_population(T, whole, 0)
+    one = YearLoop(engine, pop1, ag1, tabs, first_year=2026, hourly_export=True, plan=whole)
+    secs, ids = split_state_members("national_mixed", plan)
+    shards = []
+    for r in range(world):
+        pop, ag = shard_population(T, plan, r)
+        sg = P.split_groups(plan, r, secs, ids)
+        shards.append((ag, YearLoop(engine, pop, ag, tabs, first_year=2026, hourly_export=True, plan=plan,
+                                    split=sg)))
+    keys = ("market_share", "number_of_adopters", "system_kw_cum", "added", "batt_kw_cum", "batt_kwh_cum",
+            "market_share_last_year_in", "adopters_cum_last_year_in", "system_kw_cum_last_year_in")
+    ref_id = ag1["agent_id"][one.perm]
+    for y in (2026, 2027, 2028):
+        ref = one.run_year(y, keep_per_agent=True)
+        res = run_lockstep([lp for _, lp in shards], y, keep_per_agent=True)
+        pos = {int(a): i for i, a in enumerate(ref_id)}
+        for (ag, lp), r in zip(shards, res):
+            assert torch.equal(r.totals, ref.totals), (y, "totals")
+            assert torch.equal(r.hourly, ref.hourly), (y, "hourly")
+            ix = np.array([pos[int(a)] for a in ag["agent_id"][lp.perm]])
+            for k in keys:
+                a = r.per_agent[k].cpu().numpy()
+                b = ref.per_agent[k].cpu().numpy()[ix]
+                assert np.array_equal(a, b), (y, k)
+        assert ref.per_agent["added"].sum() > 0
