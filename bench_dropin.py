@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--also", default="array",
                     help="comma-separated other hourly forms timed beside it (reported, not the value)")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--no-device-export", dest="device_export", action="store_false",
+                    help="skip the hourly=\"device\" run (planes reduced per state on the device)")
     ap.add_argument("--rowwise-agents", type=int, default=5_000,
                     help="frame size for the row-by-row comparison (0: skip)")
     args = ap.parse_args()
@@ -73,15 +75,43 @@ def main():
 
     import numpy as np
     best = timed(args.hourly)
-    res = {"metric": "drop-in size_chunk agents/s (reference-schema frame -> sized frame, end to end)",
-           "value": args.agents / best["total_s"], "unit": "agents/s", "higher_is_better": True,
+    # value: the frame with its hourly cells readable on the host (the lazy
+    # mode's planes landed); the lazy return alone is a secondary field
+    on_host = best.get("planes_on_host_after_s", best["total_s"])
+    res = {"metric": "drop-in size_chunk agents/s (reference-schema frame -> sized frame with the hourly "
+                     "planes on the host, end to end)",
+           "value": args.agents / on_host, "unit": "agents/s", "higher_is_better": True,
+           "agents_per_s_frame_returned": args.agents / best["total_s"],
            "config": {"agents": args.agents, "hourly": args.hourly, "reps": args.reps,
                       "frame": "dgen_amd.synth.reference_frame (synthetic, reference schema)",
                       "hourly_planes": "float64, 3 x 8760 x 8 B per agent over PCIe"},
            "phases_s": {k: round(v, 4) for k, v in best.items()},
            "device_share": best["device_s"] / best["total_s"]}
-    if "planes_on_host_after_s" in best:
-        res["agents_per_s_planes_on_host"] = args.agents / best["planes_on_host_after_s"]
+    # the planes reduced on the device instead (hourly="device"): size_chunk +
+    # the per-state export of the sized frame, no plane crosses PCIe
+    if args.device_export:
+        from dgen_amd import attachment as ga
+        rng = np.random.default_rng(4)
+        runs = []
+        for _ in range(args.reps):
+            tm = {}
+            t0 = time.perf_counter()
+            out, agg = ff.size_chunk(df, None, table, hourly="device", timing=tm)
+            t1 = time.perf_counter()
+            out["customers_in_bin"] = rng.uniform(10, 400, len(out))
+            out["number_of_adopters"] = rng.uniform(0, 20, len(out))
+            out["batt_kw_cum_last_year"] = 0.0
+            out["batt_adopters_added_this_year"] = rng.integers(0, 3, len(out))
+            t2 = time.perf_counter()
+            rec = ga.export_state_hourly_with_storage_mix("eng", "s", "o", 2027, out)
+            t3 = time.perf_counter()
+            runs.append({"size_chunk_s": t1 - t0, "export_s": t3 - t2, "total_s": (t1 - t0) + (t3 - t2),
+                         "states": len(rec)})
+            del out
+        b = min(runs, key=lambda r: r["total_s"])
+        res["device_mode"] = {"agents_per_s_sized_and_exported": args.agents / b["total_s"],
+                              "phases_s": {k: round(v, 4) if isinstance(v, float) else v for k, v in b.items()},
+                              "note": "hourly planes reduced per state on the device; no plane crosses PCIe"}
     for mode in [m for m in args.also.split(",") if m and m != args.hourly]:
         b2 = timed(mode)
         res[f"{mode}_mode"] = {"agents_per_s": args.agents / b2["total_s"],

@@ -43,7 +43,9 @@ class Cfg(ctypes.Structure):
         ("itc_fed_max", _f64), ("depr_sl_years", _i32), ("pad0", _i32),
         ("batt_v_nom", _f64), ("batt_q_full", _f64), ("batt_min_soc", _f64),
         ("batt_max_soc", _f64), ("batt_init_soc", _f64), ("batt_eta_in", _f64),
-        ("batt_eta_out", _f64), ("batt_update_hours", _i32), ("pad1", _i32),
+        ("batt_eta_out", _f64), ("batt_update_hours", _i32), ("batt_loss_model", _i32),
+        ("batt_r_cell", _f64), ("batt_conv_eff", _f64), ("batt_v_cell_empty", _f64),
+        ("batt_v_cell_full", _f64),
     ]
 
 

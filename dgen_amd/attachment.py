@@ -235,6 +235,30 @@ def _len_safe(x) -> int:
         return 0
 
 
+NH_FULL = 8760
+
+
+def _device_planes(df):
+    """((baseline, pvonly, with_batt) tiled device planes, device column of
+    each frame row) when the frame's three hourly columns are full-width rows
+    of DevicePlanes of one sizing call (size_frame(hourly="device")), else None."""
+    from .engine import DevicePlane
+    from .hourly_column import RowColumn
+    arrs = [df[c].array for c in HOURLY_COLS]
+    if not all(isinstance(a, RowColumn) and isinstance(a._plane, DevicePlane) and a._lens is None
+               for a in arrs):
+        return None
+    p0 = arrs[0]._plane
+    if any(a._plane.t.shape != p0.t.shape or a._plane.t.device != p0.t.device or
+           not np.array_equal(a._idx, arrs[0]._idx) for a in arrs):
+        return None
+    if any((a._plane.inv is None) != (p0.inv is None) or
+           (a._plane.inv is not None and not bool((a._plane.inv == p0.inv).all())) for a in arrs):
+        return None
+    cols = p0.device_columns()[arrs[0]._idx]
+    return tuple(a._plane.t for a in arrs), cols
+
+
 def export_state_hourly_with_storage_mix(engine, schema, owner, year: int,
                                          solar_agents_df: pd.DataFrame,
                                          writer: Optional[Callable] = None, dev_engine=None):
@@ -251,8 +275,12 @@ def export_state_hourly_with_storage_mix(engine, schema, owner, year: int,
     df = solar_agents_df
     n = len(df)
     idx, seg_off, states = group_segments(df['state_abbr'].tolist())
-    lens = np.stack([df[c].map(_len_safe).to_numpy(np.int64) for c in HOURLY_COLS]) if n else \
-        np.zeros((3, 0), np.int64)
+    from .hourly_column import RowColumn
+
+    def cell_lens(c):          # series columns know their cells' lengths without reading them
+        a = df[c].array
+        return a.cell_lens() if isinstance(a, RowColumn) else df[c].map(_len_safe).to_numpy(np.int64)
+    lens = np.stack([cell_lens(c) for c in HOURLY_COLS]) if n else np.zeros((3, 0), np.int64)
     if not states:
         return None
     nh_state = []
@@ -276,7 +304,24 @@ def export_state_hourly_with_storage_mix(engine, schema, owner, year: int,
     w = export_weights(eng, col('customers_in_bin'), col('number_of_adopters'),
                        col('batt_kw_cum_last_year'), col('batt_kw'), added)
     out_rows = [None] * len(states)
-    for nh in sorted(set(nh_state)):
+    dev = _device_planes(df)
+    if dev is not None and all(nh == NH_FULL for nh in nh_state):
+        # size_frame(hourly="device"): the three planes are still in HBM, full
+        # rows -- the same sums in the same member order straight from the
+        # tiles (the cells' values are these planes' entries), no PCIe
+        planes, dcol = dev
+        ncol = planes[0].shape[1]
+        wd = []
+        cols_t = torch.as_tensor(dcol, device=eng.dev)
+        for x in w:
+            z = torch.zeros(ncol, dtype=torch.float64, device=eng.dev)
+            z.index_copy_(0, cols_t, x)
+            wd.append(z)
+        res = state_hourly(eng, planes, tuple(wd), dcol[idx], seg_off).cpu().numpy()
+        for s_ in range(len(states)):
+            out_rows[s_] = res[s_]
+        nh_state = [NH_FULL] * len(states)
+    for nh in (sorted(set(nh_state)) if dev is None or out_rows[0] is None else []):
         sids = [s for s in range(len(states)) if nh_state[s] == nh]
         members = np.concatenate([idx[seg_off[s]:seg_off[s + 1]] for s in sids])
         so = np.concatenate([[0], np.cumsum([seg_off[s + 1] - seg_off[s] for s in sids])])

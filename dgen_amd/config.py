@@ -34,10 +34,20 @@ class EngineConfig:
     batt_update_hours: int = 24         # peak-shaving re-plan interval (24: a 24-h plan
                                         # per calendar day; 1: re-planned every hour,
                                         # bdh:86-87 read literally)
+    # Li-ion loss model (batt_loss_model = 1; default 0 = the constant
+    # efficiencies above).  SSC's battery runs a voltage model, converter
+    # efficiencies and cell losses (batt_chem = 1, ff:134); restated as
+    # converters each way + cell I^2 R with an open-circuit voltage linear in
+    # SOC.  Values are recalled SAM Li-ion NMC defaults, unverifiable offline.
+    batt_loss_model: int = 0
+    batt_r_cell: float = 0.001          # ohm     cell internal resistance
+    batt_conv_eff: float = 0.96         #         AC-DC / DC-AC converter efficiency
+    batt_v_cell_empty: float = 3.0      # V       open-circuit voltage at SOC 0
+    batt_v_cell_full: float = 4.2       # V       open-circuit voltage at SOC 1
 
     def to_c(self) -> _lib.Cfg:
         d = asdict(self)
-        return _lib.Cfg(pad0=0, pad1=0, **d)
+        return _lib.Cfg(pad0=0, **d)
 
     def oracle_kwargs(self) -> dict:
         d = asdict(self)

@@ -728,6 +728,42 @@ __device__ __forceinline__ HourStep batt_hour(double nn, double pv, double targe
     return r;
 }
 
+// The same hour under the Li-ion loss model (dgen_cfg.batt_loss_model = 1;
+// the oracle's orc_batt_dispatch loss branch, operation for operation):
+// converters of efficiency eta each way and the cells' I^2 R at the bank's
+// open-circuit voltage, k = r q v_nom / (bank v(soc)^2) at the hour's
+// starting SOC (rqv = (r q) v_nom); the limits are the quadratics' roots.
+__device__ __forceinline__ HourStep batt_hour_loss(double nn, double pv, double target, double power,
+                                                   double bank, double& soc, const dgen_cfg& cfg,
+                                                   double rqv, double eta) {
+    const double v = cfg.batt_v_cell_empty + (cfg.batt_v_cell_full - cfg.batt_v_cell_empty) * soc;
+    const double k = rqv / (bank * (v * v));
+    HourStep r;
+    if (nn < 0.0) {
+        const double e_room = fmax((cfg.batt_max_soc - soc) * bank, 0.0);
+        const double disc = 1.0 - 4.0 * k * e_room;
+        const double x_max = disc > 0.0 ? 2.0 * e_room / (1.0 + sqrt(disc)) : 0.5 / k;
+        double c = -nn;
+        if (c > power) c = power;
+        if (c > x_max / eta) c = x_max / eta;
+        const double x = c * eta;
+        soc = soc + (x - k * (x * x)) / bank;
+        r.sys = pv - c;
+        r.g2l = 0.0;
+    } else {
+        const double e_av = fmax((soc - cfg.batt_min_soc) * bank, 0.0);
+        const double y_max = 2.0 * e_av / (1.0 + sqrt(1.0 + 4.0 * k * e_av));
+        double d = nn - target;
+        if (d < 0.0) d = 0.0;
+        if (d > power) d = power;
+        if (d > y_max * eta) d = y_max * eta;
+        const double y = d / eta;
+        soc = soc - (y + k * (y * y)) / bank;
+        r.sys = pv + d;
+        r.g2l = nn - d;
+    }
+    return r;
+}
 
 // 16 B per lane global -> LDS at lds + lane * 16 (m0 = wave-uniform base)
 __device__ __forceinline__ void lds_dma16(const void* g, uint32_t lds) {
@@ -834,7 +870,10 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 // DCR: the batch bills demand charges (or kWh/kW tier peaks) and has room for
 // the battery-case demand records (dcr: DCR_BYTES per scratch slot, dc_nq the
 // batch's demand periods, which size the scan's per-period LDS maxima).
-template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR>
+// LOSS: the Li-ion loss model (dgen_cfg.batt_loss_model = 1, batt_hour_loss);
+// instantiated without the scan-built records (NB, DCR), whose finance
+// kernels then take the plane passes (equal results).
+template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR, bool LOSS = false>
 __global__ void __launch_bounds__(BLOCK, ROLL ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
@@ -963,6 +1002,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const double out_per_bank = bank > 0.0 ? 1.0 / (cfg.batt_eta_out * bank) : 0.0;
     const bool has_batt = bank > 0.0;
     if (!has_batt) power = 0.0;
+    const double rqv = LOSS ? cfg.batt_r_cell * cfg.batt_q_full * cfg.batt_v_nom : 0.0;   // loss model: r q v_nom
     double soc = m_lo == 0 ? cfg.batt_init_soc : W.carry[i];
     double annual = m_lo == 0 ? 0.0 : W.carry[n + i];
     const int d_lo = c_month_start_day[m_lo];
@@ -1098,7 +1138,10 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 for (int hh = 0; hh < 24; hh++)
                     dv[hh] = fmax((double)r.s[hh] * ls - (double)r.c[hh] * cs6, 0.0);
                 sort24_desc(dv);
-                const double avail = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
+                // deliverable energy of the plan (the loss model's without the
+                // cell losses: the oracle's e_av x eta)
+                const double avail = LOSS ? fmax((soc - cfg.batt_min_soc) * bank, 0.0) * cfg.batt_conv_eff
+                                          : fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
 #if DGEN_PHASE_PROF && DGEN_DAY_COUNTERS
                 int its = 0;
                 target = day_target_sorted(dv, power, avail, &its);
@@ -1136,7 +1179,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     // this hour's plan over hours h .. h + 23, from the energy
                     // stored now; only an hour that can discharge needs one
                     // (elsewhere the dispatch is the same for any target)
-                    const double av = fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
+                    const double av = LOSS ? fmax((soc - cfg.batt_min_soc) * bank, 0.0) * cfg.batt_conv_eff
+                                           : fmax((soc - cfg.batt_min_soc) * bank * cfg.batt_eta_out, 0.0);
                     const bool need = has_batt && nn > 0.0 && av > 0.0;
                     target = 0.0;
                     if (__ballot(need)) {
@@ -1148,8 +1192,13 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                         target = need ? t : 0.0;
                     }
                 }
-                HourStep st = batt_hour(nn, pv, target, power, bank, soc, cfg, inv_eta_in,
-                                        in_per_bank, out_per_bank);
+                HourStep st;
+                if constexpr (LOSS) {
+                    if (has_batt) st = batt_hour_loss(nn, pv, target, power, bank, soc, cfg, rqv, cfg.batt_conv_eff);
+                    else { st.sys = pv; st.g2l = fmax(nn, 0.0); }
+                } else {
+                    st = batt_hour(nn, pv, target, power, bank, soc, cfg, inv_eta_in, in_per_bank, out_per_bank);
+                }
                 if constexpr (ROLL) {   // the window moves on: tomorrow's hour hh comes in
                     float ts;
                     int32_t tc;
@@ -4328,6 +4377,16 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
         set_err("dgen_open: invalid battery/loan configuration");
         return DGEN_E_ARG;
     }
+    if (cfg->batt_loss_model != 0 && cfg->batt_loss_model != 1) {
+        set_err("dgen_open: batt_loss_model must be 0 (constant efficiencies) or 1 (Li-ion loss model)");
+        return DGEN_E_ARG;
+    }
+    if (cfg->batt_loss_model == 1 &&
+        (!(cfg->batt_r_cell >= 0.0) || !(cfg->batt_conv_eff > 0.0 && cfg->batt_conv_eff <= 1.0) ||
+         !(cfg->batt_v_cell_empty > 0.0) || !(cfg->batt_v_cell_full > 0.0))) {
+        set_err("dgen_open: loss model needs batt_r_cell >= 0, 0 < batt_conv_eff <= 1 and positive cell voltages");
+        return DGEN_E_ARG;
+    }
     if (cfg->batt_update_hours != 24 && cfg->batt_update_hours != 1) {
         set_err("dgen_open: batt_update_hours must be 24 (a plan per day) or 1 (re-planned every hour)");
         return DGEN_E_ARG;
@@ -4510,7 +4569,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // scratch slot, context-owned; their per-period maxima add [dc_nq][BLOCK]
     // double2 to the scan's LDS
     const int dc_nq = (T->max_dc_periods > 0 && T->max_dc_periods <= DCP) ? T->max_dc_periods : DCP;
-    bool dcr_on = dc && n_scratch > 0 && c->battery && c->cfg.batt_update_hours != 1 && c->dcr_enable;
+    // the Li-ion loss model's scan has no record forms: its batches bill from the planes
+    const bool loss = c->cfg.batt_loss_model == 1;
+    bool dcr_on = dc && n_scratch > 0 && c->battery && c->cfg.batt_update_hours != 1 && c->dcr_enable && !loss;
     if (dcr_on && (size_t)n_scratch * DCR_BYTES > c->dcr_cap) {
         if (c->dcr_buf) HIP_TRY(hipFree(c->dcr_buf));
         c->dcr_buf = nullptr;
@@ -4527,7 +4588,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     const size_t lds_dcr = dcr_on ? (size_t)16 * dc_nq * BLOCK : 0;
     const size_t lds_nb = sizeof(double) * 4 * (size_t)lds_half(T->max_periods) * BLOCK + lds_dcr +
                           (size_t)(BLOCK / 64) * HB_DAY_BYTES;
-    const bool nb_scan = n_scratch > 0 && c->nb_scan && c->battery && lds_nb <= 65536;
+    const bool nb_scan = n_scratch > 0 && c->nb_scan && c->battery && lds_nb <= 65536 && !loss;
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK * (nb_scan ? 2 : 1) +
                        lds_dcr + (size_t)(BLOCK / 64) * HB_DAY_BYTES;
     const int rep_mask = (nb_scan ? 1 : 0) | (dcr_on ? 2 : 0);
@@ -4616,9 +4677,14 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                                c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? rep_mask : 0, \
                                (REP) ? dcr : nullptr, 0, 0);                                                               \
     } while (0)
+#define DGEN_HB_LAUNCH_LOSS(H, F, R)                                                              \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false, R, false, true>), grid, block, lds, s2, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, 0, nullptr, 0, 0)
 #define DGEN_HB_LAUNCH(H, F, REP)                                                                 \
     do {                                                                                          \
-        if (c->cfg.batt_update_hours == 1) DGEN_HB_LAUNCH_R(H, F, REP, true);                     \
+        if (loss && c->cfg.batt_update_hours == 1) DGEN_HB_LAUNCH_LOSS(H, F, true);              \
+        else if (loss) DGEN_HB_LAUNCH_LOSS(H, F, false);                                          \
+        else if (c->cfg.batt_update_hours == 1) DGEN_HB_LAUNCH_R(H, F, REP, true);                \
         else DGEN_HB_LAUNCH_R(H, F, REP, false);                                                  \
     } while (0)
             if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, false);
@@ -4634,6 +4700,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             else DGEN_HB_LAUNCH(false, false, true);
 #undef DGEN_HB_LAUNCH
 #undef DGEN_HB_LAUNCH_R
+#undef DGEN_HB_LAUNCH_LOSS
         }
         HIP_TRY(hipEventRecord(e[3], s2));
         if (!c->battery) {
@@ -4713,11 +4780,16 @@ int32_t dgen_hourly_planes(dgen_ctx* c, const dgen_tables* T, const dgen_agents*
     const bool roll = c->cfg.batt_update_hours == 1;
     for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
         const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
-#define DGEN_HP_LAUNCH(F, R)                                                                       \
-        hipLaunchKernelGGL((k_hourly_batt<true, F, false, R, false>), grid, block, lds, s, *T, *A, *O, c->cfg, \
+#define DGEN_HP_LAUNCH(F, R, L)                                                                    \
+        hipLaunchKernelGGL((k_hourly_batt<true, F, false, R, false, L>), grid, block, lds, s, *T, *A, *O, c->cfg, \
                            n, ws, n_scratch, (int64_t)0, n, m0, m1, c->battery, 0, 0, nullptr, 0, 0)
-        if (O->hourly_f64) { if (roll) DGEN_HP_LAUNCH(true, true); else DGEN_HP_LAUNCH(true, false); }
-        else { if (roll) DGEN_HP_LAUNCH(false, true); else DGEN_HP_LAUNCH(false, false); }
+        if (c->cfg.batt_loss_model == 1) {
+            if (O->hourly_f64) { if (roll) DGEN_HP_LAUNCH(true, true, true); else DGEN_HP_LAUNCH(true, false, true); }
+            else { if (roll) DGEN_HP_LAUNCH(false, true, true); else DGEN_HP_LAUNCH(false, false, true); }
+        } else {
+            if (O->hourly_f64) { if (roll) DGEN_HP_LAUNCH(true, true, false); else DGEN_HP_LAUNCH(true, false, false); }
+            else { if (roll) DGEN_HP_LAUNCH(false, true, false); else DGEN_HP_LAUNCH(false, false, false); }
+        }
 #undef DGEN_HP_LAUNCH
     }
     HIP_TRY(hipGetLastError());

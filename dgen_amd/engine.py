@@ -251,12 +251,27 @@ class Engine:
         the hourly scan for every agent that bills net without a TS sell rate
         (the scan decides per agent; profile_order groups those agents into
         their own waves), so an agent's battery-case outputs do not depend on
-        the batch it is sized in.  DGEN_NB_SCAN=0 turns it off (A/B: the
-        finance kernel's build over the system-output plane; the two builds
-        re-associate the split's sums, ~1e-9 relative on the battery-case
-        bills and NPV)."""
+        the batch it is sized in.  The scan form is compiled in only when the
+        batch holds such an agent (its instantiation carries the export sums:
+        more registers, and with the demand records a spill), which changes no
+        result.  DGEN_NB_SCAN=0 turns it off (A/B: the finance kernel's build
+        over the system-output plane; the two builds re-associate the split's
+        sums, ~1e-9 relative on the battery-case bills and NPV)."""
         import os
-        return os.environ.get("DGEN_NB_SCAN", "1") != "0"
+        if os.environ.get("DGEN_NB_SCAN", "1") == "0":
+            return False
+        mo_t = getattr(self, "_tariff_mo", None)
+        if n == 0 or n_scratch == 0 or mo_t is None:
+            return n_scratch > 0
+        try:
+            sl = np.asarray(cols["scratch_slot"])
+            mo = mo_t[np.asarray(cols["tariff0"], np.int64)]
+            ts = (mo == 2) & ((np.asarray(cols["flags"]) & 2) == 0) & (np.asarray(cols["wholesale_row"]) >= 0)
+        except Exception:          # device-tensor columns: keep it on
+            return True
+        if not self.tables.wholesale:
+            ts[:] = False
+        return bool(((sl >= 0) & ((mo == 2) | (mo == 3)) & ~ts).any())
 
     def validate_agents(self, dev, n):
         """Host-side bounds checks before any kernel indexes a table."""
@@ -562,14 +577,44 @@ class HostPlane:
         return self._arr is not None or self._fut.done()
 
 
+class DevicePlane:
+    """An hourly plane left in HBM (size_frame(hourly="device")): consumers
+    that reduce it on the device (attachment.export_state_hourly_with_storage
+    _mix) read the tiled tensor in place and it never crosses PCIe; reading a
+    cell downloads the whole plane once (result(), like HostPlane's).  Row j
+    of the [n][8760] view is device column inv[j] (inv None: j)."""
+
+    def __init__(self, t, inv):
+        self.t = t
+        self.inv = inv
+        self.n = int(t.shape[1])
+        self.width = int(t.shape[0]) * int(t.shape[2])      # hours per row, known without a download
+        self._arr = None
+
+    def device_columns(self) -> np.ndarray:
+        """Device column of each plane row (host int64)."""
+        return (np.arange(self.n, dtype=np.int64) if self.inv is None
+                else self.inv.cpu().numpy().astype(np.int64))
+
+    def result(self) -> np.ndarray:
+        if self._arr is None:
+            self._arr = hourly_to_host(self.t, self.inv)
+        return self._arr
+
+    def done(self) -> bool:
+        return self._arr is not None
+
+
 def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None,
-                    hourly_async: bool = False) -> Dict[str, object]:
+                    hourly_async: bool = False, hourly_device: bool = False) -> Dict[str, object]:
     """Device outputs -> host numpy ([agent][year] yearly arrays, [agent][hour] hourly),
     in caller order when `perm` (AgentBatch.perm) is given.  The reorder to
     caller order (and the hourly tiles' transpose) is one device gather per
     array, so each crosses PCIe once, already in its final layout.
     hourly_async: the hourly planes come back as HostPlane (background
-    download) instead of arrays, the scalars and yearly arrays at once."""
+    download) instead of arrays, the scalars and yearly arrays at once;
+    hourly_device: as DevicePlane (kept in HBM, downloaded only if a cell is
+    read)."""
     torch = _torch()
     res = {}
     inv = None
@@ -588,6 +633,8 @@ def outputs_to_host(out: Dict[str, object], perm: Optional[np.ndarray] = None,
         t = out.get(name)
         if t is None:
             res[name] = None
+        elif hourly_device:
+            res[name] = DevicePlane(t, inv)
         elif hourly_async:
             res[name] = HostPlane(t, inv)
         elif t.shape[1] >= 16384:         # large planes: pinned, chunked, threaded

@@ -159,7 +159,8 @@ def _device_tables(eng, src: ProfileStore, b: PopulationBuilder):
 
 
 def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[dict] = None,
-                net_weights: Optional[Tuple[np.ndarray, np.ndarray]] = None, hourly_async: bool = False):
+                net_weights: Optional[Tuple[np.ndarray, np.ndarray]] = None, hourly_async: bool = False,
+                hourly_device: bool = False):
     """Size the batch; net_weights = (number_of_adopters, non-adopters) per
     caller row also returns o["net_sum_kw"], size_chunk's hourly aggregate
     summed on the device from the planes in place (k_state_hourly, one
@@ -189,7 +190,7 @@ def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[
                            [0, batch.n])[0] * 1000.0
     torch.cuda.synchronize(eng.dev)
     t2 = time.perf_counter()
-    o = outputs_to_host(out, batch.perm, hourly_async=hourly_async)
+    o = outputs_to_host(out, batch.perm, hourly_async=hourly_async, hourly_device=hourly_device)
     del out
     unsized = (o["status"] & _lib.ST_UNIT) != 0
     if unsized.any():          # kWh/kW tiers without month peaks: every sizing output NaN
@@ -321,7 +322,9 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
     waits for it), a yearly cell the agent's Python list, made when read; the
     reference's consumers read hourly cells with len() and np.asarray,
     attachment_rate_functions.py:166-182, and yearly cells as lists,
-    finance_series_export.py:51-64), "array" (the planes on the host before
+    finance_series_export.py:51-64), "device" (as lazy, but the hourly planes
+    stay in HBM: attachment.export_state_hourly_with_storage_mix reduces them
+    there and they never cross PCIe unless a cell is read), "array" (the planes on the host before
     returning: hourly and yearly cells float64 row views -- the reference's
     own finance export skips non-list cells), "list" (the reference's fp64
     lists throughout) or "none" (no hourly columns, yearly lists).  The device
@@ -338,7 +341,8 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
     cols = b.frame_columns
     t1 = time.perf_counter()
     dev_t: dict = {}
-    o = _run_device(b, cols, src, dev_t, net_weights, hourly_async=hourly != "none")
+    o = _run_device(b, cols, src, dev_t, net_weights, hourly_async=hourly in ("lazy", "array", "list"),
+                    hourly_device=hourly == "device")
     t2 = time.perf_counter()
     ids = df["agent_id"].tolist() if "agent_id" in df else list(df.index)
     _raise_for_status(o["status"], ids)
@@ -347,7 +351,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
         out.insert(len(out.columns), "agent_id", list(df.index))
     n1 = df["economic_lifetime_yrs"].astype(np.int64).to_numpy() + 1
     from .hourly_column import hourly_column, yearly_column
-    if hourly == "lazy":
+    if hourly in ("lazy", "device"):
         def ycol(a):     # O(1): lists made when a cell is read
             return pd.Series(yearly_column(a, n1), index=out.index, copy=False)
     else:
@@ -383,7 +387,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
     if hourly != "none":
         def conv(plane):
             nonlocal t_wait
-            if hourly == "lazy":
+            if hourly in ("lazy", "device"):
                 # O(1): the column is the plane and its row index
                 return pd.Series(hourly_column(plane), index=out.index, copy=False)
             tw = time.perf_counter()

@@ -93,7 +93,15 @@ typedef struct {
                                    /* plan per calendar day (SSC's BTM peak-shaving */
                                    /* update), 1 = a 24-h look-ahead plan every     */
                                    /* hour (bdh:86-87 read literally); DESIGN.md 3  */
-    int32_t pad1;
+    int32_t batt_loss_model;       /* 0: constant efficiencies batt_eta_in / _out   */
+                                   /* (default); 1: Li-ion loss model (ABI 9):      */
+                                   /* converters batt_conv_eff each way + cell I^2 R */
+                                   /* with an open-circuit voltage linear in SOC     */
+                                   /* (parameters are guesses)  */
+    double  batt_r_cell;           /* cell internal resistance (ohm)                */
+    double  batt_conv_eff;         /* AC-DC and DC-AC converter efficiency          */
+    double  batt_v_cell_empty;     /* cell open-circuit voltage at SOC 0 (V)        */
+    double  batt_v_cell_full;      /* cell open-circuit voltage at SOC 1 (V)        */
 } dgen_cfg;
 
 /* Compiled tariff = the Utilityrate5.ElectricityRates energy fields that

@@ -55,6 +55,8 @@ class Cfg(ctypes.Structure):
         ("batt_min_soc", _c_double), ("batt_max_soc", _c_double),
         ("batt_init_soc", _c_double), ("batt_eta_in", _c_double),
         ("batt_eta_out", _c_double), ("batt_update_hours", _c_int32),
+        ("batt_loss_model", _c_int32), ("batt_r_cell", _c_double), ("batt_conv_eff", _c_double),
+        ("batt_v_cell_empty", _c_double), ("batt_v_cell_full", _c_double),
     ]
 
 
@@ -114,6 +116,7 @@ DEFAULT_CFG = dict(
     nm_yearend_sell_rate=0.02, loan_rate_pct=7.5, insurance_rate_pct=0.0, itc_fed_max=1e38,
     depr_sl_years=7, batt_v_nom=3.6, batt_q_full=3.2, batt_min_soc=0.10, batt_max_soc=0.95,
     batt_init_soc=0.30, batt_eta_in=0.9408, batt_eta_out=0.9408, batt_update_hours=24,
+    batt_loss_model=0, batt_r_cell=0.001, batt_conv_eff=0.96, batt_v_cell_empty=3.0, batt_v_cell_full=4.2,
 )
 
 

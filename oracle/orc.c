@@ -541,6 +541,24 @@ static double day_target(const double* load, const double* pv, int h0, double po
  *       batt_dispatch_update_frequency_hours = 1).  A plan only matters in an
  *       hour that can discharge (net load > 0, energy stored > 0), so the
  *       hourly rule forms it only there; the result is the same.            */
+/* Li-ion loss model (cfg->batt_loss_model = 1): converters of efficiency
+ * batt_conv_eff each way, and the cells' I^2 R at the bank's open-circuit
+ * voltage.  With s cells in series and p strings (battery_model_sizing) the
+ * bank has V(soc) = s (v_e + (v_f - v_e) soc) and R = s r / p, so a DC power x
+ * (kW) loses k x^2 with k = 1000 R / V^2 = r q v_nom / (bank_kwh v(soc)^2)
+ * (s p = 1000 bank_kwh / (q v_nom)).  k is taken at the hour's starting SOC.
+ * Charging c kW (AC) stores x - k x^2, x = c eta; discharging d kW (AC) draws
+ * y + k y^2, y = d / eta.  The limits are the roots of those quadratics,
+ * in their cancellation-free forms:
+ *   room:  x_max = 2 E_room / (1 + sqrt(1 - 4 k E_room))  (x up to 1 / 2k)
+ *   avail: y_max = 2 E_av / (1 + sqrt(1 + 4 k E_av))
+ * The day's plan uses the deliverable energy without the cell losses,
+ * E_av eta (the per-hour limits are exact). */
+static double loss_k(const orc_cfg* cfg, double soc, double bank_kwh) {
+    const double v = cfg->batt_v_cell_empty + (cfg->batt_v_cell_full - cfg->batt_v_cell_empty) * soc;
+    return cfg->batt_r_cell * cfg->batt_q_full * cfg->batt_v_nom / (bank_kwh * (v * v));
+}
+
 void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, double power_kw,
                        const orc_cfg* cfg, double* sysgen, double* grid_to_load) {
     double soc = cfg->batt_init_soc;
@@ -550,11 +568,48 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
     const double inv_eta_in = 1.0 / cfg->batt_eta_in;
     const double in_per_bank = bank_kwh > 0.0 ? cfg->batt_eta_in / bank_kwh : 0.0;
     const double out_per_bank = bank_kwh > 0.0 ? 1.0 / (cfg->batt_eta_out * bank_kwh) : 0.0;
+    const int loss = cfg->batt_loss_model == 1;
+    const double eta = cfg->batt_conv_eff;
     for (int h = 0; h < ORC_NH; h++) {
         double n = load[h] - pv[h];
         if (!(bank_kwh > 0.0)) {
             sysgen[h] = pv[h];
             grid_to_load[h] = n > 0.0 ? n : 0.0;
+            continue;
+        }
+        if (loss) {
+            if (h % 24 == 0 || hourly) {
+                double e_av = (soc - cfg->batt_min_soc) * bank_kwh;
+                if (e_av < 0.0) e_av = 0.0;
+                if (!hourly) target = day_target(load, pv, h, power_kw, e_av * eta);
+                else target = (n > 0.0 && e_av > 0.0) ? day_target(load, pv, h, power_kw, e_av * eta) : 0.0;
+            }
+            const double k = loss_k(cfg, soc, bank_kwh);
+            if (n < 0.0) {
+                double e_room = (cfg->batt_max_soc - soc) * bank_kwh;
+                if (e_room < 0.0) e_room = 0.0;
+                const double disc = 1.0 - 4.0 * k * e_room;
+                const double x_max = disc > 0.0 ? 2.0 * e_room / (1.0 + sqrt(disc)) : 0.5 / k;
+                double c = -n;
+                if (c > power_kw) c = power_kw;
+                if (c > x_max / eta) c = x_max / eta;
+                const double x = c * eta;
+                soc = soc + (x - k * (x * x)) / bank_kwh;
+                sysgen[h] = pv[h] - c;
+                grid_to_load[h] = 0.0;
+            } else {
+                double e_av = (soc - cfg->batt_min_soc) * bank_kwh;
+                if (e_av < 0.0) e_av = 0.0;
+                const double y_max = 2.0 * e_av / (1.0 + sqrt(1.0 + 4.0 * k * e_av));
+                double d = n - target;
+                if (d < 0.0) d = 0.0;
+                if (d > power_kw) d = power_kw;
+                if (d > y_max * eta) d = y_max * eta;
+                const double y = d / eta;
+                soc = soc - (y + k * (y * y)) / bank_kwh;
+                sysgen[h] = pv[h] + d;
+                grid_to_load[h] = n - d;
+            }
             continue;
         }
         if (!hourly && h % 24 == 0) {

@@ -79,6 +79,11 @@ typedef struct {
     double batt_eta_in;            /* AC->stored efficiency                       */
     double batt_eta_out;           /* stored->AC efficiency                       */
     int32_t batt_update_hours;     /* 24: daily plan, 1: re-planned every hour    */
+    int32_t batt_loss_model;       /* 0: constant efficiencies, 1: Li-ion losses  */
+    double batt_r_cell;            /* cell internal resistance (ohm)              */
+    double batt_conv_eff;          /* converter efficiency each way               */
+    double batt_v_cell_empty;      /* open-circuit voltage at SOC 0 (V)           */
+    double batt_v_cell_full;       /* open-circuit voltage at SOC 1 (V)           */
 } orc_cfg;
 
 /* One row of the rate-switch table, already filtered to (tech, eia_id, res_com). */

@@ -153,3 +153,38 @@ def test_size_chunk_lazy_mode_equals_array_mode():
     for k in ARRAYS:
         for a, c in zip(arr[k], lz[k]):
             assert isinstance(c, list) and c == a.tolist(), k
+
+
+def test_device_mode_export_reduces_planes_in_place():
+    """size_chunk(hourly="device"): the hourly planes stay in HBM; the per-state
+    export (attachment.export_state_hourly_with_storage_mix) sums them there,
+    bit-identical to the export of the array mode's host cells, and the planes
+    never cross PCIe (until a cell is read: then they match the array mode)."""
+    from dgen_amd import attachment as ga
+    from dgen_amd.synth import reference_frame
+    df, store, table = reference_frame(3000)
+    ff._worker_conn = store
+    arr, _ = ff.size_chunk(df, None, table, "simple", hourly="array")
+    dv, _ = ff.size_chunk(df, None, table, "simple", hourly="device")
+    rng = np.random.default_rng(4)
+    extra = {"customers_in_bin": rng.uniform(10, 400, len(df)), "number_of_adopters": rng.uniform(0, 20, len(df)),
+             "batt_kw_cum_last_year": rng.uniform(0, 30, len(df)),
+             "batt_adopters_added_this_year": rng.integers(0, 3, len(df))}
+    recs = []
+    for frame in (arr, dv):
+        f = frame.copy()
+        for k, v in extra.items():
+            f[k] = v
+        f = f.iloc[::-1]                 # a reordered frame: rows map to their own device columns
+        recs.append(ga.export_state_hourly_with_storage_mix("eng", "s", "o", 2027, f))
+    planes = [dv[k].array._plane for k in ("baseline_net_hourly", "adopter_net_hourly_pvonly",
+                                           "adopter_net_hourly_with_batt")]
+    assert not any(p.done() for p in planes)                    # nothing downloaded
+    a, d = recs
+    assert a["state_abbr"].tolist() == d["state_abbr"].tolist()
+    assert a["n_hours"].tolist() == d["n_hours"].tolist()
+    for x, y in zip(a["net_sum"], d["net_sum"]):
+        assert np.array_equal(np.asarray(x), np.asarray(y))
+    j = len(df) // 2
+    assert np.array_equal(np.asarray(dv["adopter_net_hourly_with_batt"].iloc[j]),
+                          np.asarray(arr["adopter_net_hourly_with_batt"].iloc[j]))

@@ -373,3 +373,42 @@ def test_battery_case_independent_of_batch(engine):
         one = run(np.array([j]))
         for k in keys:
             assert np.array_equal(full[k][j], one[k][0], equal_nan=True), (j, k)
+
+
+@pytest.mark.parametrize("cfg,n,replan", [("ca_res_storage", 300, 24), ("national_mixed", 400, 24),
+                                          ("res_1m_nem_tou", 300, 1)])
+def test_li_ion_loss_model_matches_oracle(cfg, n, replan):
+    """The Li-ion loss model option (batt_loss_model = 1: converters + cell
+    I^2 R at an SOC-dependent open-circuit voltage) in
+    k_hourly_batt<LOSS> against the oracle's dispatch, with a resistance large
+    enough to move the dispatch."""
+    from dgen_amd.config import EngineConfig
+    from dgen_amd.engine import Engine
+    kw = dict(batt_loss_model=1, batt_r_cell=0.02, batt_update_hours=replan)
+    eng = Engine(0, EngineConfig(**kw))
+    try:
+        pop = _small_pop(cfg, n)
+        eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+        eng.set_tariffs(pop.tariffs)
+        eng.set_switches(pop.switches)
+        batch = eng.upload_agents(pop.cols, pop.n_scratch)
+        out = eng.alloc_outputs(batch.n, hourly=True)
+        eng.size(batch, out)
+        torch.cuda.synchronize()
+        o = outputs_to_host(out)
+    finally:
+        eng.close()
+    opop = helpers.oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs, pop.wholesale)
+    ref = opop.run(orc.make_cfg(**kw), hourly=True)
+    base = opop.run(orc.make_cfg(batt_update_hours=replan), hourly=True)
+    moved = 0
+    for i, (r, b) in enumerate(zip(ref, base)):
+        assert o["status"][i] == 0 and r["status"] == 0, i
+        for k in ("npv_pv_batt", "batt_kwh", "first_with", "npv"):
+            assert np.isclose(o[k][i], r[k], rtol=1e-6, atol=1e-6), (i, k, o[k][i], r[k])
+        N1 = int(pop.cols["econ_life"][i]) + 1
+        assert np.allclose(o["bill_w_batt"][i, :N1], r["bill_w_pv_batt"], rtol=1e-6, atol=1e-5), i
+        ref_h = r["adopter_net_hourly_with_batt"]
+        assert np.allclose(o["net_with_batt"][i], ref_h, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(ref_h).max())), i
+        moved += not np.allclose(ref_h, b["adopter_net_hourly_with_batt"], rtol=1e-9, atol=1e-9)
+    assert moved > 0

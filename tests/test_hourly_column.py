@@ -7,6 +7,7 @@ import pickle
 import threading
 
 import numpy as np
+import pytest
 import pandas as pd
 
 from dgen_amd.hourly_column import NH, RowDtype, hourly_column, yearly_column
@@ -124,3 +125,44 @@ def test_mixed_concat_materialises():
     cat = pd.concat([df[["baseline_net_hourly"]], y], ignore_index=True)
     assert np.array_equal(np.asarray(cat["baseline_net_hourly"].iloc[0]), a[0])
     assert list(cat["baseline_net_hourly"].iloc[8]) == [1.0, 1.0, 1.0]
+
+
+def test_cells_are_read_only_and_assignment_copies():
+    """Hourly cells are views of a plane shared by every reader: writing
+    through one fails; assigning through the frame gives the column its own
+    rows and leaves the plane (and other columns over it) unchanged."""
+    import pandas as pd
+    from dgen_amd.hourly_column import RowColumn, _Ready
+    a = np.arange(12, dtype=np.float64).reshape(3, 4)
+    col = RowColumn(_Ready(a))
+    other = RowColumn(_Ready(a))
+    cell = col[1]
+    with pytest.raises(ValueError):
+        cell[0] = 99.0
+    df = pd.DataFrame({"h": col, "g": other})
+    df.at[1, "h"] = np.full(4, -1.0)           # as with the reference's object cells
+    assert np.array_equal(np.asarray(df["h"].iloc[1]), np.full(4, -1.0))
+    assert np.array_equal(a[1], [4.0, 5.0, 6.0, 7.0])            # the shared plane is untouched
+    assert np.array_equal(np.asarray(df["g"].iloc[1]), [4.0, 5.0, 6.0, 7.0])
+
+
+def test_concat_of_different_planes_keeps_segments():
+    """pd.concat of chunk frames over different planes builds no dense copy:
+    cells read through to each chunk's plane; the 2-D view is made on demand."""
+    import pandas as pd
+    from dgen_amd.hourly_column import RowColumn, _Ready, _Segments
+    a = np.arange(8, dtype=np.float64).reshape(2, 4)
+    b = 100 + np.arange(12, dtype=np.float64).reshape(3, 4)
+    f = pd.concat([pd.DataFrame({"h": RowColumn(_Ready(a))}), pd.DataFrame({"h": RowColumn(_Ready(b))})],
+                  ignore_index=True)
+    col = f["h"].array
+    assert isinstance(col._plane, _Segments) and col._plane._dense is None
+    assert np.array_equal(np.asarray(f["h"].iloc[3]), b[1])
+    assert col._plane._dense is None
+    g = pd.concat([f, f.iloc[[0]]], ignore_index=True)
+    assert np.array_equal(np.asarray(g["h"].iloc[5]), a[0])
+    assert np.array_equal(g["h"].array.to_2d(), np.concatenate([a, b, a[:1]]))
+    y1 = RowColumn(_Ready(np.ones((2, 5))), None, [3, 5], lists=True)
+    y2 = RowColumn(_Ready(np.zeros((1, 2))), None, [2], lists=True)
+    yc = RowColumn._concat_same_type([y1, y2])
+    assert [len(c) for c in yc] == [3, 5, 2] and yc[2] == [0.0, 0.0]

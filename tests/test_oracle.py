@@ -309,3 +309,85 @@ def test_oracle_kwh_per_kw_tiers_known_answer(unit):
     assert r["bill_w"][1] == pytest.approx(bill(2.0), rel=1e-12)
     if unit in (1, 3):       # the lower peak shrank the cheap tier: the 3 kWh saved are not all
         assert bill(5.0) - r["bill_w"][1] < 12 * 3 * float(b2) - 1.0    # billed at the top rate
+
+
+# ---------------------------------------------------------------------------
+# Li-ion loss model option (batt_loss_model = 1): converters + cell I^2 R at an
+# open-circuit voltage linear in SOC (parity unpinned)
+# ---------------------------------------------------------------------------
+def _py_dispatch_loss(load, pv, bank, power, cfg):
+    """Direct restatement: SOC tracked in energy; the cell loss k x^2 with
+    k = r q v_nom / (bank v(soc)^2); limits by solving the quadratics with numpy."""
+    d = np.maximum(load - pv, 0.0)
+    soc, target, eta = cfg.batt_init_soc, 0.0, cfg.batt_conv_eff
+    sg, g2l = np.zeros(orc.NH), np.zeros(orc.NH)
+    for h in range(orc.NH):
+        n = load[h] - pv[h]
+        e_av = max((soc - cfg.batt_min_soc) * bank, 0.0)
+        if h % 24 == 0:
+            target = _py_target(d[h:h + 24], power, e_av * eta)
+        v = cfg.batt_v_cell_empty + (cfg.batt_v_cell_full - cfg.batt_v_cell_empty) * soc
+        k = cfg.batt_r_cell * cfg.batt_q_full * cfg.batt_v_nom / (bank * v * v)
+        if n < 0:
+            e_room = max((cfg.batt_max_soc - soc) * bank, 0.0)
+            roots = np.roots([k, -1.0, e_room])            # k x^2 - x + E = 0
+            x_max = min(r.real for r in roots if abs(r.imag) < 1e-12) if 1 - 4 * k * e_room > 0 else 0.5 / k
+            c = min(-n, power, x_max / eta)
+            x = c * eta
+            soc += (x - k * x * x) / bank
+            sg[h], g2l[h] = pv[h] - c, 0.0
+        else:
+            y_max = max(r.real for r in np.roots([k, 1.0, -e_av]))   # k y^2 + y - E = 0
+            x = min(max(n - target, 0.0), power, y_max * eta)
+            y = x / eta
+            soc -= (y + k * y * y) / bank
+            sg[h], g2l[h] = pv[h] + x, n - x
+    return sg, g2l
+
+
+def test_loss_model_matches_python_restatement():
+    rng = np.random.default_rng(43)
+    hod = np.arange(orc.NH) % 24
+    load = 0.6 + 0.9 * np.exp(-((hod - 19) / 2.5) ** 2) + 0.3 * rng.random(orc.NH)
+    pv = np.maximum(0.0, np.sin((hod - 6) / 12 * np.pi)) * (2.2 + rng.random(orc.NH))
+    # a resistance large enough that the losses move the dispatch visibly
+    cfg = orc.make_cfg(batt_loss_model=1, batt_r_cell=0.05)
+    bank, power = 10.0, 2.5
+    sg, g2l = orc.batt_dispatch(load, pv, bank, power, cfg)
+    rs, rg = _py_dispatch_loss(load, pv, bank, power, cfg)
+    assert np.allclose(sg, rs, rtol=1e-9, atol=1e-9)
+    assert np.allclose(g2l, rg, rtol=1e-9, atol=1e-9)
+    base = orc.batt_dispatch(load, pv, bank, power, orc.make_cfg())
+    assert not np.allclose(g2l, base[1])
+
+
+def test_loss_model_without_resistance_is_the_constant_efficiency():
+    """r = 0 and converters of the constant model's efficiency: the loss model
+    reduces to batt_loss_model = 0 (equal up to the rounding of the
+    rearranged SOC updates)."""
+    rng = np.random.default_rng(44)
+    hod = np.arange(orc.NH) % 24
+    load = 0.5 + 1.2 * np.exp(-((hod - 20) / 2.0) ** 2) + 0.2 * rng.random(orc.NH)
+    pv = np.maximum(0.0, np.sin((hod - 6) / 12 * np.pi)) * 3.0
+    a = orc.batt_dispatch(load, pv, 8.0, 2.0, orc.make_cfg())
+    b = orc.batt_dispatch(load, pv, 8.0, 2.0, orc.make_cfg(batt_loss_model=1, batt_r_cell=0.0,
+                                                           batt_conv_eff=0.9408))
+    assert np.allclose(a[0], b[0], rtol=1e-9, atol=1e-9) and np.allclose(a[1], b[1], rtol=1e-9, atol=1e-9)
+
+
+def test_loss_model_energy_balance():
+    """Every charge stores less than it takes (converter + I^2 R), every
+    discharge draws more than it delivers, and the SOC stays in its window."""
+    rng = np.random.default_rng(45)
+    hod = np.arange(orc.NH) % 24
+    load = 0.4 + 1.5 * np.exp(-((hod - 19) / 2.0) ** 2) + 0.2 * rng.random(orc.NH)
+    pv = np.maximum(0.0, np.sin((hod - 6) / 12 * np.pi)) * 4.0
+    cfg = orc.make_cfg(batt_loss_model=1, batt_r_cell=0.02)
+    bank = 10.0
+    sg, g2l = orc.batt_dispatch(load, pv, bank, 3.0, cfg)
+    flow = sg - pv                                  # + discharge to the load, - charge from PV
+    charged, delivered = -flow[flow < 0].sum(), flow[flow > 0].sum()
+    # stored energy can only come from charging: delivered <= eta^2 x charged + initial usable energy
+    usable0 = (cfg.batt_init_soc - cfg.batt_min_soc) * bank
+    assert delivered <= cfg.batt_conv_eff ** 2 * charged + usable0 * cfg.batt_conv_eff + 1e-9
+    assert delivered > 0.5 * charged                 # and the battery does cycle
