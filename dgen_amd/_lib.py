@@ -45,7 +45,7 @@ class Cfg(ctypes.Structure):
         ("batt_max_soc", _f64), ("batt_init_soc", _f64), ("batt_eta_in", _f64),
         ("batt_eta_out", _f64), ("batt_update_hours", _i32), ("batt_loss_model", _i32),
         ("batt_r_cell", _f64), ("batt_conv_eff", _f64), ("batt_v_cell_empty", _f64),
-        ("batt_v_cell_full", _f64),
+        ("batt_v_cell_full", _f64), ("batt_month_floor", _i32), ("pad1", _i32),
     ]
 
 

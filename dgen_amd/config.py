@@ -44,10 +44,14 @@ class EngineConfig:
     batt_conv_eff: float = 0.96         #         AC-DC / DC-AC converter efficiency
     batt_v_cell_empty: float = 3.0      # V       open-circuit voltage at SOC 0
     batt_v_cell_full: float = 4.2       # V       open-circuit voltage at SOC 1
+    # 1: a peak-shaving plan's target never falls below the month's earlier
+    # targets (SSC's BTM dispatcher keeps a monthly target, as we read its
+    # source; parity unpinned); 0: every plan stands alone (default)
+    batt_month_floor: int = 0
 
     def to_c(self) -> _lib.Cfg:
         d = asdict(self)
-        return _lib.Cfg(pad0=0, **d)
+        return _lib.Cfg(pad0=0, pad1=0, **d)
 
     def oracle_kwargs(self) -> dict:
         d = asdict(self)

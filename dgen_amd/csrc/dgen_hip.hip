@@ -1079,6 +1079,9 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
         double2 xacc = make_double2(0.0, 0.0);
         int n_m = 0;
         NbEntC* const nb_ent = (NB && put_nb) ? reinterpret_cast<NbEntC*>(nbr.ent) + m * NB_CAPM : nullptr;
+        // monthly target floor (dgen_cfg.batt_month_floor): the largest target
+        // planned so far this month (a month-segment launch starts at a month)
+        double mfloor = 0.0;
         // the current period's bin in registers (the same additions in the same
         // order as a per-hour LDS read-modify-write), written back when the
         // period changes and at the month's end
@@ -1163,6 +1166,10 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
 #else
                 target = day_target_sorted(dv, power, avail);
 #endif
+                if (cfg.batt_month_floor) {           // the month's target never falls
+                    if (target < mfloor) target = mfloor;
+                    else mfloor = target;
+                }
                 day_reread(dlane, r);
             }
             if (!ROLL && d < d_last) day_dma(d + 1);            // after the last read of the buffer
@@ -1188,7 +1195,11 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
 #pragma unroll
                         for (int k = 0; k < 24; k++) dv[k] = win[k];
                         sort24_desc(dv);
-                        const double t = day_target_sorted(dv, power, av);
+                        double t = day_target_sorted(dv, power, av);
+                        if (cfg.batt_month_floor && need) {
+                            if (t < mfloor) t = mfloor;
+                            else mfloor = t;
+                        }
                         target = need ? t : 0.0;
                     }
                 }
@@ -4375,6 +4386,10 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     if (!(cfg->batt_v_nom > 0.0) || !(cfg->batt_q_full > 0.0) || !(cfg->batt_eta_in > 0.0) ||
         !(cfg->batt_eta_out > 0.0) || cfg->depr_sl_years < 1) {
         set_err("dgen_open: invalid battery/loan configuration");
+        return DGEN_E_ARG;
+    }
+    if (cfg->batt_month_floor != 0 && cfg->batt_month_floor != 1) {
+        set_err("dgen_open: batt_month_floor must be 0 or 1");
         return DGEN_E_ARG;
     }
     if (cfg->batt_loss_model != 0 && cfg->batt_loss_model != 1) {

@@ -102,6 +102,10 @@ typedef struct {
     double  batt_conv_eff;         /* AC-DC and DC-AC converter efficiency          */
     double  batt_v_cell_empty;     /* cell open-circuit voltage at SOC 0 (V)        */
     double  batt_v_cell_full;      /* cell open-circuit voltage at SOC 1 (V)        */
+    int32_t batt_month_floor;      /* 1: a plan's target never falls below the     */
+                                   /* month's earlier targets (SSC's monthly peak-  */
+                                   /* shaving target, as we read it; ABI 9); 0: off */
+    int32_t pad1;
 } dgen_cfg;
 
 /* Compiled tariff = the Utilityrate5.ElectricityRates energy fields that

@@ -57,6 +57,7 @@ class Cfg(ctypes.Structure):
         ("batt_eta_out", _c_double), ("batt_update_hours", _c_int32),
         ("batt_loss_model", _c_int32), ("batt_r_cell", _c_double), ("batt_conv_eff", _c_double),
         ("batt_v_cell_empty", _c_double), ("batt_v_cell_full", _c_double),
+        ("batt_month_floor", _c_int32),
     ]
 
 
@@ -117,6 +118,7 @@ DEFAULT_CFG = dict(
     depr_sl_years=7, batt_v_nom=3.6, batt_q_full=3.2, batt_min_soc=0.10, batt_max_soc=0.95,
     batt_init_soc=0.30, batt_eta_in=0.9408, batt_eta_out=0.9408, batt_update_hours=24,
     batt_loss_model=0, batt_r_cell=0.001, batt_conv_eff=0.96, batt_v_cell_empty=3.0, batt_v_cell_full=4.2,
+    batt_month_floor=0,
 )
 
 

@@ -570,8 +570,18 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
     const double out_per_bank = bank_kwh > 0.0 ? 1.0 / (cfg->batt_eta_out * bank_kwh) : 0.0;
     const int loss = cfg->batt_loss_model == 1;
     const double eta = cfg->batt_conv_eff;
+    /* monthly target floor (cfg->batt_month_floor): a plan's target is raised
+     * to the largest target planned earlier in the month, and raises it */
+    const int mfl = cfg->batt_month_floor == 1;
+    double floor_t = 0.0;
+    int month = 0, next_month_h = kDaysInMonth[0] * 24;
     for (int h = 0; h < ORC_NH; h++) {
         double n = load[h] - pv[h];
+        if (h == next_month_h) {
+            month++;
+            next_month_h += kDaysInMonth[month] * 24;
+            floor_t = 0.0;
+        }
         if (!(bank_kwh > 0.0)) {
             sysgen[h] = pv[h];
             grid_to_load[h] = n > 0.0 ? n : 0.0;
@@ -583,6 +593,10 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
                 if (e_av < 0.0) e_av = 0.0;
                 if (!hourly) target = day_target(load, pv, h, power_kw, e_av * eta);
                 else target = (n > 0.0 && e_av > 0.0) ? day_target(load, pv, h, power_kw, e_av * eta) : 0.0;
+                if (mfl && (!hourly || (n > 0.0 && e_av > 0.0))) {
+                    if (target < floor_t) target = floor_t;
+                    else floor_t = target;
+                }
             }
             const double k = loss_k(cfg, soc, bank_kwh);
             if (n < 0.0) {
@@ -616,6 +630,10 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
             double avail = (soc - cfg->batt_min_soc) * bank_kwh * cfg->batt_eta_out;
             if (avail < 0.0) avail = 0.0;
             target = day_target(load, pv, h, power_kw, avail);
+            if (mfl) {
+                if (target < floor_t) target = floor_t;
+                else floor_t = target;
+            }
         }
         if (n < 0.0) {
             double room = (cfg->batt_max_soc - soc) * bank_kwh * inv_eta_in;
@@ -629,7 +647,13 @@ void orc_batt_dispatch(const double* load, const double* pv, double bank_kwh, do
         } else {
             double avail = (soc - cfg->batt_min_soc) * bank_kwh * cfg->batt_eta_out;
             if (avail < 0.0) avail = 0.0;
-            if (hourly) target = (n > 0.0 && avail > 0.0) ? day_target(load, pv, h, power_kw, avail) : 0.0;
+            if (hourly) {
+                target = (n > 0.0 && avail > 0.0) ? day_target(load, pv, h, power_kw, avail) : 0.0;
+                if (mfl && n > 0.0 && avail > 0.0) {
+                    if (target < floor_t) target = floor_t;
+                    else floor_t = target;
+                }
+            }
             double d = n - target;
             if (d < 0.0) d = 0.0;
             if (d > power_kw) d = power_kw;

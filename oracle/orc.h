@@ -84,6 +84,7 @@ typedef struct {
     double batt_conv_eff;          /* converter efficiency each way               */
     double batt_v_cell_empty;      /* open-circuit voltage at SOC 0 (V)           */
     double batt_v_cell_full;       /* open-circuit voltage at SOC 1 (V)           */
+    int32_t batt_month_floor;      /* 1: targets floored at the month's earlier   */
 } orc_cfg;
 
 /* One row of the rate-switch table, already filtered to (tech, eia_id, res_com). */

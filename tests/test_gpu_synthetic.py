@@ -412,3 +412,36 @@ def test_li_ion_loss_model_matches_oracle(cfg, n, replan):
         assert np.allclose(o["net_with_batt"][i], ref_h, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(ref_h).max())), i
         moved += not np.allclose(ref_h, b["adopter_net_hourly_with_batt"], rtol=1e-9, atol=1e-9)
     assert moved > 0
+
+
+@pytest.mark.parametrize("replan", [24, 1])
+def test_month_floor_matches_oracle(replan):
+    """batt_month_floor = 1 (the monthly peak-shaving target floor) in
+    k_hourly_batt against the oracle, daily plan and hourly re-plan."""
+    from dgen_amd.config import EngineConfig
+    from dgen_amd.engine import Engine
+    kw = dict(batt_month_floor=1, batt_update_hours=replan)
+    eng = Engine(0, EngineConfig(**kw))
+    try:
+        pop = _small_pop("national_mixed", 300)
+        eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+        eng.set_tariffs(pop.tariffs)
+        eng.set_switches(pop.switches)
+        batch = eng.upload_agents(pop.cols, pop.n_scratch)
+        out = eng.alloc_outputs(batch.n, hourly=True)
+        eng.size(batch, out)
+        torch.cuda.synchronize()
+        o = outputs_to_host(out)
+    finally:
+        eng.close()
+    opop = helpers.oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs, pop.wholesale)
+    ref = opop.run(orc.make_cfg(**kw), hourly=True)
+    base = opop.run(orc.make_cfg(batt_update_hours=replan), hourly=True)
+    moved = 0
+    for i, (r, b) in enumerate(zip(ref, base)):
+        assert o["status"][i] == 0 and r["status"] == 0, i
+        assert np.isclose(o["npv_pv_batt"][i], r["npv_pv_batt"], rtol=1e-6, atol=1e-6), i
+        ref_h = r["adopter_net_hourly_with_batt"]
+        assert np.allclose(o["net_with_batt"][i], ref_h, rtol=1e-5, atol=1e-5 * max(1.0, np.abs(ref_h).max())), i
+        moved += not np.allclose(ref_h, b["adopter_net_hourly_with_batt"], rtol=1e-9, atol=1e-9)
+    assert moved > 0

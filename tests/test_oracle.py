@@ -391,3 +391,27 @@ def test_loss_model_energy_balance():
     usable0 = (cfg.batt_init_soc - cfg.batt_min_soc) * bank
     assert delivered <= cfg.batt_conv_eff ** 2 * charged + usable0 * cfg.batt_conv_eff + 1e-9
     assert delivered > 0.5 * charged                 # and the battery does cycle
+
+
+@pytest.mark.parametrize("hourly", [False, True])
+def test_month_floor_option(hourly):
+    """batt_month_floor = 1: a plan's target is raised to the month's earlier
+    targets (SSC's monthly target, as read; unpinned).  The battery then holds
+    energy back on low days: the dispatch differs, imports never exceed the
+    no-battery imports, and the floor resets each month."""
+    rng = np.random.default_rng(46)
+    hod = np.arange(orc.NH) % 24
+    day = np.arange(orc.NH) // 24
+    # a few high-demand days early in each month, low days after
+    peak = np.where((day % 30) < 3, 3.0, 0.6)
+    load = 0.4 + peak * np.exp(-((hod - 19) / 2.0) ** 2) + 0.1 * rng.random(orc.NH)
+    pv = np.maximum(0.0, np.sin((hod - 6) / 12 * np.pi)) * 2.5
+    base = orc.make_cfg(batt_update_hours=1 if hourly else 24)
+    flo = orc.make_cfg(batt_update_hours=1 if hourly else 24, batt_month_floor=1)
+    a = orc.batt_dispatch(load, pv, 8.0, 2.0, base)
+    b = orc.batt_dispatch(load, pv, 8.0, 2.0, flo)
+    assert not np.allclose(a[1], b[1])
+    assert (b[1] <= np.maximum(load - pv, 0.0) + 1e-12).all()
+    # on the low days the floored dispatch discharges less (it keeps energy)
+    low = (day % 30) >= 10
+    assert (b[0] - pv)[low].clip(min=0).sum() <= (a[0] - pv)[low].clip(min=0).sum() + 1e-9
