@@ -52,7 +52,7 @@ GROUPS_=("FETCH_SIZE" "WRITE_SIZE"
 for step in "$@"; do
   case $step in
   tests)
-    timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} -m gpu ${PYTEST_X--x} -v --timeout 300 \
+    timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest ${TESTS:-tests} -m gpu ${PYTEST_X--x} -v -rP --timeout 300 \
       --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
     echo "pytest gpu rc=$rc"; grep -E "passed|failed|error" $O/pytest_gpu.log | tail -3; stop $rc;;
   smoke)

@@ -188,6 +188,20 @@ VARIANTS = {
                        "        c.nb_ok = c.nb != nullptr;"),
                       ("        wb = c.nb_ok ? yl_bill_nb(t, c.src, c.s_y, c.nb, c.S) : yl_bill_mo2(t, c.src, c.s_y, true, c.S);",
                        "        wb = c.nb_ok ? 1000.0 - kws * c.s_y : yl_bill_mo2(t, c.src, c.s_y, true, c.S);")],
+    # k_hourly_batt: the day-start read-back waits for every outstanding store
+    # (vmcnt(0)) instead of only the DMA: how much the scan waits on stores
+    "hb_vm0": [("            else if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);",
+                "            else if (HOURLY && d > d_lo) day_read<0>(dlane, r);")],
+    # year-lane kernels (k_nb_env, k_size_w, k_batt_finance_w): XCD-aware block
+    # order, so agents adjacent in device order (sharing a load-shape row) run
+    # on one XCD and its L2 serves the row (blocks are dealt round-robin to the
+    # 8 XCDs)
+    "xcd_yl": [("constexpr int WAVE = 64;\n",
+                "constexpr int WAVE = 64;\n__device__ __forceinline__ unsigned xcd_map(unsigned b, unsigned nb) {\n"
+                "    const unsigned q = nb / 8u, r = nb % 8u, x = b % 8u, k = b / 8u;\n"
+                "    return x < r ? x * (q + 1u) + k : r * (q + 1u) + (x - r) * q + k;\n}\n"),
+               ("    const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);",
+                "    const int64_t i = i0 + (int64_t)xcd_map(blockIdx.x, gridDim.x) * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);")],
     # k_batt_finance net-billing: without the split build / bill
     "kf_nb_none": [("            nb_ok = yl_nb_build(t, src, s_lo, s_hi, nbp, S, g);\n            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S);",
                     "            nb_ok = true; wb = 1000.0 * s_y + (double)(size_t)nbp * 0.0;")],

@@ -113,6 +113,8 @@ def test_c4_commercial_dc_1m_sample_vs_oracle(engine_dc):
     torch.cuda.empty_cache()
     flips = _check_sample(subset(pop, idx), sample, np.arange(SAMPLE), orc.make_cfg(),
                           demand=pop.demand, tag="C4")
+    print(f"\nC4 1M sample: demand-charge Brent path flips {len(flips)} of {SAMPLE} (allowed <= 2): {flips}",
+          flush=True)
     assert len(flips) <= 2, flips
     if flips:                            # positions in the sample
         opop = helpers.oracle_population({k: v[idx] for k, v in pop.cols.items()}, pop.tariffs, pop.switches,
