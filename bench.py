@@ -153,6 +153,11 @@ def parse():
                     help="size() pipeline depth (default: the library's DGEN_DEFAULT_CHUNKS)")
     ap.add_argument("--hb-months", type=int, default=None,
                     help="months per k_hourly_batt launch (default: the library's)")
+    ap.add_argument("--hb-split", type=int, default=None, choices=[1, 2],
+                    help="k_hourly_batt's chunk halves on 1 or 2 streams (A/B; DGEN_HB_SPLIT)")
+    ap.add_argument("--hb-nem", type=int, default=None, choices=[0, 1],
+                    help="batches without scratch slots run the bins-only scan (1, default) or the general one "
+                         "(0; A/B; DGEN_HB_NEM)")
     ap.add_argument("--order-major", default="load", choices=["cf", "load"],
                     help="profile_order grouping: by (cf_row, load_row) or (load_row, cf_row)")
     ap.add_argument("--caller-order", action="store_true",
@@ -248,6 +253,10 @@ def main():
     from dgen_amd.engine import Engine, profile_order
     from dgen_amd.synth import make_population
 
+    if args.hb_nem is not None:
+        os.environ["DGEN_HB_NEM"] = str(args.hb_nem)              # read by dgen_open
+    if args.hb_split is not None:
+        os.environ["DGEN_HB_SPLIT"] = str(args.hb_split)          # read by dgen_open
     pop = make_population(args.config, args.agents, seed=20260000 + 3 + 7919 * rank)
     # demand-charge configs run the extension mode; every other config the
     # reference's switch (SKIP_DEMAND_CHARGES = True, ff:35)

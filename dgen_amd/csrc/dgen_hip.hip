@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <type_traits>
@@ -873,7 +874,11 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 // LOSS: the Li-ion loss model (dgen_cfg.batt_loss_model = 1, batt_hour_loss);
 // instantiated without the scan-built records (NB, DCR), whose finance
 // kernels then take the plane passes (equal results).
-template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR, bool LOSS = false>
+// NEM: the batch has no scratch slot (dgen_size_agents' n_scratch == 0), so no
+// agent bills hourly imports: the bins path only, no system-output plane and
+// no per-hour net-billing branch (an agent that would need one is flagged
+// DGEN_ST_SCRATCH, as in every form).
+template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR, bool LOSS = false, bool NEM = false>
 __global__ void __launch_bounds__(BLOCK, ROLL ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
@@ -931,14 +936,14 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     }
     const dgen_tariff& t = T.tariffs[tariff];
     const int P = t.P;
-    const bool mo2 = net_hourly(t);     // hourly imports (net billing 2 / 3), else bins
+    const bool mo2 = !NEM && net_hourly(t);     // hourly imports (net billing 2 / 3), else bins
     const int slot = A.scratch_slot[i];
     // the battery-case bill reads the hourly system output for net billing and
     // for demand charges (both need hourly imports, not bins)
     const bool has_dc = tariff_demand(T, cfg, t) != nullptr ||
                         tariff_peaks(T.demand, T.n_demand, t) != nullptr;   // kWh/kW tiers: peaks
-    const bool need_sys = mo2 || has_dc;
-    const bool put_sys = need_sys && slot >= 0 && batt_on;
+    const bool need_sys = net_hourly(t) || has_dc;
+    const bool put_sys = !NEM && need_sys && slot >= 0 && batt_on;
     int status = O.status[i] | t.flags;
     if (need_sys && slot < 0 && batt_on) status |= DGEN_ST_SCRATCH;
     // The battery case's net-billing split over the agent's degradation range
@@ -1112,6 +1117,10 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
             dse[0] = b[0]; dse[1] = b[1]; dse[2] = b[2];
             for (int q = 0; q < dc_nq; q++) dcb[q * BLOCK] = make_double2(0.0, 0.0);
         }
+        // the month's schedule rows land here, once per month: left pending,
+        // the compiler's wait for them can fall inside the day loop, where
+        // (loop-carried) it drains every day's stores and the next-day DMA
+        __builtin_amdgcn_s_waitcnt(0x0f70);                  // vmcnt(0)
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             if (ROLL && d > d_lo) day_reread(dlane, r);    // the DMA was waited for yesterday
             else if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);
@@ -4323,6 +4332,10 @@ struct dgen_ctx {
     int nch[RING];     // chunks recorded in the slot
     hipEvent_t fork, join;
     hipStream_t s2;    // hourly + finance stream of the chunk pipeline
+    hipStream_t s3;    // second hourly stream (hb_split = 2)
+    hipEvent_t hb_join;
+    int hb_split;      // 1, or 2: the hourly scan's chunk halves on two streams (DGEN_HB_SPLIT)
+    int hb_nem;        // 1: batches without scratch slots run the bins-only scan (DGEN_HB_NEM=0: off)
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
     int battery;       // PV+battery forward run (dgen_set_battery)
@@ -4417,7 +4430,15 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     c->battery = 1;
     c->nb_scan = DGEN_NB_CAPM;
     c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
+    {
+        const char* v = getenv("DGEN_HB_SPLIT");
+        c->hb_split = (v && v[0] == '2') ? 2 : 1;
+        const char* w = getenv("DGEN_HB_NEM");
+        c->hb_nem = (w && w[0] == '0') ? 0 : 1;
+    }
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->s3, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->hb_join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
     for (int r = 0; r < dgen_ctx::RING && e == hipSuccess; r++) {
@@ -4438,12 +4459,15 @@ int32_t dgen_close(dgen_ctx* c) {
     if (!c) return DGEN_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->s2);
+    (void)hipStreamSynchronize(c->s3);
     for (int r = 0; r < dgen_ctx::RING; r++)
         for (int j = 0; j < dgen_ctx::MAXCH; j++)
             for (int k = 0; k < 5; k++) (void)hipEventDestroy(c->ev[r][j][k]);
     (void)hipEventDestroy(c->fork);
     (void)hipEventDestroy(c->join);
     (void)hipStreamDestroy(c->s2);
+    (void)hipStreamDestroy(c->s3);
+    (void)hipEventDestroy(c->hb_join);
     if (c->dc_buf) (void)hipFree(c->dc_buf);
     if (c->dcr_buf) (void)hipFree(c->dcr_buf);
     delete c;
@@ -4673,31 +4697,46 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
         HIP_TRY(hipEventRecord(e[2], s2));
-        dim3 grid((unsigned)((m + BLOCK - 1) / BLOCK)), block(BLOCK);
+        const dim3 block(BLOCK);
+        // hourly split (DGEN_HB_SPLIT=2 at dgen_open, A/B): the chunk's two
+        // halves sweep their months on two streams, so one half's launch tails
+        // overlap the other's waves
+        const int nparts = (c->hb_split == 2 && m >= 4 * BLOCK) ? 2 : 1;
+        // no scratch slot in the batch: the bins-only scan (DGEN_HB_NEM=0 disables, A/B)
+        const bool nem_only = n_scratch == 0 && c->hb_nem;
+        const int64_t cut = i0 + (((m + 1) / 2 + BLOCK - 1) / BLOCK) * BLOCK;
+        if (nparts == 2) HIP_TRY(hipStreamWaitEvent(c->s3, e[1], 0));
+        for (int part = 0; part < nparts; part++) {
+        const int64_t ha = part == 0 ? i0 : cut, hb = (nparts == 1 || part == 1) ? i1 : cut;
+        hipStream_t hs = part == 0 ? s2 : c->s3;
+        const dim3 hgrid((unsigned)((hb - ha + BLOCK - 1) / BLOCK));
         for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
 #define DGEN_HB_LAUNCH_R(H, F, REP, R)                                                            \
     do {                                                                                          \
         if (nb_scan && !(REP) && dcr_on && !(R))                                                  \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, true>), grid, block, lds, s2, *T, *A, *O, \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, dcr, dc_nq, c->dcr_enable); \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, true>), hgrid, block, lds, hs, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, dcr, dc_nq, c->dcr_enable); \
         else if (nb_scan && !(REP))                                                               \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, true, R, false>), grid, block, lds, s2, *T, *A, *O, c->cfg, \
-                               n, ws, n_scratch, i0, i1, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0); \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, true, R, false>), hgrid, block, lds, hs, *T, *A, *O, c->cfg, \
+                               n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0); \
         else if (!(REP) && dcr_on && !(R))                                                        \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, false, false, true>), grid, block, lds, s2, *T, *A, *O, \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, 0, dcr, dc_nq, c->dcr_enable); \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false, false, true>), hgrid, block, lds, hs, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, 0, 0, dcr, dc_nq, c->dcr_enable); \
         else                                                                                      \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, false, R, false>), grid, block, lds, s2, *T, *A, *O, \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, (REP) ? rep_mask : 0, \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false, R, false>), hgrid, block, lds, hs, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, 0, (REP) ? rep_mask : 0, \
                                (REP) ? dcr : nullptr, 0, 0);                                                               \
     } while (0)
 #define DGEN_HB_LAUNCH_LOSS(H, F, R)                                                              \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, false, R, false, true>), grid, block, lds, s2, *T, *A, *O, \
-                               c->cfg, n, ws, n_scratch, i0, i1, m0, m1, c->battery, 0, 0, nullptr, 0, 0)
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false, R, false, true>), hgrid, block, lds, hs, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, 0, 0, nullptr, 0, 0)
 #define DGEN_HB_LAUNCH(H, F, REP)                                                                 \
     do {                                                                                          \
-        if (loss && c->cfg.batt_update_hours == 1) DGEN_HB_LAUNCH_LOSS(H, F, true);              \
+        if (nem_only && !loss && c->cfg.batt_update_hours != 1 && !(REP))                         \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, false, false, false, false, true>), hgrid, block, lds, hs, \
+                               *T, *A, *O, c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, 0, 0, nullptr, 0, 0); \
+        else if (loss && c->cfg.batt_update_hours == 1) DGEN_HB_LAUNCH_LOSS(H, F, true);         \
         else if (loss) DGEN_HB_LAUNCH_LOSS(H, F, false);                                          \
         else if (c->cfg.batt_update_hours == 1) DGEN_HB_LAUNCH_R(H, F, REP, true);                \
         else DGEN_HB_LAUNCH_R(H, F, REP, false);                                                  \
@@ -4706,8 +4745,16 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             else if (hourly) DGEN_HB_LAUNCH(true, false, false);
             else DGEN_HB_LAUNCH(false, false, false);
         }
+        }
+        if (nparts == 2) {
+            HIP_TRY(hipEventRecord(c->hb_join, c->s3));
+            HIP_TRY(hipStreamWaitEvent(s2, c->hb_join, 0));
+        }
         // repair pass (agents whose scan-built split or demand record
-        // overflowed: their plane)
+        // overflowed: their plane), whole chunk on s2
+        const int64_t ha = i0, hb = i1;
+        hipStream_t hs = s2;
+        const dim3 hgrid((unsigned)((m + BLOCK - 1) / BLOCK));
         for (int m0 = 0; rep_mask && m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
             if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, true);

@@ -41,6 +41,8 @@ VARIANTS = {
     # hour-lane envelope build: days of loads in flight per lane
     "dcb16": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 16;")],
     "dcb12": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 12;")],
+    "dcb4": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 4; ")],
+    "dcb6": [("constexpr int DCB_DAYS = 8; ", "constexpr int DCB_DAYS = 6; ")],
     # phase timers only (DGEN_PHASE_PROF slots, see dgen_hip.hip)
     "phase": [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1")],
     # timing probes of the hour-lane envelope build (wrong results by construction)
