@@ -153,8 +153,8 @@ def parse():
                     help="size() pipeline depth (default: the library's DGEN_DEFAULT_CHUNKS)")
     ap.add_argument("--hb-months", type=int, default=None,
                     help="months per k_hourly_batt launch (default: the library's)")
-    ap.add_argument("--hb-split", type=int, default=None, choices=[1, 2],
-                    help="k_hourly_batt's chunk halves on 1 or 2 streams (A/B; DGEN_HB_SPLIT)")
+    ap.add_argument("--hb-split", type=int, default=None, choices=[1, 2, 3, 4],
+                    help="parts of k_hourly_batt's scan, each on its own stream (default the library's, 2; A/B; DGEN_HB_SPLIT)")
     ap.add_argument("--hb-nem", type=int, default=None, choices=[0, 1],
                     help="batches without scratch slots run the bins-only scan (1, default) or the general one "
                          "(0; A/B; DGEN_HB_NEM)")
@@ -170,6 +170,11 @@ def parse():
     ap.add_argument("--pmc-dir", default=os.path.join(REPO, "profiles", "pmc"),
                     help="per-workload PMC summaries (traffic field); none -> traffic null")
     return ap.parse_args()
+
+
+def _lib_default_split() -> int:
+    from dgen_amd import _lib
+    return _lib.DEFAULT_HOURLY_SPLIT
 
 
 def dist_env():
@@ -374,6 +379,7 @@ def main():
                        "battery_run": not args.no_batt,
                        "battery_replan_hours": args.replan_hours,
                        "pipeline_chunks": eng.chunks, "hourly_months_per_launch": eng.hb_months,
+                       "hourly_scan_streams": int(os.environ.get("DGEN_HB_SPLIT", _lib_default_split())),
                        "device_order": "caller" if args.caller_order else
                        ("profile (cf_row, load_row)" if args.order_major == "cf" else "profile (load_row, cf_row)"),
                        "parallelism": f"dp{ws} (agent shards, no collective in the step)",

@@ -108,6 +108,7 @@ _LIB: Optional[ctypes.CDLL] = None
 ABI_VERSION = 9   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
+DEFAULT_HOURLY_SPLIT = 2   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_SPLIT
 
 EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",

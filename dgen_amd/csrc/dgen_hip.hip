@@ -4332,9 +4332,10 @@ struct dgen_ctx {
     int nch[RING];     // chunks recorded in the slot
     hipEvent_t fork, join;
     hipStream_t s2;    // hourly + finance stream of the chunk pipeline
-    hipStream_t s3;    // second hourly stream (hb_split = 2)
-    hipEvent_t hb_join;
-    int hb_split;      // 1, or 2: the hourly scan's chunk halves on two streams (DGEN_HB_SPLIT)
+    static constexpr int MAXSPLIT = 4;
+    hipStream_t sx[MAXSPLIT - 1];       // the hourly scan's other parts' streams
+    hipEvent_t hb_join[MAXSPLIT - 1];
+    int hb_split;      // parts of a chunk's hourly scan, each on its own stream (1..4; DGEN_HB_SPLIT)
     int hb_nem;        // 1: batches without scratch slots run the bins-only scan (DGEN_HB_NEM=0: off)
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
@@ -4432,13 +4433,15 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     c->sum_ms[0] = c->sum_ms[1] = c->sum_ms[2] = 0.0;
     {
         const char* v = getenv("DGEN_HB_SPLIT");
-        c->hb_split = (v && v[0] == '2') ? 2 : 1;
+        c->hb_split = (v && v[0] >= '1' && v[0] <= '4') ? v[0] - '0' : DGEN_DEFAULT_HOURLY_SPLIT;
         const char* w = getenv("DGEN_HB_NEM");
         c->hb_nem = (w && w[0] == '0') ? 0 : 1;
     }
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->s3, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->hb_join, hipEventDisableTiming);
+    for (int k = 0; k < dgen_ctx::MAXSPLIT - 1 && e == hipSuccess; k++) {
+        e = hipStreamCreateWithFlags(&c->sx[k], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->hb_join[k], hipEventDisableTiming);
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
     for (int r = 0; r < dgen_ctx::RING && e == hipSuccess; r++) {
@@ -4459,15 +4462,17 @@ int32_t dgen_close(dgen_ctx* c) {
     if (!c) return DGEN_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->s2);
-    (void)hipStreamSynchronize(c->s3);
+    for (int k = 0; k < dgen_ctx::MAXSPLIT - 1; k++) (void)hipStreamSynchronize(c->sx[k]);
     for (int r = 0; r < dgen_ctx::RING; r++)
         for (int j = 0; j < dgen_ctx::MAXCH; j++)
             for (int k = 0; k < 5; k++) (void)hipEventDestroy(c->ev[r][j][k]);
     (void)hipEventDestroy(c->fork);
     (void)hipEventDestroy(c->join);
     (void)hipStreamDestroy(c->s2);
-    (void)hipStreamDestroy(c->s3);
-    (void)hipEventDestroy(c->hb_join);
+    for (int k = 0; k < dgen_ctx::MAXSPLIT - 1; k++) {
+        (void)hipStreamDestroy(c->sx[k]);
+        (void)hipEventDestroy(c->hb_join[k]);
+    }
     if (c->dc_buf) (void)hipFree(c->dc_buf);
     if (c->dcr_buf) (void)hipFree(c->dcr_buf);
     delete c;
@@ -4698,17 +4703,21 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
         HIP_TRY(hipEventRecord(e[2], s2));
         const dim3 block(BLOCK);
-        // hourly split (DGEN_HB_SPLIT=2 at dgen_open, A/B): the chunk's two
-        // halves sweep their months on two streams, so one half's launch tails
-        // overlap the other's waves
-        const int nparts = (c->hb_split == 2 && m >= 4 * BLOCK) ? 2 : 1;
+        // hourly split (dgen_ctx::hb_split parts, default 2; DGEN_HB_SPLIT
+        // overrides): the chunk's parts sweep their months on their own
+        // streams, so one part's launch tails overlap the others' waves (C3
+        // 1M: k_hourly_batt 24.26 -> 23.68 ms with 2 parts, profiles/r04/ab)
+        int nparts = c->hb_split;
+        while (nparts > 1 && m < (int64_t)nparts * 2 * BLOCK) nparts--;
+        const int64_t psz = ((m + nparts - 1) / nparts + BLOCK - 1) / BLOCK * BLOCK;
         // no scratch slot in the batch: the bins-only scan (DGEN_HB_NEM=0 disables, A/B)
         const bool nem_only = n_scratch == 0 && c->hb_nem;
-        const int64_t cut = i0 + (((m + 1) / 2 + BLOCK - 1) / BLOCK) * BLOCK;
-        if (nparts == 2) HIP_TRY(hipStreamWaitEvent(c->s3, e[1], 0));
+        for (int part = 1; part < nparts; part++) HIP_TRY(hipStreamWaitEvent(c->sx[part - 1], e[1], 0));
         for (int part = 0; part < nparts; part++) {
-        const int64_t ha = part == 0 ? i0 : cut, hb = (nparts == 1 || part == 1) ? i1 : cut;
-        hipStream_t hs = part == 0 ? s2 : c->s3;
+        const int64_t ha = i0 + part * psz < i1 ? i0 + part * psz : i1;
+        const int64_t hb = part == nparts - 1 ? i1 : (ha + psz < i1 ? ha + psz : i1);
+        hipStream_t hs = part == 0 ? s2 : c->sx[part - 1];
+        if (hb <= ha) continue;
         const dim3 hgrid((unsigned)((hb - ha + BLOCK - 1) / BLOCK));
         for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
@@ -4746,9 +4755,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             else DGEN_HB_LAUNCH(false, false, false);
         }
         }
-        if (nparts == 2) {
-            HIP_TRY(hipEventRecord(c->hb_join, c->s3));
-            HIP_TRY(hipStreamWaitEvent(s2, c->hb_join, 0));
+        for (int part = 1; part < nparts; part++) {
+            HIP_TRY(hipEventRecord(c->hb_join[part - 1], c->sx[part - 1]));
+            HIP_TRY(hipStreamWaitEvent(s2, c->hb_join[part - 1], 0));
         }
         // repair pass (agents whose scan-built split or demand record
         // overflowed: their plane), whole chunk on s2

@@ -43,17 +43,20 @@ E_BOUND_E = np.array([1.0, 2.0, 2.0, 3.0, 4.0, 6.0, 8.0, 9.0, 11.0, 13.0, 16.0])
 
 # Device ns per agent by billing path (engine.path_class: 0 bins / NEM, 1 net
 # billing from the scan-built split, 2 other hourly: TS sell rate or demand
-# charges) and sector: (scan + battery-case finance, per Brent evaluation).
-# Calibrated on MI355X by scripts/calibrate_cost.py (national population,
-# 200k agents per path batch; profiles/r04/calibrate/cost.json).
+# charges) and sector: (scan + battery-case finance, per Brent evaluation of
+# the search).  Measured on MI355X by scripts/calibrate_cost.py: each class of
+# a national population sized alone, 100k agents (profiles/r04/calibrate/
+# cost.log).  The commercial net-billing class had 32k agents, whose fixed
+# per-launch costs inflate its scan figure (128 ns): its scan is taken as the
+# residential one's.
 PATH_COST_NS = {
     # (path, is_res): (scan, per_eval)
-    (0, True): (28.0, 4.0),
-    (0, False): (30.0, 4.0),
-    (1, True): (55.0, 45.0),
-    (1, False): (60.0, 45.0),
-    (2, True): (80.0, 45.0),
-    (2, False): (85.0, 45.0),
+    (0, True): (42.8, 4.5),
+    (0, False): (42.2, 2.8),
+    (1, True): (57.2, 43.3),
+    (1, False): (57.2, 37.7),
+    (2, True): (125.6, 60.0),
+    (2, False): (142.6, 39.0),
 }
 
 

@@ -468,10 +468,15 @@ class YearLoop:
             rows_local = np.flatnonzero(keep)
             fst = [st[i] for i in rows_local]
             fsec = [sec[i] for i in rows_local]
-            dev_index = [self.inv[rows_local]]
-            vals_w, vals_c = [w], [cx]
-            ext = n
-            take = []
+            # value columns in frame order: this rank's rows outside split
+            # groups, then the gathered groups (the frame and its values have
+            # one row each, initial_market_shares' contract)
+            loc_dev = torch.as_tensor(self.inv[rows_local], device=self.eng.dev)
+            L = int(rows_local.size)
+            dev_index = [np.arange(L, dtype=np.int64)]
+            vals_w, vals_c = [w.index_select(0, loc_dev)], [cx.index_select(0, loc_dev)]
+            ext = L
+            take = [(0, loc_dev)]
             for (b0, G, o, rows, _), key in zip(self.sg, [k for k, c in zip(self.split.keys, self.split.own_cnt)
                                                           if c > 0]):
                 fst += [STATES[key[0]]] * G
@@ -487,8 +492,8 @@ class YearLoop:
                                         torch.cat(vals_c), caps, dev_index=np.concatenate(dev_index))
             for k in list(ini.keys()):
                 v = ini[k]
-                if isinstance(v, torch.Tensor) and v.dim() == 1 and v.numel() == ext:
-                    own = v[:n].clone()
+                if isinstance(v, torch.Tensor) and v.dim() == 1 and v.numel() == ext and k != "agent_count":
+                    own = torch.empty(n, dtype=v.dtype, device=v.device)
                     for e0, rows in take:
                         own.index_copy_(0, rows, v[e0:e0 + rows.numel()])
                     ini[k] = own

@@ -42,6 +42,7 @@ extern "C" {
 #define DGEN_ABI_VERSION 9
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
+#define DGEN_DEFAULT_HOURLY_SPLIT 2   /* parts of a chunk's hourly scan, each on its own stream */
 #define DGEN_NH    8760   /* hours per year                                    */
 #define DGEN_NSLOT 576    /* 12 months x {weekday, weekend} x 24 hours         */
 #define DGEN_MAXP  12     /* TOU periods                                        */

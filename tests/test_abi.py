@@ -35,6 +35,8 @@ def test_library_exports_every_declared_symbol():
     assert m and int(m.group(1)) == _lib.DEFAULT_CHUNKS
     m = re.search(r"#define DGEN_DEFAULT_HOURLY_MONTHS\s+(\d+)", open(HEADER).read())
     assert m and int(m.group(1)) == _lib.DEFAULT_HOURLY_MONTHS
+    m = re.search(r"#define DGEN_DEFAULT_HOURLY_SPLIT\s+(\d+)", open(HEADER).read())
+    assert m and int(m.group(1)) == _lib.DEFAULT_HOURLY_SPLIT
 
 
 def test_workspace_bytes_formula():

@@ -87,8 +87,10 @@ def test_profile_order_is_invisible(engine, cfg, n):
     for order in (None, profile_order(pop.cols)):
         batch = engine.upload_agents(pop.cols, pop.n_scratch, order=order)
         if order is not None:
-            rows = pop.cols["load_row"][batch.perm]
-            assert (np.diff(rows) >= 0).all()
+            # grouped by billing path, then load row (engine.profile_order)
+            from dgen_amd.engine import path_class
+            key = path_class(pop.cols).astype(np.int64)[batch.perm] * (1 << 32) + pop.cols["load_row"][batch.perm]
+            assert (np.diff(key) >= 0).all()
         out = engine.alloc_outputs(batch.n, hourly=True)
         engine.size(batch, out)
         torch.cuda.synchronize()
