@@ -6,7 +6,8 @@ usage: pmc_summary.py 'DIR_GLOB' AGENTS OUT_JSON [HB_LAUNCHES]
   DIR_GLOB     rocprofv3 -d directories of the workload's PMC passes
   AGENTS       agents per sizing call
   OUT_JSON     e.g. profiles/pmc/<workload>.json (read by bench.py --pmc-dir)
-  HB_LAUNCHES  k_hourly_batt dispatches per sizing call (month segments; 12)
+  HB_LAUNCHES  k_hourly_batt dispatches per sizing call when the passes do not
+               show it (default 12); measured from the dispatch counts otherwise
 
 HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE
 are KiB from the L2's memory-side request counters; on gfx950 FETCH_SIZE
@@ -26,16 +27,28 @@ agg = collections.defaultdict(list)
 files = []
 for d in glob.glob(pattern):
     files += glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
+disp = collections.defaultdict(set)       # (file, kernel) -> dispatch ids
 for f in files:
     for r in csv.DictReader(open(f)):
         kn = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("<")[0]
         agg[(kn, r["Counter_Name"])].append(float(r["Counter_Value"]))
+        disp[(f, kn)].add(r["Dispatch_Id"])
+# dispatches per sizing call, measured: a kernel's dispatches over k_size_w's
+# (one per call) in the same pass (k_hourly_batt: month segments x scan parts)
+measured = {}
+for (f, kn), ids in disp.items():
+    ks = disp.get((f, "k_size_w"))
+    if ks:
+        measured.setdefault(kn, []).append(len(ids) / len(ks))
 res = {}
 for kn in sorted({k for k, _ in agg}):
     if not kn.startswith("k_"):
         continue
     means = {c: sum(v) / len(v) for (k, c), v in agg.items() if k == kn}
-    per_call = hb_launches if kn == "k_hourly_batt" else 1
+    if kn in measured and measured[kn]:
+        per_call = round(sum(measured[kn]) / len(measured[kn]), 3)
+    else:
+        per_call = hb_launches if kn == "k_hourly_batt" else 1
     rec = {"counters_per_dispatch": means, "dispatches_per_call": per_call, "agents": agents}
     if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
         rd = 2.0 * means["FETCH_SIZE"] * 1024.0 * per_call
