@@ -69,6 +69,26 @@ VARIANTS = {
                    "                target = 0.0; asm volatile(\"\" :: \"v\"(dv[0]), \"v\"(dv[23]), \"v\"(avail));")],
     "no_bisect": [("    if (s[0] <= power) {\n        double S = 0.0, SK = s[0];", "    if (true) {\n        double S = 0.0, SK = s[0];")],
     "no_sort": [("                sort24_desc(dv);", "")],
+    # k_hourly_batt wave priority: the hour loop (stores) above the day's sort
+    # / target, or the reverse
+    "hb_prio": [("            const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);",
+                 "            __builtin_amdgcn_s_setprio(2);\n            const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);"),
+                ("            if (ROLL && d > d_lo) day_reread(dlane, r);",
+                 "            __builtin_amdgcn_s_setprio(0);\n            if (ROLL && d > d_lo) day_reread(dlane, r);")],
+    "hb_prio_rev": [("            const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);",
+                     "            __builtin_amdgcn_s_setprio(0);\n            const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);"),
+                    ("            if (ROLL && d > d_lo) day_reread(dlane, r);",
+                     "            __builtin_amdgcn_s_setprio(2);\n            if (ROLL && d > d_lo) day_reread(dlane, r);")],
+    # k_hourly_batt: odd waves of a block start about half a day later (phase
+    # offset between the waves' sort and store phases)
+    "hb_stagger": [("    WsLayout W = ws_layout(ws, n);\n    // battery-case bins",
+                    "    WsLayout W = ws_layout(ws, n);\n    if ((threadIdx.x >> 6) & 1) { __builtin_amdgcn_s_sleep(127); __builtin_amdgcn_s_sleep(127); }\n    // battery-case bins")],
+    "hb_stagger4": [("    WsLayout W = ws_layout(ws, n);\n    // battery-case bins",
+                     "    WsLayout W = ws_layout(ws, n);\n    for (int k = 0; k < (int)(threadIdx.x >> 6); k++) __builtin_amdgcn_s_sleep(80);\n    // battery-case bins")],
+    # k_hourly_batt without the day's deficits, sort and target (hour loop and
+    # stores only; wrong results by construction: the write / VALU split)
+    "no_day_target": [("            } else if (has_batt) {\n                // the day's deficits",
+                       "            } else if (false) {\n                // the day's deficits")],
     "no_hourly_stores": [("st_f32(ob + ho4, off4, (float)ld);", "asm volatile(\"\" :: \"v\"(ld));"),
                          ("st_f32(op + ho4, off4, (float)fmax(dn, 0.0));", "asm volatile(\"\" :: \"v\"(dn));"),
                          ("st_f32(ow + ho4, off4, (float)st.g2l);", "asm volatile(\"\" :: \"v\"(st.g2l));")],
