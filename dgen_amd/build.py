@@ -82,6 +82,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     for attempt in range(2):
         work, lib, asm = _compile(defines, verbose)
         try:
+            if os.environ.get("DGEN_KEEP_ASM"):        # a copy of the device assembly to study
+                shutil.copyfile(asm, os.environ["DGEN_KEEP_ASM"])
             hits = spill_guard.scan(asm)
             if attempt == 0:
                 first = {k: [b for b, _ in v] for k, v in hits.items()}

@@ -1013,16 +1013,16 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const int d_lo = c_month_start_day[m_lo];
     // hour rows: wave-uniform bases advanced per row; per-lane 32-bit byte
     // offsets (host guarantees n < 2^28, n_scratch < 2^28)
-    // system-output scratch plane in hour-quad tiles [2190][n_scratch][4] f64:
-    // a lane stores its 4 hours as 32 contiguous bytes, a reader loads them
-    // as two 16-B loads (sys_quad)
-    const size_t off32 = (size_t)(put_sys ? slot : 0) * 32u;
-    const size_t row32 = (size_t)n_scratch * 32u;
+    // system-output scratch plane in day tiles [365][n_scratch][24] f64
+    // (sys_index): a lane stores each hour quad as 32 contiguous bytes of its
+    // 192-B day, a reader loads a quad as two 16-B loads (sys_quad)
+    const size_t off192 = (size_t)(put_sys ? slot : 0) * 192u;
+    const size_t row192 = (size_t)n_scratch * 192u;
     char* const ob = reinterpret_cast<char*>(O.baseline);
     char* const op = reinterpret_cast<char*>(O.net_pvonly);
     char* const ow = reinterpret_cast<char*>(O.net_with_batt);
     char* const osc = reinterpret_cast<char*>(W.scratch);
-    size_t hq32 = (size_t)d_lo * 6 * row32;
+    size_t hd192 = (size_t)d_lo * row192;                // the current day's tile
     double qs[4] = {0.0, 0.0, 0.0, 0.0};
     // hourly planes in hour-quad tiles (include/dgen_hip.h): (hour h, agent i)
     // at ((h / 4) * n + i) * 4 + h % 4, so a lane stores 16 B and a wave 1 KB
@@ -1266,12 +1266,12 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                 }
                 qs[hh & 3] = st.sys;
                 if ((hh & 3) == 3) {
-                    if (put_sys && !skip_plane) {               // tile [h / 4][slot][4]
-                        double2* q = reinterpret_cast<double2*>(osc + hq32 + off32);
+                    if (put_sys && !skip_plane) {               // tile [d][slot][24], quad hh / 4
+                        double2* q = reinterpret_cast<double2*>(osc + hd192 + off192 + (size_t)(hh >> 2) * 32u);
                         q[0] = make_double2(qs[0], qs[1]);
                         q[1] = make_double2(qs[2], qs[3]);
                     }
-                    hq32 += row32;
+                    if (hh == 23) hd192 += row192;
                 }
                 if (!mo2) {   // NEM energy bill from bins (demand charges also read the plane)
                     const int p = (int)((sched[hh >> 3] >> (8 * (hh & 7))) & 0xffu);
@@ -1802,10 +1802,23 @@ struct YSrc {
     double ts_mult;
 };
 
-// The 4 system-output values of hours h .. h + 3 (h % 4 == 0) from the
-// hour-quad scratch tiles (src.sysgen = scratch + 4 x slot, stride n_scratch).
+// The battery case's system-output plane in day tiles [365][n_scratch][24] f64
+// (src.sysgen = scratch + 24 x slot, stride n_scratch): an agent's day is 192
+// contiguous bytes, so the finance kernel's hour lanes read a day as 1.5 cache
+// lines (the hour-quad tiles [2190][n_scratch][4] cost them a line per 4 hours,
+// each shared with 3 other agents: ~3.4x the plane in L2 fills on the national
+// TS sell-rate agents), while a scan wave's 6 quad stores of a day still cover
+// one contiguous 12 KB run.
+__device__ __forceinline__ int64_t sys_index(const YSrc& src, int h) {
+    const int d = h / 24;
+    return (int64_t)d * src.sys_stride * 24 + (h - d * 24);
+}
+__device__ __forceinline__ double sys_at(const YSrc& src, int h) { return src.sysgen[sys_index(src, h)]; }
+
+// The 4 system-output values of hours h .. h + 3 (h % 4 == 0; a quad never
+// straddles a day)
 __device__ __forceinline__ void sys_quad(const YSrc& src, int h, double* g) {
-    const double2* q = reinterpret_cast<const double2*>(src.sysgen + (int64_t)(h >> 2) * src.sys_stride * 4);
+    const double2* q = reinterpret_cast<const double2*>(src.sysgen + sys_index(src, h));
     const double2 a = q[0], b = q[1];
     g[0] = a.x; g[1] = a.y; g[2] = b.x; g[3] = b.y;
 }
@@ -2194,7 +2207,7 @@ __device__ __forceinline__ double yl_demand_staged(const dgen_demand* D, const Y
                     const int pp = ((d % 7) >= 5) ? D->wkend[m][hod] : D->wkday[m][hod];
                     pq[u] = valid ? (pp < DCP ? pp : 0) : -1;
                     Lq[u] = (double)src.shape[hu] * src.load_scale;
-                    gq[u] = with_gen ? src.sysgen[(int64_t)(hu >> 2) * src.sys_stride * 4 + (hu & 3)] : 0.0;
+                    gq[u] = with_gen ? src.sysgen[(int64_t)d * src.sys_stride * 24 + hod] : 0.0;
                 }
             }
         };
@@ -2313,6 +2326,36 @@ __device__ __forceinline__ DcEnv dc_env_at(void* base, int64_t i) {
     e.maxl = reinterpret_cast<double*>(b + (size_t)12 * DCP * DC_NL * sizeof(double2));
     e.cnt = reinterpret_cast<int*>(b + (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double)));
     return e;
+}
+
+// L2 warm-up for the hour-lane walks (yl_dc_build_coop, yl_nb_build): those
+// read an agent's rows a few days at a time and wait for each batch, so on a
+// loaded chip every batch paid an HBM / Infinity-Cache round trip (C4: ~5k of
+// the ~8k cycles per 8-day batch of the envelope build).  Before a month's
+// walk the segment touches the NEXT month's lines: lane k of the segment
+// issues one 4-B LDS-DMA into the wave's scratch slot (no VGPR held in
+// flight, nothing reads the slot) at line k of the span, so the whole span
+// comes into L2 while the current month is walked.  vmcnt retires in issue
+// order: a batch issued after the touch waits for it too, but both were
+// issued together and overlap.  The compiler does not see the DMA, which only
+// makes its own vmcnt waits stricter.
+__device__ __forceinline__ uint32_t l2_touch_slot() {
+    __shared__ uint32_t touch_slot[WAVE];
+    return (uint32_t)(size_t)(lds_ptr_t)(reinterpret_cast<char*>(touch_slot));
+}
+__device__ __forceinline__ void l2_touch(const void* g, uint32_t slot) {
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" :: "v"(g), "s"(slot) : "memory", "m0");
+}
+// the lines of [p, p + bytes) (bytes <= NI x LPA x 128): lane sl of the
+// segment takes lines sl, sl + LPA, ...; a lane past the span touches its first line
+template <int NI, int LPA>
+__device__ __forceinline__ void l2_touch_span(const void* p, int bytes, int sl, uint32_t slot) {
+    const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)127, end = (uintptr_t)p + (uintptr_t)bytes;
+#pragma unroll
+    for (int k = 0; k < NI; k++) {
+        const uintptr_t a = a0 + (uintptr_t)(sl + k * LPA) * 128u;
+        l2_touch(reinterpret_cast<const void*>(a < end ? a : a0), slot);
+    }
 }
 
 // Build the agent's envelopes: segment lane m < 12 takes month m (two passes
@@ -2499,8 +2542,15 @@ __device__ __forceinline__ bool yl_dc_build_coop(const dgen_demand* D, const YSr
     const bool act = hd < 24;
     const int hq = act ? hd : 23;                                 // in-range loads for idle lanes
     bool ok = true;
+    const uint32_t tslot = l2_touch_slot();
     for (int m = 0; m < 12; m++) {
         const int d0 = c_month_start_day[m], d1 = c_month_start_day[m + 1];
+        // this month's rows (month 0) and the next month's into L2 (l2_touch)
+        for (int mm = m == 0 ? 0 : m + 1; mm <= m + 1 && mm < 12; mm++) {
+            const int a = c_month_start_day[mm] * 24, nb = (c_month_start_day[mm + 1] * 24 - a) * 4;
+            l2_touch_span<1, LPA>(src.shape + a, nb, g.sl, tslot);
+            l2_touch_span<1, LPA>(src.cf + a, nb, g.sl, tslot);
+        }
         const int pd = (int)D->wkday[m][hq], pe = (int)D->wkend[m][hq];
         uint32_t mask = act ? (1u << pd) | (1u << pe) : 0u;
 #pragma unroll
@@ -2740,7 +2790,7 @@ __device__ __forceinline__ void nb_load_days(const YSrc& src, int d0, int hd, bo
         const bool v = act && d0 + k < 365;
         b.sh[k] = v ? src.shape[h] : 0.0f;
         b.w[k] = (v && src.ts) ? (float)(src.ts[h] * src.ts_mult) : 1.0f;
-        if constexpr (SYS) b.sg[k] = v ? src.sysgen[(int64_t)(h >> 2) * src.sys_stride * 4 + (h & 3)] : 0.0;
+        if constexpr (SYS) b.sg[k] = v ? src.sysgen[(int64_t)(d0 + k) * src.sys_stride * 24 + hd] : 0.0;
         else b.cf[k] = v ? src.cf[h] : 0;
     }
 }
@@ -2770,8 +2820,25 @@ __device__ __forceinline__ bool yl_nb_build(const dgen_tariff& t, const YSrc& sr
     bool ok = true;
     constexpr int DB = NbDays<SYS>::D;
     NbDays<SYS> cur, nxt;
+    const uint32_t tslot = l2_touch_slot();
+    // month mm's rows into L2 (l2_touch): shape, the cf row or the day tiles
+    // of the system output (2 lines a day), the TS row
+    auto touch = [&](int mm) __attribute__((always_inline)) {
+        const int da = c_month_start_day[mm], nd = c_month_start_day[mm + 1] - da;
+        l2_touch_span<1, LPA>(src.shape + da * 24, nd * 96, g.sl, tslot);
+        if constexpr (SYS) {
+            const double* day = src.sysgen + (int64_t)(da + (g.sl < nd ? g.sl : 0)) * src.sys_stride * 24;
+            l2_touch(day, tslot);
+            l2_touch(reinterpret_cast<const char*>(day) + 128 - ((uintptr_t)day & 127u) + 0, tslot);
+        } else {
+            l2_touch_span<1, LPA>(src.cf + da * 24, nd * 96, g.sl, tslot);
+        }
+        if (src.ts) l2_touch_span<2, LPA>(src.ts + da * 24, nd * 192, g.sl, tslot);
+    };
+    touch(0);
     nb_load_days<SYS>(src, 0, hd, act, cur);
     for (int m = 0; m < 12; m++) {
+        if (m + 1 < 12) touch(m + 1);
         const int pd = act ? (int)t.wkday[m][hd] : 0, pe = act ? (int)t.wkend[m][hd] : 0;
         double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0};
         int n_m = 0;
@@ -3063,6 +3130,49 @@ __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double
                                               const double* __restrict__ gslots, double load_scale,
                                               const YLds& S, const Seg<LPA>& g) {
     const int P = t.P;
+    if (P <= PREG) {
+        // month lanes: lane j < 24 of the segment takes month j % 12 of the
+        // load row (j < 12) or the per-kW generation row, loads the month's 48
+        // slot sums once (4 batches of 12 in flight) and keeps every period's
+        // sum in a register, each in slot order with skipped slots as selects
+        // -- the per-cell form's additions, in its order.  The per-cell form
+        // re-read the month's 96 sums for every period (12 dependent load
+        // batches per lane at P = 4: over half of C3's k_size cycles, phase
+        // counter 12).
+        const int j = g.sl;
+        if (j < 24) {
+            const int m = j < 12 ? j : j - 12;
+            const bool gen = j >= 12;
+            const double* src = (gen ? gslots : lslots) + m * 48;
+            double acc[PREG];
+#pragma unroll
+            for (int p = 0; p < PREG; p++) acc[p] = 0.0;
+            constexpr int BB = 12;
+#pragma unroll 1
+            for (int k0 = 0; k0 < 48; k0 += BB) {
+                double v[BB];
+#pragma unroll
+                for (int k = 0; k < BB; k++) v[k] = src[k0 + k];
+                const uint8_t* sc = k0 < 24 ? t.wkday[m] + k0 : t.wkend[m] + (k0 - 24);
+#pragma unroll
+                for (int k = 0; k < BB; k++) {
+                    const int pk = (int)sc[k];
+#pragma unroll
+                    for (int p = 0; p < PREG; p++)
+                        if (p < P) acc[p] = pk == p ? acc[p] + v[k] : acc[p];
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < PREG; p++) {
+                if (p < P) {
+                    if (gen) S.G[m * S.half + p] = acc[p];
+                    else S.L[m * S.half + p] = acc[p] * load_scale;
+                }
+            }
+        }
+        wave_lds_sync();
+        return;
+    }
     for (int cell = g.sl; cell < 12 * P; cell += LPA) {
         int m = cell / P, p = cell % P;
         double la = 0.0, ga = 0.0;
@@ -3697,7 +3807,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
         src.gen_scale = 0.0;
         src.sys_stride = n_scratch;
         const int slot = A.scratch_slot[i];
-        src.sysgen = (slot >= 0) ? W.scratch + (int64_t)slot * 4 : nullptr;
+        src.sysgen = (slot >= 0) ? W.scratch + (int64_t)slot * 24 : nullptr;   // day tiles (sys_index)
         const int wr = A.wholesale_row[i];
         src.ts = (t.mo == 2 && !is_ca && wr >= 0 && T.wholesale) ? T.wholesale + (int64_t)wr * NH : nullptr;
         src.ts_mult = A.price_mult[i];

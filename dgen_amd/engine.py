@@ -217,8 +217,8 @@ class Engine:
                 raise ValueError("order must be a permutation of range(n)")
             cols = {k: np.asarray(v)[order] for k, v in cols.items()}
             # scratch slots renumbered in device order: the workspace plane is
-            # [8760][n_scratch], so neighbouring lanes then store to neighbouring
-            # slots (one line per wave-hour, not one partial line per lane)
+            # [365][n_scratch][24], so neighbouring lanes then store to
+            # neighbouring slots (a wave's day is one contiguous 12 KB run)
             sl = np.asarray(cols["scratch_slot"])
             need = sl >= 0
             renum = np.full(n, -1, dtype=np.int32)
