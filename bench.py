@@ -295,6 +295,18 @@ def main():
         ph = (ctypes.c_uint64 * 16)()
         if eng.lib.dgen_phase_read(ph, 0) == 0:
             print(json.dumps({"phase_cycles": list(ph)}), file=sys.stderr, flush=True)
+    if hasattr(eng.lib, "dgen_clk_read"):      # clock-stamp ablation builds only (scripts/make_ablations.py)
+        import ctypes
+        import numpy as _np
+        ck = (ctypes.c_uint64 * (4 * 8192))()
+        if eng.lib.dgen_clk_read(ck) == 0:
+            a = _np.frombuffer(ck, dtype=_np.uint64).reshape(4, 8192).astype(_np.float64)
+            ok = (a[3] > a[1]) & (a[2] > a[0])
+            ghz = (a[2][ok] - a[0][ok]) / (a[3][ok] - a[1][ok]) * 0.1
+            if ghz.size:
+                print(json.dumps({"hourly_clock_ghz": {"median": float(_np.median(ghz)), "p10": float(_np.percentile(ghz, 10)),
+                                                       "p90": float(_np.percentile(ghz, 90)), "blocks": int(ghz.size)}}),
+                      file=sys.stderr, flush=True)
 
     st = out["status"].cpu().numpy()
     n_bad = int(((st & 0x3B) != 0).sum())

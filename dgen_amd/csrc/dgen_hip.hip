@@ -2328,36 +2328,6 @@ __device__ __forceinline__ DcEnv dc_env_at(void* base, int64_t i) {
     return e;
 }
 
-// L2 warm-up for the hour-lane walks (yl_dc_build_coop, yl_nb_build): those
-// read an agent's rows a few days at a time and wait for each batch, so on a
-// loaded chip every batch paid an HBM / Infinity-Cache round trip (C4: ~5k of
-// the ~8k cycles per 8-day batch of the envelope build).  Before a month's
-// walk the segment touches the NEXT month's lines: lane k of the segment
-// issues one 4-B LDS-DMA into the wave's scratch slot (no VGPR held in
-// flight, nothing reads the slot) at line k of the span, so the whole span
-// comes into L2 while the current month is walked.  vmcnt retires in issue
-// order: a batch issued after the touch waits for it too, but both were
-// issued together and overlap.  The compiler does not see the DMA, which only
-// makes its own vmcnt waits stricter.
-__device__ __forceinline__ uint32_t l2_touch_slot() {
-    __shared__ uint32_t touch_slot[WAVE];
-    return (uint32_t)(size_t)(lds_ptr_t)(reinterpret_cast<char*>(touch_slot));
-}
-__device__ __forceinline__ void l2_touch(const void* g, uint32_t slot) {
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" :: "v"(g), "s"(slot) : "memory", "m0");
-}
-// the lines of [p, p + bytes) (bytes <= NI x LPA x 128): lane sl of the
-// segment takes lines sl, sl + LPA, ...; a lane past the span touches its first line
-template <int NI, int LPA>
-__device__ __forceinline__ void l2_touch_span(const void* p, int bytes, int sl, uint32_t slot) {
-    const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)127, end = (uintptr_t)p + (uintptr_t)bytes;
-#pragma unroll
-    for (int k = 0; k < NI; k++) {
-        const uintptr_t a = a0 + (uintptr_t)(sl + k * LPA) * 128u;
-        l2_touch(reinterpret_cast<const void*>(a < end ? a : a0), slot);
-    }
-}
-
 // Build the agent's envelopes: segment lane m < 12 takes month m (two passes
 // over the month per demand period present).  Returns true when every group
 // fit in DC_NL lines (segment-uniform).
@@ -2542,15 +2512,8 @@ __device__ __forceinline__ bool yl_dc_build_coop(const dgen_demand* D, const YSr
     const bool act = hd < 24;
     const int hq = act ? hd : 23;                                 // in-range loads for idle lanes
     bool ok = true;
-    const uint32_t tslot = l2_touch_slot();
     for (int m = 0; m < 12; m++) {
         const int d0 = c_month_start_day[m], d1 = c_month_start_day[m + 1];
-        // this month's rows (month 0) and the next month's into L2 (l2_touch)
-        for (int mm = m == 0 ? 0 : m + 1; mm <= m + 1 && mm < 12; mm++) {
-            const int a = c_month_start_day[mm] * 24, nb = (c_month_start_day[mm + 1] * 24 - a) * 4;
-            l2_touch_span<1, LPA>(src.shape + a, nb, g.sl, tslot);
-            l2_touch_span<1, LPA>(src.cf + a, nb, g.sl, tslot);
-        }
         const int pd = (int)D->wkday[m][hq], pe = (int)D->wkend[m][hq];
         uint32_t mask = act ? (1u << pd) | (1u << pe) : 0u;
 #pragma unroll
@@ -2820,25 +2783,8 @@ __device__ __forceinline__ bool yl_nb_build(const dgen_tariff& t, const YSrc& sr
     bool ok = true;
     constexpr int DB = NbDays<SYS>::D;
     NbDays<SYS> cur, nxt;
-    const uint32_t tslot = l2_touch_slot();
-    // month mm's rows into L2 (l2_touch): shape, the cf row or the day tiles
-    // of the system output (2 lines a day), the TS row
-    auto touch = [&](int mm) __attribute__((always_inline)) {
-        const int da = c_month_start_day[mm], nd = c_month_start_day[mm + 1] - da;
-        l2_touch_span<1, LPA>(src.shape + da * 24, nd * 96, g.sl, tslot);
-        if constexpr (SYS) {
-            const double* day = src.sysgen + (int64_t)(da + (g.sl < nd ? g.sl : 0)) * src.sys_stride * 24;
-            l2_touch(day, tslot);
-            l2_touch(reinterpret_cast<const char*>(day) + 128 - ((uintptr_t)day & 127u) + 0, tslot);
-        } else {
-            l2_touch_span<1, LPA>(src.cf + da * 24, nd * 96, g.sl, tslot);
-        }
-        if (src.ts) l2_touch_span<2, LPA>(src.ts + da * 24, nd * 192, g.sl, tslot);
-    };
-    touch(0);
     nb_load_days<SYS>(src, 0, hd, act, cur);
     for (int m = 0; m < 12; m++) {
-        if (m + 1 < 12) touch(m + 1);
         const int pd = act ? (int)t.wkday[m][hd] : 0, pe = act ? (int)t.wkend[m][hd] : 0;
         double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0};
         int n_m = 0;
@@ -3130,49 +3076,6 @@ __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double
                                               const double* __restrict__ gslots, double load_scale,
                                               const YLds& S, const Seg<LPA>& g) {
     const int P = t.P;
-    if (P <= PREG) {
-        // month lanes: lane j < 24 of the segment takes month j % 12 of the
-        // load row (j < 12) or the per-kW generation row, loads the month's 48
-        // slot sums once (4 batches of 12 in flight) and keeps every period's
-        // sum in a register, each in slot order with skipped slots as selects
-        // -- the per-cell form's additions, in its order.  The per-cell form
-        // re-read the month's 96 sums for every period (12 dependent load
-        // batches per lane at P = 4: over half of C3's k_size cycles, phase
-        // counter 12).
-        const int j = g.sl;
-        if (j < 24) {
-            const int m = j < 12 ? j : j - 12;
-            const bool gen = j >= 12;
-            const double* src = (gen ? gslots : lslots) + m * 48;
-            double acc[PREG];
-#pragma unroll
-            for (int p = 0; p < PREG; p++) acc[p] = 0.0;
-            constexpr int BB = 12;
-#pragma unroll 1
-            for (int k0 = 0; k0 < 48; k0 += BB) {
-                double v[BB];
-#pragma unroll
-                for (int k = 0; k < BB; k++) v[k] = src[k0 + k];
-                const uint8_t* sc = k0 < 24 ? t.wkday[m] + k0 : t.wkend[m] + (k0 - 24);
-#pragma unroll
-                for (int k = 0; k < BB; k++) {
-                    const int pk = (int)sc[k];
-#pragma unroll
-                    for (int p = 0; p < PREG; p++)
-                        if (p < P) acc[p] = pk == p ? acc[p] + v[k] : acc[p];
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < PREG; p++) {
-                if (p < P) {
-                    if (gen) S.G[m * S.half + p] = acc[p];
-                    else S.L[m * S.half + p] = acc[p] * load_scale;
-                }
-            }
-        }
-        wave_lds_sync();
-        return;
-    }
     for (int cell = g.sl; cell < 12 * P; cell += LPA) {
         int m = cell / P, p = cell % P;
         double la = 0.0, ga = 0.0;

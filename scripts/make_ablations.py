@@ -183,6 +183,25 @@ VARIANTS = {
     # doubled: the occupancy cost alone) / without its mixed-entry stores
     "hb_nb_off": [("        put_nb = put_sys && mo2 && !ts_on;", "        put_nb = false && put_sys && mo2 && !ts_on;")],
     "hb_nb_nostore": [("                            nb_ent[n_m] = e;", "                            (void)e;")],
+    # --- k_hourly_batt attribution on the current source (round 4; timing only,
+    # results wrong by construction except hb_w3) ---------------------------
+    # the three hourly-plane stores sunk (the day read-back then waits for the
+    # DMA alone): the scan's VALU / LDS part
+    "hb_nostores": [("                        st_f32x4(ob + q16, off16, qb);\n"
+                     "                        st_f32x4(op + q16, off16, qp);\n"
+                     "                        st_f32x4(ow + q16, off16, qw);\n",
+                     "                        asm volatile(\"\" :: \"v\"(qb[0]), \"v\"(qb[1]), \"v\"(qb[2]), \"v\"(qb[3]),\n"
+                     "                                     \"v\"(qp[0]), \"v\"(qp[1]), \"v\"(qp[2]), \"v\"(qp[3]));\n"
+                     "                        asm volatile(\"\" :: \"v\"(qw[0]), \"v\"(qw[1]), \"v\"(qw[2]), \"v\"(qw[3]));\n"),
+                    ("day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r)", "day_read<0>(dlane, r)")],
+    # the next-day DMA not waited for (LDS read races it): the cost of the
+    # in-order vmcnt wait, which also waits for every store older than the DMA
+    "hb_dma_nowait": [("day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r)", "day_read<60>(dlane, r)")],
+    # the day's deficits / sort / target skipped: the hour loop and its stores
+    # 3 waves per SIMD (VGPR cap 168)
+    "hb_w3b": [("__launch_bounds__(BLOCK, ROLL ? 1 : 2)\nk_hourly_batt(", "__launch_bounds__(BLOCK, ROLL ? 1 : 3)\nk_hourly_batt(")],
+    "hb_notarget": [("            } else if (has_batt) {\n                // the day's deficits d_h",
+                     "            } else if (false) {\n                // the day's deficits d_h")],
     # per-agent kernels' block size (k_hourly_batt: waves per block)
     "block64": [("constexpr int BLOCK = 128;", "constexpr int BLOCK = 64;"),
                  ("__launch_bounds__(BLOCK, 2)\nk_hourly_batt(", "__launch_bounds__(BLOCK, 8)\nk_hourly_batt(")],
@@ -228,6 +247,24 @@ VARIANTS = {
     "kf_nb_none": [("            nb_ok = yl_nb_build(t, src, s_lo, s_hi, nbp, S, g);\n            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S);",
                     "            nb_ok = true; wb = 1000.0 * s_y + (double)(size_t)nbp * 0.0;")],
 }
+
+# in-kernel clock of k_hourly_batt (MI355X_MICROARCH.md DVFS item 6): thread 0 of
+# each block stamps s_memtime / s_memrealtime at its start and after its month
+# loop into a buffer of its own; bench.py prints the median clock (run with
+# --hb-split 1 so the last launch owns every stamp)
+CLK = [("constexpr int HB_DAY_BYTES = 12 * 1024;",
+        "__device__ unsigned long long g_clk[4][8192];\nconstexpr int HB_DAY_BYTES = 12 * 1024;"),
+       ("    WsLayout W = ws_layout(ws, n);\n    // battery-case bins",
+        "    WsLayout W = ws_layout(ws, n);\n"
+        "    if (threadIdx.x == 0 && blockIdx.x < 8192) { g_clk[0][blockIdx.x] = __builtin_amdgcn_s_memtime();"
+        " g_clk[1][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); }\n    // battery-case bins"),
+       ("    if (m_hi < 12) {\n        W.carry[i] = soc;",
+        "    if (threadIdx.x == 0 && blockIdx.x < 8192) { g_clk[2][blockIdx.x] = __builtin_amdgcn_s_memtime();"
+        " g_clk[3][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); }\n    if (m_hi < 12) {\n        W.carry[i] = soc;"),
+       ('extern "C" {', 'extern "C" {\nint32_t dgen_clk_read(void* dst) { return (int32_t)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_clk), sizeof(g_clk)); }')]
+VARIANTS["hb_clk"] = CLK
+VARIANTS["hb_nostores_clk"] = VARIANTS["hb_nostores"] + CLK
+VARIANTS["hb_notarget_clk"] = VARIANTS["hb_notarget"] + CLK
 
 
 def main():
