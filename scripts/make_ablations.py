@@ -266,6 +266,39 @@ VARIANTS["hb_clk"] = CLK
 VARIANTS["hb_nostores_clk"] = VARIANTS["hb_nostores"] + CLK
 VARIANTS["hb_notarget_clk"] = VARIANTS["hb_notarget"] + CLK
 
+# the three plane stores kept but always to the launch's first hour-quad row
+# (48 MB at 1M agents: cache-resident, no HBM write stream): store issue vs HBM
+VARIANTS["hb_stores_l2"] = [("                        st_f32x4(ow + q16, off16, qw);\n                        q16 += row16;\n",
+                             "                        st_f32x4(ow + q16, off16, qw);\n")]
+VARIANTS["hb_stores_l2_clk"] = VARIANTS["hb_stores_l2"] + CLK
+
+# day counters with slot 13 / 14 = lane-days / wave-days whose battery holds
+# no deliverable energy at the day's first hour (avail = 0: the day's target
+# cannot discharge anything, so its value does not matter)
+VARIANTS["phase_empty"] = [("#define DGEN_PHASE_PROF 0", "#define DGEN_PHASE_PROF 1"),
+                           ("#define DGEN_DAY_COUNTERS 0", "#define DGEN_DAY_COUNTERS 1"),
+                           ("                    const bool fits = need <= avail;",
+                            "                    const bool fits = !(avail > 0.0); (void)need;")]
+
+# C3 k_size attribution by doubling (results unchanged, the time difference is
+# one copy's cost): the NEM bins build twice per tariff / the objective twice
+# per Brent evaluation
+VARIANTS["ks_bins_x2"] = [("        PH_T0(tn);\n        wave_lds_sync();\n        yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);\n",
+                           "        PH_T0(tn);\n        wave_lds_sync();\n        yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);\n"
+                           "        yl_build_bins(t, c.lslots, c.gslots, c.load_scale, c.S, c.g);\n")]
+VARIANTS["ks_nosys_x2"] = [("        c.wo1 = yl_bill_nem_nosys(t, c.S, c.yearend, c.g);\n",
+                            "        c.wo1 = yl_bill_nem_nosys(t, c.S, c.yearend, c.g);\n"
+                            "        c.wo1 = yl_bill_nem_nosys(t, c.S, c.yearend, c.g);\n")]
+VARIANTS["ks_obj_x2"] = [("            return yl_objective<LPA, DC, NET, PK>(c, x);",
+                          "            (void)yl_objective<LPA, DC, NET, PK>(c, x);\n            return yl_objective<LPA, DC, NET, PK>(c, x);")]
+
+# k_size (bins-only and net-billing instantiations) at 4 waves per SIMD
+VARIANTS["ks_occ4"] = [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? 2 : 4)")]
+
+# yl_bill_nb: staged entries read per group ahead of the billed group
+VARIANTS["nbu2"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 2")]
+VARIANTS["nbu8"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 8")]
+
 
 def main():
     os.makedirs(OUT, exist_ok=True)
