@@ -40,7 +40,7 @@ DCR_HEAD = 2 * 12 * DCP * 8 + 64  # a demand record's per-(month, period) max lo
 
 
 def scratch_paths(cols, recs, tariff_final, *, battery=True, skip_dc=True, nb_scan=True,
-                  dcr_on=True, has_wholesale=True):
+                  dcr_on=True, has_wholesale=True, ts_scan=False):
     """Which scratch-slot agents move the battery case's f64 system-output
     plane and which hand k_batt_finance a compact record instead, per agent in
     the order of `cols` (dgen_hip.hip k_hourly_batt: put_sys / put_nb / put_dcr
@@ -48,7 +48,9 @@ def scratch_paths(cols, recs, tariff_final, *, battery=True, skip_dc=True, nb_sc
     storage switch, outputs["tariff_final"]); `recs` the engine's tariff
     records (Engine.tariff_records).  Returns (plane, nb_rec, dcr_rec, mo2, P)
     boolean / int arrays.  Agents whose record overflowed (the repair pass
-    writes their plane) are counted as record agents: a lower bound."""
+    writes their plane) are counted as record agents: a lower bound.
+    ts_scan: the TS sell-rate agents' split is built in their own scan
+    (k_hourly_batt<TS>; dgen_size_agents' ts_split), so they hand a record too."""
     tf = np.asarray(tariff_final, np.int64)
     sl = np.asarray(cols["scratch_slot"]) >= 0
     mo, dc, unit = recs["mo"][tf], recs["dc"][tf], recs["unit"][tf]
@@ -58,13 +60,13 @@ def scratch_paths(cols, recs, tariff_final, *, battery=True, skip_dc=True, nb_sc
     ca = (np.asarray(cols["flags"]) & 2) != 0
     ts_on = (mo == 2) & ~ca & (np.asarray(cols["wholesale_row"]) >= 0) & bool(has_wholesale)
     put_sys = (mo2 | has_dc) & sl & bool(battery)
-    put_nb = put_sys & mo2 & ~ts_on & bool(nb_scan)
+    put_nb = put_sys & mo2 & (~ts_on | bool(ts_scan)) & bool(nb_scan)
     put_dcr = put_sys & has_dc & bool(dcr_on)
     skip = (put_nb & ~has_dc) | (put_dcr & ~mo2)
     return put_sys & ~skip, put_nb, put_dcr, mo2, P
 
 
-def algorithmic_bytes(cols, hourly: bool, battery: bool, paths=None, recs=None):
+def algorithmic_bytes(cols, hourly: bool, battery: bool, paths=None, recs=None, ts_rows: int = 0):
     """ALGORITHMIC HBM bytes per step of each sizing kernel for this population
     (DESIGN.md section 5): the bytes the step cannot avoid moving.  Profile
     rows are shared: every distinct load-shape / cf row the batch uses is read
@@ -90,7 +92,9 @@ def algorithmic_bytes(cols, hourly: bool, battery: bool, paths=None, recs=None):
                       agents read their plane and their distinct load rows,
                       the record agents their record's sums / maxima
     `paths` = scratch_paths(...) after a run; without it every scratch-slot
-    agent is taken to write and read the plane (an upper bound)."""
+    agent is taken to write and read the plane (an upper bound).  `ts_rows`:
+    the distinct TS rows the scan reads for the agents whose split it builds
+    with the hourly sell rate (f64, 70 KB each)."""
     n = len(cols["load_kwh"])
     lr, cr = np.asarray(cols["load_row"]), np.asarray(cols["cf_row"])
     yearly = 8.0 * (np.asarray(cols["econ_life"], np.int64) + 1).sum()
@@ -108,7 +112,7 @@ def algorithmic_bytes(cols, hourly: bool, battery: bool, paths=None, recs=None):
     k_size = slots + n * 24 * 8 + 4 * yearly + rows_h
     bins = float((12 * P * 16)[~mo2].sum())              # NEM agents' (load, system) pairs
     recb = float((12 * P * 4 * 8)[nbr].sum() + 64 * nbr.sum() + DCR_HEAD * dcr.sum())
-    k_hourly = rows + n * 16 * 8 + bins + recb
+    k_hourly = rows + n * 16 * 8 + bins + recb + int(ts_rows) * 8 * 8760
     if hourly:
         k_hourly += n * 3 * PLANE_BYTES
     if battery:
@@ -320,11 +324,22 @@ def main():
     dc_batch = eng.tables.n_demand > 0 and (not pop.skip_demand_charges or eng.tables.peak_units != 0)
     hp = max(1, min(int(recs["P"].max()), 12))
     nb_lds = 8 * 4 * hp * 128 + (16 * (eng.tables.max_dc_periods or 8) * 128 if dc_batch else 0) + 2 * 12 * 1024   # dgen_size_agents' gate
-    paths = scratch_paths(dcols, recs, out["tariff_final"].cpu().numpy(), battery=not args.no_batt,
-                          skip_dc=pop.skip_demand_charges, nb_scan=batch.nb_scan and nb_lds <= 65536,
-                          dcr_on=dc_batch and args.replan_hours != 1,
-                          has_wholesale=bool(eng.tables.wholesale))
-    nbytes = algorithmic_bytes(dcols, not args.no_hourly, not args.no_batt, paths)
+    nb_on = batch.nb_scan and nb_lds <= 65536
+    dcr_on = dc_batch and args.replan_hours != 1
+    # dgen_size_agents' ts_split gate (12 KB more day buffer per wave)
+    ts_scan = (nb_on and bool(eng.tables.wholesale) and not dcr_on and args.replan_hours != 1 and
+               not args.no_hourly and
+               os.environ.get("DGEN_TS_SCAN", "1") != "0" and nb_lds + 2 * 12 * 1024 <= 65536)
+    tf_dev = out["tariff_final"].cpu().numpy()
+    paths = scratch_paths(dcols, recs, tf_dev, battery=not args.no_batt,
+                          skip_dc=pop.skip_demand_charges, nb_scan=nb_on, dcr_on=dcr_on,
+                          has_wholesale=bool(eng.tables.wholesale), ts_scan=ts_scan)
+    ts_rows = 0
+    if ts_scan:
+        wr = np.asarray(dcols["wholesale_row"])
+        ts_ag = paths[1] & (recs["mo"][tf_dev] == 2) & ((np.asarray(dcols["flags"]) & 2) == 0) & (wr >= 0)
+        ts_rows = int(np.unique(wr[ts_ag]).size) if ts_ag.any() else 0
+    nbytes = algorithmic_bytes(dcols, not args.no_hourly, not args.no_batt, paths, ts_rows=ts_rows)
     traffic_pa, valu_busy, traffic_src = pmc_traffic(args.pmc_dir, args.config)
     # launches per step: k_hourly_batt sweeps the year in month-segment launches
     # per pipeline chunk; the year-lane kernels launch once per chunk

@@ -878,11 +878,20 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 // agent bills hourly imports: the bins path only, no system-output plane and
 // no per-hour net-billing branch (an agent that would need one is flagged
 // DGEN_ST_SCRATCH, as in every form).
-template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR, bool LOSS = false, bool NEM = false>
-__global__ void __launch_bounds__(BLOCK, ROLL ? 1 : 2)
+// TS (with NB): the scan also builds the split of the agents billed net with
+// the hourly TS sell rate (non-CA, metering option 2): their exported kWh are
+// weighted by the hour's float32 sell rate, so the wave DMAs the agents' TS
+// rows day by day next to the profile rows (12 KB more LDS per wave: this form
+// runs one wave per SIMD and is launched for those agents alone, ts_mode 2,
+// beside the NB form over the rest, ts_mode 1) and the record holds full
+// 24-B entries (load, generation, weight, period; flag 4).
+// ts_mode: 0 every agent; 1 the agents that can bill the TS rate (a scratch
+// slot and a wholesale row, non-CA: engine.path_class 2) skipped; 2 only those.
+template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR, bool LOSS = false, bool NEM = false, bool TS = false>
+__global__ void __launch_bounds__(BLOCK, (ROLL || TS) ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
-              int repair, char* dcr, int dc_nq, int dcr_cap) {
+              int repair, char* dcr, int dc_nq, int dcr_cap, int ts_mode = 0) {
     // agents [i0, i1) of a batch of n (row stride of every plane stays n),
     // months [m_lo, m_hi) of the year: the year is swept in month segments,
     // one launch each, so that every resident wave works on the same weeks
@@ -891,6 +900,11 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     int64_t i = i0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= i1) return;
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
+    if (ts_mode) {
+        const bool ts_cap = A.scratch_slot[i] >= 0 && A.wholesale_row[i] >= 0 && (A.flags[i] & 2) == 0 &&
+                            T.wholesale != nullptr;
+        if (ts_cap != (ts_mode == 2)) return;
+    }
     // repair pass: only the agents whose scan-built split (repair bit 1) or
     // demand record (bit 2) overflowed and whose system-output plane was
     // therefore not written (flag 2) run again, with the plane; every other
@@ -955,12 +969,14 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // (import) and bins2 (export), the current period's in registers.
     bool put_nb = false;
     bool nb_over = false;        // a month's mixed hours exceeded nb_cap
+    bool nb_full = false;        // TS: full entries with the hour's sell weight
     double nb_lo = 0.0, nb_hi = 0.0;
     NbRec nbr{nullptr, nullptr, nullptr};
     if constexpr (NB) {
         const bool is_ca = (A.flags[i] & 2) != 0;
         const bool ts_on = t.mo == 2 && !is_ca && A.wholesale_row[i] >= 0 && T.wholesale != nullptr;
-        put_nb = put_sys && mo2 && !ts_on && nb_cap > 0;
+        put_nb = put_sys && mo2 && (TS || !ts_on) && nb_cap > 0;
+        nb_full = TS && ts_on && put_nb;
         if (put_nb) {
             const int N = A.econ_life[i];
             const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
@@ -1057,16 +1073,32 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     const uint32_t dbase = (uint32_t)(size_t)(lds_ptr_t)(reinterpret_cast<char*>(dyn_lds) +
                            (size_t)(NB ? 32 : 16) * lds_half(T.max_periods) * BLOCK +
                            (DCR ? (size_t)16 * dc_nq * BLOCK : 0) +
-                           (size_t)(threadIdx.x / 64) * HB_DAY_BYTES);
+                           (size_t)(threadIdx.x / 64) * HB_DAY_BYTES * (TS ? 2 : 1));
     const uint32_t dbase_s = __builtin_amdgcn_readfirstlane(dbase);
     const uint32_t dlane = dbase_s + (threadIdx.x & 63u) * 16u;
+    // TS: the lane's chunks of the TS day (a pointer into dyn_lds: ds_read)
+    const char* const tsl = reinterpret_cast<const char*>(dyn_lds) + (size_t)(NB ? 32 : 16) * lds_half(T.max_periods) * BLOCK +
+                            (DCR ? (size_t)16 * dc_nq * BLOCK : 0) +
+                            (size_t)(threadIdx.x / 64) * HB_DAY_BYTES * 2 + HB_DAY_BYTES + (threadIdx.x & 63u) * 16u;
+    (void)tsl;
+    // TS: the agent's TS row (a path-2 agent always has one), its day in 12
+    // more chunks after the profile rows' (2 hours each)
+    const double* __restrict__ tsp = TS ? T.wholesale + (int64_t)(A.wholesale_row[i] >= 0 ? A.wholesale_row[i] : 0) * NH
+                                        : nullptr;
+    const double ts_mult = TS ? A.price_mult[i] : 1.0;
     auto day_dma = [&](int dd) {
 #pragma unroll
         for (int q = 0; q < 6; q++) {
             lds_dma16(shp + dd * 24 + 4 * q, dbase_s + q * 1024u);
             lds_dma16(cfp + dd * 24 + 4 * q, dbase_s + (6 + q) * 1024u);
         }
+        if constexpr (TS) {
+#pragma unroll
+            for (int q = 0; q < 12; q++) lds_dma16(tsp + dd * 24 + 2 * q, dbase_s + HB_DAY_BYTES + q * 1024u);
+        }
     };
+    float tw[24];                  // TS: the day's sell weights (float)(rate x price multiplier)
+    (void)tw;
     // settle every load before the day loop: the waitcnt pass merges the
     // loop entry with the back edge, and a pending entry load would put a
     // vmcnt wait (which also drains the in-flight day DMA) into hour 0
@@ -1180,6 +1212,17 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     else mfloor = target;
                 }
                 day_reread(dlane, r);
+            }
+            if constexpr (TS) {   // the day's weights, before the next-day DMA reuses the buffer
+                f64x2 tv[12];
+#pragma unroll
+                for (int q = 0; q < 12; q++) tv[q] = *reinterpret_cast<const f64x2*>(tsl + q * 1024u);
+#pragma unroll
+                for (int q = 0; q < 12; q++) {
+                    tw[2 * q] = (float)(tv[q].x * ts_mult);
+                    tw[2 * q + 1] = (float)(tv[q].y * ts_mult);
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): the reads are done
             }
             if (!ROLL && d < d_last) day_dma(d + 1);            // after the last read of the buffer
             const double ls2 = opaque(ls), cs2 = opaque(cs6), cl2 = opaque(cl6);
@@ -1298,15 +1341,27 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     const bool exq = !imp && fmax(vlo, vhi) < -slack;      // exports at every s
                     bacc.x += imp ? ld : 0.0;
                     bacc.y += imp ? gk : 0.0;
-                    xacc.x += exq ? gk : 0.0;
-                    xacc.y += exq ? ld : 0.0;
+                    // the export side x the hour's sell weight (yl_nb_build<true>'s
+                    // products; 1 without a TS rate: gk x 1.0 is gk)
+                    const double wd = nb_full ? (double)tw[hh] : 1.0;
+                    xacc.x += exq ? gk * wd : 0.0;
+                    xacc.y += exq ? ld * wd : 0.0;
                     if (!imp && !exq) {
                         if (n_m < nb_cap) {
-                            NbEntC e;
-                            e.g = gk;
-                            e.sh = r.s[hh];
-                            e.p = p;
-                            nb_ent[n_m] = e;
+                            if (TS && nb_full) {
+                                NbEnt e;
+                                e.L = ld;
+                                e.g = gk;
+                                e.w = tw[hh];
+                                e.p = p;
+                                nbr.ent[m * NB_CAPM + n_m] = e;
+                            } else {
+                                NbEntC e;
+                                e.g = gk;
+                                e.sh = r.s[hh];
+                                e.p = p;
+                                nb_ent[n_m] = e;
+                            }
                         }
                         n_m++;
                     }
@@ -1372,7 +1427,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
         int fl = 0;
         if (put_nb) {
             for (int k = 0; k < 12; k++) nb_over = nb_over || nbr.cnt[k] > NB_CAPM;
-            fl = !nb_over ? 1 : (skip_plane ? 2 : 0);
+            fl = !nb_over ? (nb_full ? 4 : 1) : (skip_plane ? 2 : 0);
         }
         nbr_flag(ws_nb(ws, n, n_scratch) + (size_t)slot * NB_BYTES) = fl;
     }
@@ -3763,8 +3818,11 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             src.gen_scale = 1.0;
             char* nbp = nbws + (size_t)slot * NB_BYTES;
             PH_T0(tb);
-            const bool scan_rec = nb_scan && nbr_flag(nbp) == 1;
-            if (scan_rec) {    // this step's k_hourly_batt built it in its scan (compact entries)
+            // this step's k_hourly_batt built it in its scan: compact entries
+            // (flag 1) or, for a TS sell rate, full 24-B entries (flag 4)
+            const int nb_fl = nbr_flag(nbp);
+            const bool scan_rec = nb_scan && (nb_fl == 1 || nb_fl == 4);
+            if (scan_rec) {
                 const NbRec R = nb_rec(nbp);
                 nb_ok = g.first(g.sl < 12 && R.cnt[g.sl] > NB_CAPM) < 0;
             } else {
@@ -3772,7 +3830,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
             }
             PH_ADD(5, tb, g.sl == 0);
             PH_T0(te);
-            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S, g, scan_rec);
+            if (nb_ok) wb = yl_bill_nb(t, src, s_y, nbp, S, g, scan_rec && nb_fl == 1);
             PH_ADD(6, te, g.sl == 0);
         }
         if (!nb_ok) wb = yl_bill_net(t, src, s_y, true, S);
@@ -4348,8 +4406,11 @@ struct dgen_ctx {
     static constexpr int MAXSPLIT = 4;
     hipStream_t sx[MAXSPLIT - 1];       // the hourly scan's other parts' streams
     hipEvent_t hb_join[MAXSPLIT - 1];
+    hipStream_t st[MAXSPLIT];           // each part's TS scan (k_hourly_batt<TS>), beside its NB scan
+    hipEvent_t ts_join[MAXSPLIT];
     int hb_split;      // parts of a chunk's hourly scan, each on its own stream (1..4; DGEN_HB_SPLIT)
     int hb_nem;        // 1: batches without scratch slots run the bins-only scan (DGEN_HB_NEM=0: off)
+    int ts_scan;       // 1: the TS sell-rate agents' split built in their own scan (DGEN_TS_SCAN=0: off, A/B)
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
     int battery;       // PV+battery forward run (dgen_set_battery)
@@ -4449,11 +4510,17 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
         c->hb_split = (v && v[0] >= '1' && v[0] <= '4') ? v[0] - '0' : DGEN_DEFAULT_HOURLY_SPLIT;
         const char* w = getenv("DGEN_HB_NEM");
         c->hb_nem = (w && w[0] == '0') ? 0 : 1;
+        const char* x = getenv("DGEN_TS_SCAN");
+        c->ts_scan = (x && x[0] == '0') ? 0 : 1;
     }
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
     for (int k = 0; k < dgen_ctx::MAXSPLIT - 1 && e == hipSuccess; k++) {
         e = hipStreamCreateWithFlags(&c->sx[k], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&c->hb_join[k], hipEventDisableTiming);
+    }
+    for (int k = 0; k < dgen_ctx::MAXSPLIT && e == hipSuccess; k++) {
+        e = hipStreamCreateWithFlags(&c->st[k], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ts_join[k], hipEventDisableTiming);
     }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->join, hipEventDisableTiming);
@@ -4476,6 +4543,7 @@ int32_t dgen_close(dgen_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->s2);
     for (int k = 0; k < dgen_ctx::MAXSPLIT - 1; k++) (void)hipStreamSynchronize(c->sx[k]);
+    for (int k = 0; k < dgen_ctx::MAXSPLIT; k++) (void)hipStreamSynchronize(c->st[k]);
     for (int r = 0; r < dgen_ctx::RING; r++)
         for (int j = 0; j < dgen_ctx::MAXCH; j++)
             for (int k = 0; k < 5; k++) (void)hipEventDestroy(c->ev[r][j][k]);
@@ -4485,6 +4553,10 @@ int32_t dgen_close(dgen_ctx* c) {
     for (int k = 0; k < dgen_ctx::MAXSPLIT - 1; k++) {
         (void)hipStreamDestroy(c->sx[k]);
         (void)hipEventDestroy(c->hb_join[k]);
+    }
+    for (int k = 0; k < dgen_ctx::MAXSPLIT; k++) {
+        (void)hipStreamDestroy(c->st[k]);
+        (void)hipEventDestroy(c->ts_join[k]);
     }
     if (c->dc_buf) (void)hipFree(c->dc_buf);
     if (c->dcr_buf) (void)hipFree(c->dcr_buf);
@@ -4649,6 +4721,18 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK * (nb_scan ? 2 : 1) +
                        lds_dcr + (size_t)(BLOCK / 64) * HB_DAY_BYTES;
     const int rep_mask = (nb_scan ? 1 : 0) | (dcr_on ? 2 : 0);
+    // TS sell-rate agents' split built in a scan of their own (k_hourly_batt<TS>,
+    // launched beside the NB scan over the rest; 12 KB more of day buffer per
+    // wave, so it runs one wave per SIMD): batches with a wholesale table, no
+    // demand records, daily plan, hourly planes requested.  With the planes the
+    // NB scan is clock-bound and the TS blocks fill in around it (national 200k:
+    // 21.38 -> 20.22 ms per step, k_batt_finance 3.54 -> 1.11 ms); without them
+    // (the model-year loop's sizing call) the one-wave form's latency shows
+    // (C5 2.5M: k_hourly_batt 56 -> 98 ms against k_batt_finance 47 -> 15 ms),
+    // and the plane pass stays
+    const size_t lds_ts = lds + (size_t)(BLOCK / 64) * HB_DAY_BYTES;
+    const bool ts_split = nb_scan && T->wholesale != nullptr && !dcr_on && c->ts_scan && lds_ts <= 65536 &&
+                          c->cfg.batt_update_hours != 1 && hourly;
     // two agents per wave when every analysis period fits 32 lanes, unless the
     // build guard withdrew that kernel's 32-lane instantiation (DGEN_NO2_*)
     const bool fits32 = A->max_years >= 1 && A->max_years <= 32;
@@ -4726,10 +4810,16 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         // no scratch slot in the batch: the bins-only scan (DGEN_HB_NEM=0 disables, A/B)
         const bool nem_only = n_scratch == 0 && c->hb_nem;
         for (int part = 1; part < nparts; part++) HIP_TRY(hipStreamWaitEvent(c->sx[part - 1], e[1], 0));
+        // the TS agents' scans run on streams of their own beside the NB scans
+        // (disjoint agents): their one-wave-per-SIMD blocks fill in around the
+        // NB blocks instead of queueing behind them
+        if (ts_split)
+            for (int part = 0; part < nparts; part++) HIP_TRY(hipStreamWaitEvent(c->st[part], e[1], 0));
         for (int part = 0; part < nparts; part++) {
         const int64_t ha = i0 + part * psz < i1 ? i0 + part * psz : i1;
         const int64_t hb = part == nparts - 1 ? i1 : (ha + psz < i1 ? ha + psz : i1);
         hipStream_t hs = part == 0 ? s2 : c->sx[part - 1];
+        hipStream_t hts = c->st[part];
         if (hb <= ha) continue;
         const dim3 hgrid((unsigned)((hb - ha + BLOCK - 1) / BLOCK));
         for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
@@ -4739,7 +4829,13 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         if (nb_scan && !(REP) && dcr_on && !(R))                                                  \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, true>), hgrid, block, lds, hs, *T, *A, *O, \
                                c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, dcr, dc_nq, c->dcr_enable); \
-        else if (nb_scan && !(REP))                                                               \
+        else if (nb_scan && !(REP) && ts_split && !(R)) {                                         \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, false>), hgrid, block, lds, hs, *T, *A, *O, \
+                               c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0, 1); \
+            hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, false, false, false, true>), hgrid, block, lds_ts, \
+                               hts, *T, *A, *O, c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, \
+                               nullptr, 0, 0, 2);                                                  \
+        } else if (nb_scan && !(REP))                                                             \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true, R, false>), hgrid, block, lds, hs, *T, *A, *O, c->cfg, \
                                n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0); \
         else if (!(REP) && dcr_on && !(R))                                                        \
@@ -4772,10 +4868,17 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             HIP_TRY(hipEventRecord(c->hb_join[part - 1], c->sx[part - 1]));
             HIP_TRY(hipStreamWaitEvent(s2, c->hb_join[part - 1], 0));
         }
+        if (ts_split)
+            for (int part = 0; part < nparts; part++) {
+                HIP_TRY(hipEventRecord(c->ts_join[part], c->st[part]));
+                HIP_TRY(hipStreamWaitEvent(s2, c->ts_join[part], 0));
+            }
         // repair pass (agents whose scan-built split or demand record
         // overflowed: their plane), whole chunk on s2
         const int64_t ha = i0, hb = i1;
         hipStream_t hs = s2;
+        hipStream_t hts = s2;           // (the repair pass never launches the TS form)
+        (void)hts;
         const dim3 hgrid((unsigned)((m + BLOCK - 1) / BLOCK));
         for (int m0 = 0; rep_mask && m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;

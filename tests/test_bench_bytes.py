@@ -72,3 +72,19 @@ def test_algorithmic_bytes_counts_the_plane_only_for_its_writers():
     nob = bench.algorithmic_bytes(cols, True, False, bench.scratch_paths(cols, _recs(), tf, battery=False))
     assert nob["k_batt_finance"] == 0.0
     assert nob["k_hourly_batt"] < exact["k_hourly_batt"]
+
+
+def test_scratch_paths_ts_scan():
+    # with the TS agents' own scan (dgen_size_agents' ts_split) a non-CA net-billing
+    # agent with a wholesale row hands a record too; a CA one always did
+    tf = np.array([1, 1, 4])
+    cols = _cols(tf, [0, 1, 2], ca=[0, 1, 0], ws=[5, 5, 5])
+    plane, nb, *_ = bench.scratch_paths(cols, _recs(), tf, skip_dc=True)
+    assert plane.tolist() == [True, False, False] and nb.tolist() == [False, True, True]
+    plane, nb, *_ = bench.scratch_paths(cols, _recs(), tf, skip_dc=True, ts_scan=True)
+    assert not plane.any() and nb.all()
+    # the TS rows the scan reads are counted once each
+    paths = bench.scratch_paths(cols, _recs(), tf, skip_dc=True, ts_scan=True)
+    a = bench.algorithmic_bytes(cols, True, True, paths)
+    b = bench.algorithmic_bytes(cols, True, True, paths, ts_rows=1)
+    assert b["k_hourly_batt"] - a["k_hourly_batt"] == 8 * 8760
