@@ -327,7 +327,7 @@ def main():
     nb_on = batch.nb_scan and nb_lds <= 65536
     dcr_on = dc_batch and args.replan_hours != 1
     # dgen_size_agents' ts_split gate (12 KB more day buffer per wave)
-    ts_scan = (nb_on and bool(eng.tables.wholesale) and not dcr_on and args.replan_hours != 1 and
+    ts_scan = (nb_on and bool(eng.tables.wholesale) and not dc_batch and args.replan_hours != 1 and
                not args.no_hourly and
                os.environ.get("DGEN_TS_SCAN", "1") != "0" and nb_lds + 2 * 12 * 1024 <= 65536)
     tf_dev = out["tariff_final"].cpu().numpy()

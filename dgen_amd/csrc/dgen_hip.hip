@@ -4724,14 +4724,16 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // TS sell-rate agents' split built in a scan of their own (k_hourly_batt<TS>,
     // launched beside the NB scan over the rest; 12 KB more of day buffer per
     // wave, so it runs one wave per SIMD): batches with a wholesale table, no
-    // demand records, daily plan, hourly planes requested.  With the planes the
+    // demand charges or kWh/kW peaks, daily plan, hourly planes requested.  With the planes the
     // NB scan is clock-bound and the TS blocks fill in around it (national 200k:
     // 21.38 -> 20.22 ms per step, k_batt_finance 3.54 -> 1.11 ms); without them
     // (the model-year loop's sizing call) the one-wave form's latency shows
     // (C5 2.5M: k_hourly_batt 56 -> 98 ms against k_batt_finance 47 -> 15 ms),
     // and the plane pass stays
     const size_t lds_ts = lds + (size_t)(BLOCK / 64) * HB_DAY_BYTES;
-    const bool ts_split = nb_scan && T->wholesale != nullptr && !dcr_on && c->ts_scan && lds_ts <= 65536 &&
+    // (not in batches with the demand machinery at all: whether their agents
+    // take this form must not depend on the demand records being on)
+    const bool ts_split = nb_scan && T->wholesale != nullptr && !dc && c->ts_scan && lds_ts <= 65536 &&
                           c->cfg.batt_update_hours != 1 && hourly;
     // two agents per wave when every analysis period fits 32 lanes, unless the
     // build guard withdrew that kernel's 32-lane instantiation (DGEN_NO2_*)

@@ -248,13 +248,14 @@ class Engine:
 
     def _nb_scan_pays(self, cols, n: int, n_scratch: int) -> bool:
         """dgen_set_nb_scan: the battery case's net-billing split is built in
-        the hourly scan for every agent that bills net without a TS sell rate
-        (the scan decides per agent; profile_order groups those agents into
-        their own waves), so an agent's battery-case outputs do not depend on
-        the batch it is sized in.  The scan form is compiled in only when the
-        batch holds such an agent (its instantiation carries the export sums:
-        more registers, and with the demand records a spill), which changes no
-        result.  DGEN_NB_SCAN=0 turns it off (A/B: the finance kernel's build
+        the hourly scan for every agent that bills net (the scan decides per
+        agent; profile_order groups those agents into their own waves; the TS
+        sell-rate agents get a scan of their own when hourly planes are
+        requested, dgen_size_agents' ts_split), so an agent's battery-case
+        outputs do not depend on the other agents of its batch.  The scan form
+        is compiled in only when the batch holds such an agent (its
+        instantiation carries the export sums: more registers, and with the
+        demand records a spill), which changes no result.  DGEN_NB_SCAN=0 turns it off (A/B: the finance kernel's build
         over the system-output plane; the two builds re-associate the split's
         sums, ~1e-9 relative on the battery-case bills and NPV)."""
         import os
@@ -266,12 +267,9 @@ class Engine:
         try:
             sl = np.asarray(cols["scratch_slot"])
             mo = mo_t[np.asarray(cols["tariff0"], np.int64)]
-            ts = (mo == 2) & ((np.asarray(cols["flags"]) & 2) == 0) & (np.asarray(cols["wholesale_row"]) >= 0)
         except Exception:          # device-tensor columns: keep it on
             return True
-        if not self.tables.wholesale:
-            ts[:] = False
-        return bool(((sl >= 0) & ((mo == 2) | (mo == 3)) & ~ts).any())
+        return bool(((sl >= 0) & ((mo == 2) | (mo == 3))).any())
 
     def validate_agents(self, dev, n):
         """Host-side bounds checks before any kernel indexes a table."""
