@@ -228,6 +228,40 @@ def state_hourly(engine, planes, weights, idx, seg_off):
     return out
 
 
+def state_hourly_combined(engine, plane, idx, seg_off):
+    """k_state_hourly over Engine.export_plane's combined plane (float64
+    hour-quad tiles [n_hours / 4, n, 4]): the rows state_hourly gives from the
+    three planes and their weights, bit for bit (dgen_state_hourly
+    planes_f32 = 3).  idx / seg_off as in state_hourly."""
+    import torch
+    eng = _engine(engine)
+    L = _bind(eng.lib)
+    if plane.dtype != torch.float64 or plane.dim() != 3 or plane.shape[2] != 4:
+        raise ValueError("state_hourly_combined: the plane is float64 hour-quad tiles [n_hours/4, n, 4]")
+    nh, n = plane.shape[0] * 4, plane.shape[1]
+    so = np.asarray(seg_off, dtype=np.int64)
+    m = int(so[-1]) if len(so) else 0
+    if len(so) < 1 or so[0] != 0 or np.any(np.diff(so) < 0):
+        raise ValueError("segment offsets must start at 0 and be non-decreasing")
+    ti = None
+    if idx is not None:
+        ix = np.asarray(idx, dtype=np.int64)
+        if len(ix) != m or (m and (ix.min() < 0 or ix.max() >= n)):
+            raise ValueError("state_hourly_combined: idx out of range")
+        ti = eng._to_dev(ix, torch.int64)
+    elif m > n:
+        raise ValueError("state_hourly_combined: segments exceed the plane width")
+    S = len(so) - 1
+    out = torch.empty((S, nh), dtype=torch.float64, device=eng.dev)
+    pl = plane.contiguous()
+    t_off = eng._to_dev(so, torch.int64)
+    _lib.check(L.dgen_state_hourly(eng.ctx, pl.data_ptr(), None, None, 3, None, None, None,
+                                   None if ti is None else ti.data_ptr(), n, nh, t_off.data_ptr(),
+                                   S, out.data_ptr(), eng.stream_handle()), "dgen_state_hourly")
+    torch.cuda.current_stream(eng.dev).synchronize()
+    return out
+
+
 def _len_safe(x) -> int:
     try:
         return len(x)

@@ -887,11 +887,19 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 // 24-B entries (load, generation, weight, period; flag 4).
 // ts_mode: 0 every agent; 1 the agents that can bill the TS rate (a scratch
 // slot and a wholesale row, non-CA: engine.path_class 2) skipped; 2 only those.
-template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR, bool LOSS = false, bool NEM = false, bool TS = false>
+// XP (with HOURLY, f32 semantics): the per-state export's combined plane
+// instead of the three planes: per agent-hour the f64 value k_state_hourly
+// adds, ((double)pvo x w_pvo + (double)wbt x w_batt) + (double)base x w_non of
+// the float32-rounded plane values, in hour-quad tiles [h / 4][n][4] (8 B per
+// agent-hour instead of 12, and k_state_hourly reads one plane, bit-identical)
+template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR, bool LOSS = false, bool NEM = false, bool TS = false,
+          bool XP = false>
 __global__ void __launch_bounds__(BLOCK, (ROLL || TS) ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
-              int repair, char* dcr, int dc_nq, int dcr_cap, int ts_mode = 0) {
+              int repair, char* dcr, int dc_nq, int dcr_cap, int ts_mode = 0,
+              const double* xw_pvo = nullptr, const double* xw_batt = nullptr, const double* xw_non = nullptr,
+              double* xplane = nullptr) {
     // agents [i0, i1) of a batch of n (row stride of every plane stays n),
     // months [m_lo, m_hi) of the year: the year is swept in month segments,
     // one launch each, so that every resident wave works on the same weeks
@@ -1045,11 +1053,15 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // contiguous per plane every 4 hours (measured 29.3 -> 27.9 ms vs one
     // 4-B store per lane-hour)
     using PT = typename std::conditional<F64, double, float>::type;
-    constexpr uint32_t QB = 4 * sizeof(PT);          // bytes per lane per hour quad
+    constexpr uint32_t QB = (XP ? 8 : sizeof(PT)) * 4;   // bytes per lane per hour quad
     const uint32_t off16 = (uint32_t)i * QB;
     const size_t row16 = (size_t)n * QB;
     size_t q16 = (size_t)d_lo * 6 * row16;
     PT qb[4], qp[4], qw[4];
+    // XP: the agent's export weights and the combined plane
+    const double xa = XP ? xw_pvo[i] : 0.0, xb = XP ? xw_batt[i] : 0.0, xd = XP ? xw_non[i] : 0.0;
+    char* const ox = reinterpret_cast<char*>(xplane);
+    (void)ox;
 
     // Software pipeline over days through LDS: the next day's raw profile
     // values (96 B of the shape row + 96 B of the cf row per lane) are DMA'd
@@ -1155,7 +1167,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
         __builtin_amdgcn_s_waitcnt(0x0f70);                  // vmcnt(0)
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             if (ROLL && d > d_lo) day_reread(dlane, r);    // the DMA was waited for yesterday
-            else if (HOURLY && d > d_lo) day_read<HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);
+            else if (HOURLY && d > d_lo) day_read<XP ? 12 : HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);
             else day_read<0>(dlane, r);
             const bool wkend = (d % 7) >= 5;
             const uint64_t sched[3] = {wkend ? swe[0] : swd[0], wkend ? swe[1] : swd[1],
@@ -1274,9 +1286,17 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                     qp[hh & 3] = (PT)fmax(dn, 0.0);
                     qw[hh & 3] = (PT)st.g2l;
                     if ((hh & 3) == 3) {
-                        st_f32x4(ob + q16, off16, qb);
-                        st_f32x4(op + q16, off16, qp);
-                        st_f32x4(ow + q16, off16, qw);
+                        if constexpr (XP) {
+                            double xv[4];
+#pragma unroll
+                            for (int u = 0; u < 4; u++)
+                                xv[u] = ((double)qp[u] * xa + (double)qw[u] * xb) + (double)qb[u] * xd;
+                            st_f32x4(ox + q16, off16, xv);
+                        } else {
+                            st_f32x4(ob + q16, off16, qb);
+                            st_f32x4(op + q16, off16, qp);
+                            st_f32x4(ow + q16, off16, qw);
+                        }
                         q16 += row16;
                     }
                 }
@@ -4178,8 +4198,10 @@ __global__ void k_export_weights(const double* __restrict__ customers, const dou
 // a state's columns are a contiguous ascending range (the year loop's
 // state-major device order); a scattered idx fetches a 128-B line per 16-B
 // quad.  Fixed reduction order.
+// COMB: `base` is k_hourly_batt<XP>'s combined plane (f64 tiles; pvo / wbt /
+// weights unused): each agent-hour adds the value the three-plane form adds.
 constexpr int SH_TILE = 32;
-template <typename V, bool TILED>
+template <typename V, bool TILED, bool COMB = false>
 __global__ void __launch_bounds__(256)
 k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
                const V* __restrict__ wbt, const double* __restrict__ w_pvo,
@@ -4197,6 +4219,21 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
     for (int t = 0; t < SH_TILE; t++) acc[t] = 0.0;
     for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
         const int64_t c = idx ? idx[i] : i;
+        if constexpr (COMB) {
+#pragma unroll
+            for (int q = 0; q < SH_TILE / 4; q++) {
+                if (4 * q < nt) {
+                    const int64_t r = (((int64_t)(h0 >> 2) + q) * n + c) * 4;
+                    const double2 x0 = *reinterpret_cast<const double2*>(base + r);
+                    const double2 x1 = *reinterpret_cast<const double2*>(base + r + 2);
+                    acc[4 * q] += x0.x;
+                    acc[4 * q + 1] += x0.y;
+                    acc[4 * q + 2] += x1.x;
+                    acc[4 * q + 3] += x1.y;
+                }
+            }
+            continue;
+        }
         const double a = w_pvo[c], b = w_batt[c], d = w_non[c];
         if constexpr (TILED) {
             // nh % 4 == 0 (host), h0 % 4 == 0: whole quads
@@ -4975,11 +5012,61 @@ int32_t dgen_hourly_planes(dgen_ctx* c, const dgen_tables* T, const dgen_agents*
         if (c->cfg.batt_loss_model == 1) {
             if (O->hourly_f64) { if (roll) DGEN_HP_LAUNCH(true, true, true); else DGEN_HP_LAUNCH(true, false, true); }
             else { if (roll) DGEN_HP_LAUNCH(false, true, true); else DGEN_HP_LAUNCH(false, false, true); }
+        } else if (roll) {
+            if (O->hourly_f64) DGEN_HP_LAUNCH(true, true, false); else DGEN_HP_LAUNCH(false, true, false);
         } else {
-            if (O->hourly_f64) { if (roll) DGEN_HP_LAUNCH(true, true, false); else DGEN_HP_LAUNCH(true, false, false); }
-            else { if (roll) DGEN_HP_LAUNCH(false, true, false); else DGEN_HP_LAUNCH(false, false, false); }
+            // the bins-only form (NEM): no agent's bill is needed here, so no
+            // hour writes the battery case's f64 system-output plane or takes
+            // the net-billing branch; the dispatch, and so every plane, is the
+            // same
+#define DGEN_HP_LAUNCH_NEM(F)                                                                      \
+            hipLaunchKernelGGL((k_hourly_batt<true, F, false, false, false, false, true>), grid, block, lds, s, *T, *A, \
+                               *O, c->cfg, n, ws, n_scratch, (int64_t)0, n, m0, m1, c->battery, 0, 0, nullptr, 0, 0)
+            if (O->hourly_f64) DGEN_HP_LAUNCH_NEM(true); else DGEN_HP_LAUNCH_NEM(false);
+#undef DGEN_HP_LAUNCH_NEM
         }
 #undef DGEN_HP_LAUNCH
+    }
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_export_plane(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A, const dgen_outputs* O,
+                          const double* w_pvo, const double* w_batt, const double* w_non, double* plane,
+                          int64_t n, void* ws, size_t ws_bytes, int64_t n_scratch, void* stream) {
+    if (!c || !T || !A || !O || !w_pvo || !w_batt || !w_non || !plane) {
+        set_err("dgen_export_plane: null argument");
+        return DGEN_E_ARG;
+    }
+    if (n <= 0) return DGEN_OK;
+    if (c->cfg.batt_loss_model == 1 || c->cfg.batt_update_hours == 1) {
+        set_err("dgen_export_plane: the loss model / hourly re-plan scans export through dgen_hourly_planes");
+        return DGEN_E_ARG;
+    }
+    if (!T->shapes || !T->shape_sum || !T->cfs || !T->tariffs || T->n_tariffs <= 0 ||
+        (T->n_demand > 0 && !T->demand)) {
+        set_err("dgen_export_plane: incomplete tables");
+        return DGEN_E_ARG;
+    }
+    if (n >= ((int64_t)1 << 27) || n_scratch >= ((int64_t)1 << 28)) {
+        set_err("dgen_export_plane: batch too large (n < 2^27)");
+        return DGEN_E_ARG;
+    }
+    if (!ws || ws_bytes < dgen_workspace_bytes(n, n_scratch)) {
+        set_err("dgen_export_plane: workspace too small (%zu < %zu)", ws_bytes, dgen_workspace_bytes(n, n_scratch));
+        return DGEN_E_ARG;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    // the bins-only scan (as dgen_hourly_planes) writing the combined plane
+    const size_t lds = sizeof(double) * 2 * (size_t)lds_half(T->max_periods) * BLOCK +
+                       (size_t)(BLOCK / 64) * HB_DAY_BYTES;
+    const dim3 grid((unsigned)((n + BLOCK - 1) / BLOCK)), block(BLOCK);
+    for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
+        const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
+        hipLaunchKernelGGL((k_hourly_batt<true, false, false, false, false, false, true, false, true>), grid, block,
+                           lds, s, *T, *A, *O, c->cfg, n, ws, n_scratch, (int64_t)0, n, m0, m1, c->battery, 0, 0,
+                           nullptr, 0, 0, 0, w_pvo, w_batt, w_non, plane);
     }
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
@@ -5185,13 +5272,15 @@ int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
                           const double* w_batt, const double* w_non, const int64_t* idx, int64_t n,
                           int32_t n_hours, const int64_t* seg_off, int64_t n_seg, double* out,
                           void* stream) {
-    if (!c || !baseline || !pvonly || !with_batt || !w_pvo || !w_batt || !w_non || !seg_off ||
+    const bool comb = planes_f32 == 3;        // dgen_export_plane's combined plane in `baseline`
+    if (!c || !baseline || (!comb && (!pvonly || !with_batt || !w_pvo || !w_batt || !w_non)) || !seg_off ||
         !out || n < 0 || n_hours <= 0 || n_seg < 0 || n_seg > 0x7fffffff) {
         set_err("dgen_state_hourly: bad argument");
         return DGEN_E_ARG;
     }
-    if (planes_f32 < 0 || planes_f32 > 2) {
-        set_err("dgen_state_hourly: planes_f32 must be 0 (f64 [h][n]), 1 (f32 tiles) or 2 (f64 tiles)");
+    if (planes_f32 < 0 || planes_f32 > 3) {
+        set_err("dgen_state_hourly: planes_f32 must be 0 (f64 [h][n]), 1 (f32 tiles), 2 (f64 tiles) "
+                "or 3 (the combined f64 plane, tiles)");
         return DGEN_E_ARG;
     }
     if (planes_f32 && n_hours % 4 != 0) {
@@ -5201,7 +5290,11 @@ int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
     if (n_seg == 0) return DGEN_OK;
     HIP_TRY(hipSetDevice(c->device));
     const dim3 grid((unsigned)n_seg, (unsigned)((n_hours + SH_TILE - 1) / SH_TILE));
-    if (planes_f32 == 2)
+    if (comb)
+        hipLaunchKernelGGL((k_state_hourly<double, true, true>), grid, dim3(256), 0, (hipStream_t)stream,
+                           (const double*)baseline, nullptr, nullptr, nullptr, nullptr, nullptr, idx, n,
+                           (int)n_hours, seg_off, n_seg, out);
+    else if (planes_f32 == 2)
         hipLaunchKernelGGL((k_state_hourly<double, true>), grid, dim3(256), 0, (hipStream_t)stream,
                            (const double*)baseline, (const double*)pvonly, (const double*)with_batt,
                            w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);

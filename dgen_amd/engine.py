@@ -343,6 +343,25 @@ class Engine:
                                                batch.n_scratch, self.stream_handle()),
                    "dgen_hourly_planes")
 
+    def export_plane(self, batch: AgentBatch, c_out: _lib.Outputs, weights, plane) -> bool:
+        """The per-state export's combined plane of `batch` (already sized with
+        the outputs `c_out` points to; async, dgen_export_plane): the 8760-h scan
+        alone, writing per agent-hour the f64 value dgen_state_hourly adds from
+        the three planes, into `plane` (float64 hour-quad tiles [NH/4, n, 4]).
+        False (nothing launched) for the loss model and the hourly re-plan,
+        whose scans export through hourly_planes."""
+        if self.cfg.batt_loss_model == 1 or self.cfg.batt_update_hours == 1:
+            return False
+        w = [x.contiguous() for x in weights]
+        if any(x.numel() != batch.n for x in w) or plane.numel() < _lib.NH * batch.n:
+            raise ValueError("export_plane: one weight per agent and NH x n plane values")
+        _lib.check(self.lib.dgen_export_plane(self.ctx, ctypes.byref(self.tables), ctypes.byref(batch.c_agents),
+                                              ctypes.byref(c_out), _ptr(w[0]), _ptr(w[1]), _ptr(w[2]),
+                                              _ptr(plane), batch.n, _ptr(batch.workspace),
+                                              batch.workspace.numel(), batch.n_scratch, self.stream_handle()),
+                   "dgen_export_plane")
+        return True
+
     def set_pipeline(self, chunks: int):
         """Chunk-pipeline depth of size() (dgen_set_pipeline; 1 = no overlap)."""
         _lib.check(self.lib.dgen_set_pipeline(self.ctx, int(chunks)), "dgen_set_pipeline")

@@ -66,7 +66,7 @@ import pandas as pd
 from . import _lib
 from .attachment import ATTACH_IN, ATTACH_OUT, AttachIn, AttachOut
 from .attachment import _bind as _bind_attach
-from .attachment import export_weights, state_hourly, string_ranks
+from .attachment import export_weights, state_hourly, state_hourly_combined, string_ranks
 from .diffusion import DIFF_IN, DIFF_OUT, DiffIn, DiffOut, MmsTable, mms_table
 from .diffusion import _bind as _bind_diff
 from .dist import allreduce_sum
@@ -618,8 +618,15 @@ class YearLoop:
                 j0 = j1
             self._runs = runs
             mx = max((b - a for a, b, _, _ in runs), default=0)
-            self._chunk_planes = {k: torch.empty(_lib.NH * max(mx, 1), dtype=torch.float32, device=eng.dev)
-                                  for k in _lib.OUTPUT_HOURLY}
+            # the combined export plane (dgen_export_plane: 8 B per agent-hour,
+            # the daily plan without the loss model) or the three float32 planes
+            self._comb = eng.cfg.batt_loss_model != 1 and eng.cfg.batt_update_hours != 1
+            if self._comb:
+                self._chunk_comb = torch.empty(_lib.NH * max(mx, 1), dtype=torch.float64, device=eng.dev)
+                self._chunk_planes = {}
+            else:
+                self._chunk_planes = {k: torch.empty(_lib.NH * max(mx, 1), dtype=torch.float32, device=eng.dev)
+                                      for k in _lib.OUTPUT_HOURLY}
         B = self.batch
         parts = []
         for a, b, idx, so in self._runs:
@@ -630,12 +637,21 @@ class YearLoop:
             sub = AgentBatch(n=m, n_scratch=B.n_scratch, cols=cols, workspace=B.workspace,
                              c_agents=ca, nb_scan=B.nb_scan)
             out = {k: v[a:b] for k, v in self.out.items() if v is not None}
+            wc = tuple(x[a:b] for x in w)
+            if self._comb:
+                # the scan writes the per-agent-hour sum terms of the export
+                # straight into one plane (no three planes written and re-read);
+                # the per-state rows are the three-plane form's, bit for bit
+                co = eng.c_outputs(out)
+                plane = self._chunk_comb[:_lib.NH * m].view(_lib.NH // 4, m, 4)
+                eng.export_plane(sub, co, wc, plane)
+                parts.append(state_hourly_combined(eng, plane, idx, so))
+                continue
             out.update({k: v[:_lib.NH * m].view(_lib.NH // 4, m, 4)
                         for k, v in self._chunk_planes.items()})
             co = eng.c_outputs(out)
             planes = (out["baseline"], out["net_pvonly"], out["net_with_batt"])
             eng.hourly_planes(sub, co)
-            wc = tuple(x[a:b] for x in w)
             parts.append(state_hourly(eng, planes, wc, idx, so))
         return torch.cat(parts) if parts else torch.zeros((0, _lib.NH), dtype=torch.float64, device=eng.dev)
 

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 9
+#define DGEN_ABI_VERSION 10
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_DEFAULT_HOURLY_SPLIT 2   /* parts of a chunk's hourly scan, each on its own stream */
@@ -415,7 +415,8 @@ int32_t dgen_export_weights(dgen_ctx* ctx, const double* customers_in_bin,
  * (planes_f32 = 1: float32 in dgen_size_agents' hour-quad tiles
  * [n_hours / 4][n][4], its hourly outputs in place, n_hours % 4 == 0;
  * 2: the same tiles in float64 (dgen_outputs.hourly_f64); 0: float64
- * [n_hours][n]) and the per-column weights:
+ * [n_hours][n]; 3: dgen_export_plane's combined float64 plane in tiles, in
+ * `baseline`, pvonly / with_batt / weights unused) and the per-column weights:
  * out[s * n_hours + h].  Members of state s are the plane columns
  * idx[seg_off[s] .. seg_off[s+1]) (idx NULL: columns seg_off[s] ..
  * seg_off[s+1]).  Fixed summation order (deterministic); the reference's
@@ -552,6 +553,23 @@ int32_t dgen_set_pipeline(dgen_ctx* ctx, int32_t chunks);
 int32_t dgen_hourly_planes(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
                            const dgen_outputs* outputs, int64_t n, void* workspace, size_t workspace_bytes,
                            int64_t n_scratch, void* stream);
+
+/* The per-state export's combined plane of a batch already sized by
+ * dgen_size_agents (same ctx settings, tables, agents, workspace; as
+ * dgen_hourly_planes, the scan alone): per agent-hour the f64 value
+ * dgen_state_hourly adds from the three float32 planes,
+ *   ((double)pvo * w_pvo + (double)wbt * w_batt) + (double)base * w_non,
+ * in hour-quad tiles ((h, i) at ((h / 4) * n + i) * 4 + h % 4), from the
+ * weights of dgen_export_weights.  dgen_state_hourly with planes_f32 = 3 sums
+ * it (baseline = the plane; pvonly / with_batt / weights unused): the same
+ * per-state rows, bit for bit, from 8 B per agent-hour written and read
+ * instead of 12.  Daily plan without the loss model only (DGEN_E_ARG
+ * otherwise: use dgen_hourly_planes).  n < 2^27.  Replaces nothing in the
+ * reference (attachment_rate_functions.py:151-206 sums the frame's lists).   */
+int32_t dgen_export_plane(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
+                          const dgen_outputs* outputs, const double* w_pvo, const double* w_batt,
+                          const double* w_non, double* plane, int64_t n, void* workspace,
+                          size_t workspace_bytes, int64_t n_scratch, void* stream);
 
 /* Months of the year per k_hourly_batt launch (the sequential 8760-h scan of
  * dgen_size_agents): the year is swept in ceil(12 / months) launches, SOC and
