@@ -4448,6 +4448,7 @@ struct dgen_ctx {
     int hb_split;      // parts of a chunk's hourly scan, each on its own stream (1..4; DGEN_HB_SPLIT)
     int hb_nem;        // 1: batches without scratch slots run the bins-only scan (DGEN_HB_NEM=0: off)
     int ts_scan;       // 1: the TS sell-rate agents' split built in their own scan (DGEN_TS_SCAN=0: off, A/B)
+    int64_t ts_lo, ts_hi;   // the batch rows holding every TS-capable agent (dgen_set_ts_rows)
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
     int battery;       // PV+battery forward run (dgen_set_battery)
@@ -4550,6 +4551,8 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
         const char* x = getenv("DGEN_TS_SCAN");
         c->ts_scan = (x && x[0] == '0') ? 0 : 1;
     }
+    c->ts_lo = 0;
+    c->ts_hi = INT64_MAX;
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
     for (int k = 0; k < dgen_ctx::MAXSPLIT - 1 && e == hipSuccess; k++) {
         e = hipStreamCreateWithFlags(&c->sx[k], hipStreamNonBlocking);
@@ -4861,6 +4864,11 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         hipStream_t hts = c->st[part];
         if (hb <= ha) continue;
         const dim3 hgrid((unsigned)((hb - ha + BLOCK - 1) / BLOCK));
+        // the TS form's rows: the part's rows that can hold a TS-capable agent
+        // (dgen_set_ts_rows), from a block boundary of the part
+        const int64_t tsa = c->ts_lo > ha ? ha + (c->ts_lo - ha) / BLOCK * BLOCK : ha;
+        const int64_t tsb = c->ts_hi < hb ? c->ts_hi : hb;
+        const dim3 tsgrid((unsigned)(tsb > tsa ? (tsb - tsa + BLOCK - 1) / BLOCK : 1));
         for (int m0 = 0; m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
 #define DGEN_HB_LAUNCH_R(H, F, REP, R)                                                            \
@@ -4871,9 +4879,10 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         else if (nb_scan && !(REP) && ts_split && !(R)) {                                         \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, false>), hgrid, block, lds, hs, *T, *A, *O, \
                                c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0, 1); \
-            hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, false, false, false, true>), hgrid, block, lds_ts, \
-                               hts, *T, *A, *O, c->cfg, n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, \
-                               nullptr, 0, 0, 2);                                                  \
+            if (tsb > tsa)                                                                        \
+                hipLaunchKernelGGL((k_hourly_batt<H, F, true, false, false, false, false, true>), tsgrid, block, \
+                                   lds_ts, hts, *T, *A, *O, c->cfg, n, ws, n_scratch, tsa, tsb, m0, m1, c->battery, \
+                                   c->nb_scan, 0, nullptr, 0, 0, 2);                               \
         } else if (nb_scan && !(REP))                                                             \
             hipLaunchKernelGGL((k_hourly_batt<H, F, true, R, false>), hgrid, block, lds, hs, *T, *A, *O, c->cfg, \
                                n, ws, n_scratch, ha, hb, m0, m1, c->battery, c->nb_scan, 0, nullptr, 0, 0); \
@@ -4917,7 +4926,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         const int64_t ha = i0, hb = i1;
         hipStream_t hs = s2;
         hipStream_t hts = s2;           // (the repair pass never launches the TS form)
-        (void)hts;
+        const int64_t tsa = 0, tsb = 0;
+        const dim3 tsgrid(1);
+        (void)hts; (void)tsa; (void)tsb; (void)tsgrid;
         const dim3 hgrid((unsigned)((m + BLOCK - 1) / BLOCK));
         for (int m0 = 0; rep_mask && m0 < 12; m0 += c->hb_months) {
             const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
@@ -5111,6 +5122,16 @@ int32_t dgen_set_nb_scan(dgen_ctx* c, int32_t cap) {
         return DGEN_E_ARG;
     }
     c->nb_scan = cap;
+    return DGEN_OK;
+}
+
+int32_t dgen_set_ts_rows(dgen_ctx* c, int64_t lo, int64_t hi) {
+    if (!c || lo < 0 || hi < lo) {
+        set_err("dgen_set_ts_rows: need 0 <= lo <= hi");
+        return DGEN_E_ARG;
+    }
+    c->ts_lo = lo;
+    c->ts_hi = hi;
     return DGEN_OK;
 }
 

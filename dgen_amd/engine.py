@@ -39,6 +39,8 @@ class AgentBatch:
     perm: Optional[np.ndarray] = None
     # build the battery case's net-billing split in the hourly scan (dgen_set_nb_scan)
     nb_scan: bool = True
+    # device rows holding every TS-capable agent (dgen_set_ts_rows)
+    ts_rows: tuple = (0, 2 ** 62)
 
 
 def path_class(cols: Dict[str, np.ndarray]) -> np.ndarray:
@@ -244,7 +246,18 @@ class Engine:
         ca = _lib.Agents(**{name: _ptr(dev[name]) for name, _ in _lib.AGENT_COLUMNS})
         ca.max_years = int(dev["econ_life"].max().item()) if n else 0
         return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order,
-                          nb_scan=self._nb_scan_pays(cols, n, n_scratch))
+                          nb_scan=self._nb_scan_pays(cols, n, n_scratch), ts_rows=self._ts_rows_of(cols, n))
+
+    def _ts_rows_of(self, cols, n: int):
+        """dgen_set_ts_rows: the device rows [lo, hi) holding every agent that
+        can bill the TS sell rate (path_class 2); (0, 0) when there is none.
+        Host columns only (device tensors: the whole batch)."""
+        try:
+            pc = path_class(cols)
+        except Exception:
+            return (0, 2 ** 62)
+        ix = np.flatnonzero(pc == 2)
+        return (int(ix[0]), int(ix[-1]) + 1) if ix.size else (0, 0)
 
     def _nb_scan_pays(self, cols, n: int, n_scratch: int) -> bool:
         """dgen_set_nb_scan: the battery case's net-billing split is built in
@@ -327,6 +340,10 @@ class Engine:
             _lib.check(self.lib.dgen_set_nb_scan(self.ctx, _lib.NB_CAPM if batch.nb_scan else 0),
                        "dgen_set_nb_scan")
             self._nb_scan = batch.nb_scan
+        if tuple(batch.ts_rows) != getattr(self, "_ts_rows", (0, 2 ** 62)):
+            _lib.check(self.lib.dgen_set_ts_rows(self.ctx, int(batch.ts_rows[0]), int(batch.ts_rows[1])),
+                       "dgen_set_ts_rows")
+            self._ts_rows = tuple(batch.ts_rows)
         _lib.check(self.lib.dgen_size_agents(self.ctx, ctypes.byref(self.tables),
                                              ctypes.byref(batch.c_agents), ctypes.byref(co),
                                              batch.n, _ptr(batch.workspace),

@@ -603,6 +603,15 @@ int32_t dgen_set_battery(dgen_ctx* ctx, int32_t on);
  * Range [0, DGEN_NB_CAPM].  Replaces nothing in the reference.            */
 int32_t dgen_set_nb_scan(dgen_ctx* ctx, int32_t cap);
 
+/* The batch rows [lo, hi) that hold every agent able to bill the hourly TS
+ * sell rate (a scratch slot and a wholesale row, non-CA): the TS agents' own
+ * split scan (k_hourly_batt<TS>, batches with hourly planes and a wholesale
+ * table, no demand charges) is launched over those rows only; lo == hi: none.
+ * Default [0, INT64_MAX): the whole batch.  Results do not depend on it as
+ * long as the range covers those agents (the Python engine sets it from the
+ * device order, Engine.upload_agents).  Replaces nothing in the reference.  */
+int32_t dgen_set_ts_rows(dgen_ctx* ctx, int64_t lo, int64_t hi);
+
 /* Battery-case demand records holding at most cap kept hours per agent
  * (default and maximum DGEN_DCR_CAP), or none (0).  With demand charges
  * billed (or kWh/kW tier peaks) and the daily plan, k_hourly_batt's scan keeps
