@@ -62,6 +62,27 @@ def test_size_chunk_matches_golden_and_aggregates():
     assert np.allclose(agg["net_sum_kw"], base, rtol=1e-5)
 
 
+def test_empty_and_repeated_rows():
+    """An empty chunk returns what the reference's loop returns for no rows
+    (ff:1209-1218: an empty frame, n_hours 0, no sums); the same agent twice in
+    one chunk gives two identical rows, the golden ones."""
+    rows, store, table = helpers.golden_rows()
+    meta, arr = helpers.golden_agents()
+    ff._worker_conn = store
+    out, agg = ff.size_chunk(pd.DataFrame(rows).iloc[:0], None, table, "simple")
+    assert len(out) == 0 and agg == {"mode": "simple", "n_hours": 0, "net_sum_kw": []}
+    r1 = rows[4].copy()
+    r1.name = 99
+    out, agg = ff.size_chunk(pd.DataFrame([rows[4], r1]), None, table, "simple")
+    assert list(out.index) == [rows[4].name, 99]
+    for _, r in out.iterrows():
+        _check_row(r, meta["agents"][4], 4, arr)
+    a, b = out.iloc[0], out.iloc[1]
+    for k in SCALARS + ["payback_period"]:
+        assert a[k] == b[k], k
+    assert np.array_equal(np.asarray(a["adopter_net_hourly_with_batt"]), np.asarray(b["adopter_net_hourly_with_batt"]))
+
+
 def test_zero_load_raises_like_reference():
     rows, store, table = helpers.golden_rows()
     r = rows[0].copy()
