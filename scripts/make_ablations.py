@@ -294,6 +294,8 @@ VARIANTS["ks_obj_x2"] = [("            return yl_objective<LPA, DC, NET, PK>(c, 
 
 # k_size (bins-only and net-billing instantiations) at 4 waves per SIMD
 VARIANTS["ks_occ4"] = [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? 2 : 4)")]
+# the demand-charge instantiations at 3 waves per SIMD (168 VGPRs: spills)
+VARIANTS["ks_dc3"] = [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(3)")]
 
 # yl_bill_nb: staged entries read per group ahead of the billed group
 VARIANTS["nbu2"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 2")]
