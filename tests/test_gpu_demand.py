@@ -139,3 +139,31 @@ def test_kwh_per_kw_records_bit_identical(engine):
     off = _run_records(engine, pop, pop.demand, False)
     for k in ("system_kw", "npv", "npv_pv_batt", "bill_w_batt", "bill_wo_batt", "status"):
         assert np.array_equal(on[k], off[k], equal_nan=True), k
+
+
+def test_short_demand_period_table_is_flagged(engine_dc):
+    """A C-ABI caller whose dgen_tables.max_dc_periods is smaller than the
+    periods its demand schedules use (Engine.set_tariffs fills it correctly):
+    the battery-case scan sizes its per-period LDS maxima from that field, so an
+    hour of a later period flags DGEN_ST_DEMAND on the agent instead of being
+    written past the region; the same engine with the right field then gives the
+    untouched result again, bit for bit."""
+    from dgen_amd import _lib
+    pop = _pop(96, seed=13)
+    assert int(max(pop.demand["wkday"].max(), pop.demand["wkend"].max())) >= 1
+    good = _run(engine_dc, pop, pop.demand)
+    assert (good["status"] == 0).all()
+    engine_dc.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine_dc.set_tariffs(pop.tariffs, pop.demand)
+    engine_dc.set_switches(pop.switches)
+    engine_dc.tables.max_dc_periods = 1          # malformed: the schedules use more
+    batch = engine_dc.upload_agents(pop.cols, pop.n_scratch)
+    out = engine_dc.alloc_outputs(batch.n, hourly=True)
+    engine_dc.size(batch, out)
+    torch.cuda.synchronize()
+    bad = outputs_to_host(out)
+    flagged = (bad["status"] & _lib.ST_DEMAND) != 0
+    assert flagged.any()
+    again = _run(engine_dc, pop, pop.demand)
+    for k in ("status", "system_kw", "npv", "npv_pv_batt", "batt_kwh", "first_without"):
+        assert np.array_equal(again[k], good[k], equal_nan=True), k
