@@ -88,6 +88,36 @@ def test_c2_ca_like_200k_sample_vs_oracle(engine):
     assert not flips, flips
 
 
+def test_national_200k_sample_vs_oracle(engine):
+    """The national mix at 200k with hourly planes, in the bench's device
+    order: NEM bins, the scan-built net-billing split (CA and no-TS agents)
+    and the TS sell-rate agents' own scan (k_hourly_batt<TS>) in one batch; a
+    random sample plus TS-path agents against the oracle."""
+    from dgen_amd.engine import path_class
+    from dgen_amd.synth import subset
+    n = 200_000
+    pop = make_population("national_mixed", n, seed=20260000 + 5 + 211)
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    batch = engine.upload_agents(pop.cols, pop.n_scratch, order=profile_order(pop.cols))
+    assert batch.nb_scan and batch.ts_rows[1] > batch.ts_rows[0]
+    out = engine.alloc_outputs(n, hourly=True)
+    engine.size(batch, out)
+    torch.cuda.synchronize()
+    assert (out["status"].cpu().numpy() == 0).all()
+    inv = np.empty(n, np.int64)
+    inv[batch.perm] = np.arange(n)
+    rng = np.random.default_rng(15)
+    ts = np.flatnonzero(path_class(pop.cols) == 2)
+    idx = np.unique(np.concatenate([rng.choice(n, SAMPLE - 50, replace=False), rng.choice(ts, 50, replace=False)]))
+    sample = _device_sample(out, inv[idx])
+    del out, batch
+    torch.cuda.empty_cache()
+    flips = _check_sample(subset(pop, idx), sample, np.arange(idx.size), orc.make_cfg(), tag="national")
+    assert not flips, flips
+
+
 def test_c4_commercial_dc_1m_sample_vs_oracle(engine_dc):
     """C4 per GPU (8M commercial agents over 8 GPUs): demand charges billed
     (extension mode), battery run.  Demand charges make the objective
