@@ -190,7 +190,11 @@ def dist_env():
 
 def cpu_baseline(pop, seconds: float, threads: int, replan_hours: int = 24):
     """Time the CPU oracle ('port' of the reference semantics) on a bounded
-    sample of the same workload (first agents of rank 0's shard)."""
+    sample of the same workload (first agents of rank 0's shard), on every
+    host core this process may run on (len(os.sched_getaffinity(0)), SURVEY
+    8(d)(ii)): `value`.  The box's OMP_NUM_THREADS share (its CPU allotment
+    for one GPU) is timed beside it as a secondary figure.  Each timed window
+    cycles over the sample until `seconds` have passed."""
     from oracle import oracle as orc
     from tests.helpers import oracle_population
     from dgen_amd.config import EngineConfig
@@ -201,24 +205,33 @@ def cpu_baseline(pop, seconds: float, threads: int, replan_hours: int = 24):
         avail = os.cpu_count() or 1
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     share = min(avail, omp) if omp > 0 else avail
-    threads = share if threads <= 0 else max(1, min(threads, avail))
-    chunk = max(64, 32 * threads)
+    threads = avail if threads <= 0 else max(1, min(threads, avail))
     n_take = min(pop.cols["load_kwh"].size, 200_000)
     sub = {k: v[:n_take] for k, v in pop.cols.items()}
     opop = oracle_population(sub, pop.tariffs, pop.switches, pop.shapes, pop.cfs, pop.wholesale,
                              demand=pop.demand)
-    done, t0 = 0, time.perf_counter()
-    while True:
-        idx = list(range(done % n_take, min(done % n_take + chunk, n_take)))
-        _, bad = opop.run_batch_timed(cfg, threads, idx)
-        done += len(idx)
-        el = time.perf_counter() - t0
-        if el >= seconds or done >= n_take:
-            break
-    return {"value": done / el, "unit": "agents/s", "cores": threads, "kind": "port",
-            "host_cpus": os.cpu_count(), "affinity_cpus": avail, "omp_num_threads_env": omp or None,
-            "sample": f"{done} agents of the same synthetic workload ({pop.config}), "
-                      f"oracle/orc.c full per-agent driver, OpenMP x{threads}, {el:.1f} s"}
+
+    def window(nt, secs):
+        chunk = max(64, 32 * nt)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            lo = done % n_take
+            idx = list(range(lo, min(lo + chunk, n_take)))
+            opop.run_batch_timed(cfg, nt, idx)
+            done += len(idx)
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return done, el
+    done, el = window(threads, seconds)
+    res = {"value": done / el, "unit": "agents/s", "cores": threads, "kind": "port",
+           "host_cpus": os.cpu_count(), "affinity_cpus": avail, "omp_num_threads_env": omp or None,
+           "sample": f"{done} agent sizings over the first {n_take} agents of the same synthetic workload "
+                     f"({pop.config}), oracle/orc.c full per-agent driver, OpenMP x{threads}, {el:.1f} s"}
+    if share != threads:
+        d2, e2 = window(share, max(5.0, seconds / 3))
+        res["omp_share"] = {"value": d2 / e2, "cores": share,
+                            "sample": f"{d2} agent sizings, OpenMP x{share} (OMP_NUM_THREADS), {e2:.1f} s"}
+    return res
 
 
 def timed_region(step, steps: int, sync, dist_mod=None, device=None) -> float:
@@ -321,15 +334,10 @@ def main():
     # compact record (the battery case's final tariff, the batch's switches)
     dcols = pop.cols if batch.perm is None else {k: np.asarray(v)[batch.perm] for k, v in pop.cols.items()}
     recs = eng.tariff_records
-    dc_batch = eng.tables.n_demand > 0 and (not pop.skip_demand_charges or eng.tables.peak_units != 0)
-    hp = max(1, min(int(recs["P"].max()), 12))
-    nb_lds = 8 * 4 * hp * 128 + (16 * (eng.tables.max_dc_periods or 8) * 128 if dc_batch else 0) + 2 * 12 * 1024   # dgen_size_agents' gate
-    nb_on = batch.nb_scan and nb_lds <= 65536
-    dcr_on = dc_batch and args.replan_hours != 1
-    # dgen_size_agents' ts_split gate (12 KB more day buffer per wave)
-    ts_scan = (nb_on and bool(eng.tables.wholesale) and not dc_batch and args.replan_hours != 1 and
-               not args.no_hourly and
-               os.environ.get("DGEN_TS_SCAN", "1") != "0" and nb_lds + 2 * 12 * 1024 <= 65536)
+    # the record forms the kernels took in the last timed call (dgen_last_paths),
+    # not a restatement of dgen_size_agents' gates
+    lp = eng.last_paths()
+    nb_on, dcr_on, ts_scan = bool(lp["nb_scan"]), bool(lp["dcr_on"]), bool(lp["ts_split"])
     tf_dev = out["tariff_final"].cpu().numpy()
     paths = scratch_paths(dcols, recs, tf_dev, battery=not args.no_batt,
                           skip_dc=pop.skip_demand_charges, nb_scan=nb_on, dcr_on=dcr_on,

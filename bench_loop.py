@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--hourly-chunk", type=int, default=None,
                     help="re-size chunks of this many agents for the state export")
     ap.add_argument("--no-export", action="store_true", help="skip the per-state hourly export")
+    ap.add_argument("--cut-tol", type=float, default=0.02,
+                    help="plan_partition tol: a rank cut snaps to a state boundary within this share of "
+                         "the per-rank cost (0: cut inside states wherever balance puts the cut)")
     args = ap.parse_args()
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -90,7 +93,7 @@ def main():
         for s in range(len(STATES)):
             smp = make_population(args.config, 2000, tables=T, agent_seed=20268000 + s, state_pool=[s])
             cost[s] = P.cost_per_agent(smp.cols, naep_row[smp.cols["cf_row"]]).mean()
-        plan = P.plan_partition(sizes, cost, ws)
+        plan = P.plan_partition(sizes, cost, ws, tol=args.cut_tol)
         pop, ag = shard_population(T, plan, rank)
         secs, ids = split_state_members(args.config, plan)
         sg = P.split_groups(plan, rank, secs, ids)
@@ -141,7 +144,8 @@ def main():
     if rank == 0:
         line = {
             "metric": "agent-years/sec (national diffusion loop: sizing + diffusion + attachment "
-                      "+ state export + RCCL totals)",
+                      "+ state export + all-reduced state totals)",
+            "exchange_backend": (None if ws == 1 else ("RCCL" if backend == "nccl" else backend)),
             "value": n_total * len(years) / el, "unit": "agent-years/s", "n_gpus": ws,
             "steps": len(years), "warmup": args.warmup, "ms_per_step": el / len(years) * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",

@@ -290,6 +290,11 @@ def _device_planes(df):
            (a._plane.inv is not None and not bool((a._plane.inv == p0.inv).all())) for a in arrs):
         return None
     cols = p0.device_columns()[arrs[0]._idx]
+    if np.unique(cols).size != cols.size:
+        # two frame rows on one plane column (pd.concat([df, df]), a take with
+        # repeats): each row carries its own weights, which a scatter into
+        # device columns cannot hold -- the host path sums them row by row
+        return None
     return tuple(a._plane.t for a in arrs), cols
 
 

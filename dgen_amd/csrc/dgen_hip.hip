@@ -4453,6 +4453,7 @@ struct dgen_ctx {
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
     int battery;       // PV+battery forward run (dgen_set_battery)
     int nb_scan;       // battery-case split in the hourly scan: its per-month entry capacity, 0 = off (dgen_set_nb_scan)
+    int32_t last_paths[DGEN_PATHS_N] = {0};   // the record forms the last dgen_size_agents call took (dgen_last_paths)
     int head;          // next ring slot to record
     int pending;       // recorded, not yet folded
     double sum_ms[3];
@@ -4775,6 +4776,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // take this form must not depend on the demand records being on)
     const bool ts_split = nb_scan && T->wholesale != nullptr && !dc && c->ts_scan && lds_ts <= 65536 &&
                           c->cfg.batt_update_hours != 1 && hourly;
+    c->last_paths[0] = nb_scan ? 1 : 0;
+    c->last_paths[1] = dcr_on ? 1 : 0;
+    c->last_paths[2] = ts_split ? 1 : 0;
+    c->last_paths[3] = dc ? 1 : 0;
+    c->last_paths[4] = T->max_periods;
+    c->last_paths[5] = dc_nq;
     // two agents per wave when every analysis period fits 32 lanes, unless the
     // build guard withdrew that kernel's 32-lane instantiation (DGEN_NO2_*)
     const bool fits32 = A->max_years >= 1 && A->max_years <= 32;
@@ -5142,6 +5149,12 @@ int32_t dgen_set_pipeline(dgen_ctx* c, int32_t chunks) {
     }
     c->chunks = chunks;
     return DGEN_OK;
+}
+
+int32_t dgen_last_paths(dgen_ctx* c, int32_t* out, int32_t n_out) {
+    if (!c || !out || n_out < 0) { set_err("dgen_last_paths: null argument"); return DGEN_E_ARG; }
+    for (int k = 0; k < n_out && k < DGEN_PATHS_N; k++) out[k] = c->last_paths[k];
+    return DGEN_PATHS_N;
 }
 
 int32_t dgen_kernel_times(dgen_ctx* c, double* ms_size, double* ms_hourly, double* ms_finance) {

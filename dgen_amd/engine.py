@@ -404,6 +404,14 @@ class Engine:
         c = _lib.DCR_CAP if cap is True else int(cap)
         _lib.check(self.lib.dgen_set_dc_records(self.ctx, c), "dgen_set_dc_records")
 
+    def last_paths(self) -> Dict[str, int]:
+        """The record forms the last size() call took (dgen_last_paths): what
+        the kernels actually did, for the bench's byte accounting."""
+        a = (ctypes.c_int32 * 6)()
+        _lib.check(self.lib.dgen_last_paths(self.ctx, a, 6), "dgen_last_paths")
+        keys = ("nb_scan", "dcr_on", "ts_split", "dc", "max_periods", "dc_periods")
+        return dict(zip(keys, (int(v) for v in a)))
+
     def kernel_times(self):
         """Average per-launch device time (ms) of the three sizing kernels over
         the calls since the last query, from HIP events on the launch stream."""

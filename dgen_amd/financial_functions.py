@@ -37,13 +37,45 @@ _engine_lock = threading.Lock()
 _sql_sources: Dict[int, SqlProfileSource] = {}
 
 
+def worker_device() -> int:
+    """The GPU this process sizes on, chosen before anything touches the GPU.
+
+    * ``LOCAL_RANK`` (a torchrun rank): that device;
+    * otherwise this process's index among its parent's children -- the
+      reference's caller spawns ``LOCAL_CORES`` pool workers per model year
+      (``dgen_model.py:309-317``, 8-32 per node), numbered consecutively by
+      multiprocessing (``current_process()._identity``), so worker k takes
+      device (k - 1) mod the device count and the pool spreads evenly over the
+      node's GPUs with ``dgen_model.py`` unchanged;
+    * ``DGEN_DEVICES`` (e.g. ``"0,2,4,6"``) restricts that rotation to a list;
+    * the main process (the reference's ``cores=None`` path): device 0 (or the
+      list's first).
+    ``torch.cuda.device_count()`` does not initialise HIP on this image, so
+    the spawned worker may ask it before its Engine opens the device."""
+    lr = os.environ.get("LOCAL_RANK")
+    if lr is not None and lr.strip() != "":
+        return int(lr)
+    import multiprocessing as mp
+    ident = getattr(mp.current_process(), "_identity", ()) or ()
+    k = int(ident[-1]) - 1 if ident else 0
+    devs = os.environ.get("DGEN_DEVICES", "").strip()
+    if devs:
+        lst = [int(x) for x in devs.split(",") if x.strip()]
+        if not lst:
+            raise ValueError(f"DGEN_DEVICES={devs!r} names no device")
+        return lst[k % len(lst)]
+    import torch
+    n = int(torch.cuda.device_count())
+    return k % n if n > 0 else 0
+
+
 def get_engine():
-    """Process-wide Engine on this rank's GPU (LOCAL_RANK, else 0)."""
+    """Process-wide Engine on this process's GPU (worker_device())."""
     global _engine
     with _engine_lock:
         if _engine is None:
             from .engine import Engine
-            _engine = Engine(int(os.environ.get("LOCAL_RANK", "0")))
+            _engine = Engine(worker_device())
         return _engine
 
 
@@ -158,10 +190,96 @@ def _device_tables(eng, src: ProfileStore, b: PopulationBuilder):
     eng.set_switches(b.switches.array())
 
 
+def agent_device_bytes(eng) -> int:
+    """HBM one agent of a drop-in call holds while it is sized: the three fp64
+    hourly planes (3 x 8760 x 8 B), its share of the workspace (bins, scratch
+    plane, split records: dgen_workspace_bytes at a scratch slot per agent),
+    the yearly and scalar outputs twice (the caller-order gather before the
+    download) and the agent columns."""
+    k = 4096
+    ws = int(eng.lib.dgen_workspace_bytes(k, k)) // k
+    yearly = len(_lib.OUTPUT_YEARLY) * (_lib.MAXY + 1) * 8
+    return 3 * NH * 8 + ws + 2 * (yearly + 8 * len(_lib.OUTPUT_SCALARS)) + 8 * len(_lib.AGENT_COLUMNS)
+
+
+def device_rows_budget(eng, frac: float = 0.3) -> int:
+    """Largest agent count one sizing call puts on the device at a time:
+    ``DGEN_MAX_ROWS`` if set, else frac x (free HBM + this process's cached,
+    unused blocks) / agent_device_bytes.  frac 0.3: two sub-batches are
+    resident at once (one sizing while the previous one's planes download),
+    and other workers sharing the GPU (a spawn pool larger than the node's GPU
+    count) see the rest.  At least 1024."""
+    env = os.environ.get("DGEN_MAX_ROWS", "").strip()
+    if env:
+        return max(1, int(env))
+    import torch
+    free, _total = torch.cuda.mem_get_info(eng.dev)
+    spare = torch.cuda.memory_reserved(eng.dev) - torch.cuda.memory_allocated(eng.dev)
+    return max(1024, int(frac * (free + max(spare, 0)) / agent_device_bytes(eng)))
+
+
 def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[dict] = None,
                 net_weights: Optional[Tuple[np.ndarray, np.ndarray]] = None, hourly_async: bool = False,
-                hourly_device: bool = False):
-    """Size the batch; net_weights = (number_of_adopters, non-adopters) per
+                hourly_device: bool = False, max_rows: Optional[int] = None):
+    """Size the batch in sub-batches of at most max_rows agents (default
+    device_rows_budget()): a frame larger than the device budget is cut into
+    consecutive caller-order row ranges, each sized in its own device call
+    with its own outputs; the host outputs are concatenated (an agent's
+    outputs do not depend on the other agents of its batch, so they are the
+    bits a single call gives), net_sum_kw is the sum of the sub-batches'
+    (to rounding: 1e-12 relative), and the hourly planes are one segmented
+    plane over the sub-batches' (hourly_column._Segments).  At most two
+    sub-batches are on the device at once: sub-batch k sizes while k - 1's
+    planes download, and k waits for k - 2's.  hourly_device with more than
+    one sub-batch: the planes come to the host instead (keeping every
+    sub-batch's planes in HBM would undo the bound)."""
+    n = len(cols["load_kwh"])
+    if max_rows is None:
+        max_rows = device_rows_budget(get_engine())
+    max_rows = max(1, int(max_rows))
+    if n <= max_rows:
+        return _run_device_once(b, cols, src, timing, net_weights, hourly_async, hourly_device)
+    from .hourly_column import _Segments
+    parts = []
+    tm_sum: dict = {}
+    for lo in range(0, n, max_rows):
+        hi = min(n, lo + max_rows)
+        if len(parts) >= 2:            # bound: k - 2's planes have left the device
+            for name in _lib.OUTPUT_HOURLY:
+                p = parts[-2].get(name)
+                if p is not None and hasattr(p, "result"):
+                    p.result()
+        sub = {k: v[lo:hi] for k, v in cols.items()}
+        nw = None if net_weights is None else tuple(np.asarray(w)[lo:hi] for w in net_weights)
+        tm: dict = {}
+        parts.append(_run_device_once(b, sub, src, tm, nw, hourly_async=True, hourly_device=False))
+        for k, v in tm.items():
+            tm_sum[k] = tm_sum.get(k, 0.0) + v
+    o = {}
+    for name, _ in _lib.OUTPUT_SCALARS:
+        o[name] = np.concatenate([p[name] for p in parts])
+    for name in _lib.OUTPUT_YEARLY:
+        o[name] = np.concatenate([p[name] for p in parts])
+    for name in _lib.OUTPUT_HOURLY:
+        segs = _Segments([(p[name], np.arange(p[name].n, dtype=np.int64), None, False) for p in parts])
+        if hourly_async or hourly_device:
+            o[name] = segs
+        else:
+            o[name] = segs.result()
+    if net_weights is not None:
+        net = parts[0]["net_sum_kw"].copy()
+        for p in parts[1:]:
+            net += p["net_sum_kw"]
+        o["net_sum_kw"] = net
+    if timing is not None:
+        timing.update(tm_sum, sub_batches=len(parts))
+    return o
+
+
+def _run_device_once(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[dict] = None,
+                     net_weights: Optional[Tuple[np.ndarray, np.ndarray]] = None, hourly_async: bool = False,
+                     hourly_device: bool = False):
+    """Size the batch in one device call; net_weights = (number_of_adopters, non-adopters) per
     caller row also returns o["net_sum_kw"], size_chunk's hourly aggregate
     summed on the device from the planes in place (k_state_hourly, one
     segment, fixed order) instead of a host loop over the agents.
@@ -309,7 +427,7 @@ def _yearly_lists(a: np.ndarray, n1: np.ndarray, fmt: str = "list"):
 
 
 def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
-               timing: Optional[dict] = None, net_weights=None):
+               timing: Optional[dict] = None, net_weights=None, max_rows: Optional[int] = None):
     """The batched form of calc_system_size_and_performance over a whole agent
     frame (what size_chunk needs), built by column: the frame is columnised
     at once (columnar.columnize_frame), sized in one device call, and the
@@ -330,7 +448,10 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
     lists throughout) or "none" (no hourly columns, yearly lists).  The device
     computes the hourly planes in fp64 for this path (the PCIe-bound phase:
     3 x 8760 x 8 B per agent), downloaded while the frame is assembled.
-    timing: filled with the host / device phases (seconds)."""
+    timing: filled with the host / device phases (seconds).  max_rows: the
+    most agents on the device at once (default device_rows_budget(): a frame
+    larger than free HBM allows is sized in consecutive sub-batches with the
+    same outputs, _run_device)."""
     import time
     if rate_switch_table is None:
         raise AttributeError("'NoneType' object has no attribute 'loc' (rate_switch_table is required)")
@@ -342,7 +463,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
     t1 = time.perf_counter()
     dev_t: dict = {}
     o = _run_device(b, cols, src, dev_t, net_weights, hourly_async=hourly in ("lazy", "array", "list"),
-                    hourly_device=hourly == "device")
+                    hourly_device=hourly == "device", max_rows=max_rows)
     t2 = time.perf_counter()
     ids = df["agent_id"].tolist() if "agent_id" in df else list(df.index)
     _raise_for_status(o["status"], ids)
@@ -416,7 +537,7 @@ def size_frame(df: pd.DataFrame, con, rate_switch_table, hourly: str = "lazy",
 
 
 def size_chunk(static_agents_df: pd.DataFrame, sectors, rate_switch_table, mode="simple",
-               hourly: str = "lazy", timing: Optional[dict] = None):
+               hourly: str = "lazy", timing: Optional[dict] = None, max_rows: Optional[int] = None):
     """ff:1136 -- size a chunk; returns (df_out, agg) with
     agg["net_sum_kw"][h] = sum_agents adopter[h] * n_adopt + baseline[h] * (n_cust - n_adopt)."""
     global _worker_conn
@@ -431,7 +552,7 @@ def size_chunk(static_agents_df: pd.DataFrame, sectors, rate_switch_table, mode=
     # on the device; the reference's running sum in agent order and the
     # kernel's fixed-order tree agree to rounding (parity test: 1e-12 relative)
     df_out, o = size_frame(df, _worker_conn, rate_switch_table, hourly=hourly, timing=timing,
-                           net_weights=(n_adopt, n_non))
+                           net_weights=(n_adopt, n_non), max_rows=max_rows)
     df_out = df_out.drop(columns=[c for c in _DROP if c in df_out.columns])
     agg = {"mode": "simple", "n_hours": NH, "net_sum_kw": o["net_sum_kw"].tolist()}
     return df_out, agg

@@ -297,6 +297,18 @@ class YearLoop:
                  plan=None, split: Optional[SplitGroups] = None):
         import torch
         from .engine import profile_order
+        # plan and split come together: a split state's members must be
+        # numbered by the plan (agents["member"]) and its groups gathered
+        # (split), or its rows, initial shares and allocation go wrong silently
+        if split is not None and plan is None:
+            raise ValueError("YearLoop: split groups given without the plan they were built from")
+        if plan is not None and plan.split_states():
+            if split is None:
+                raise ValueError(f"YearLoop: the plan splits states {plan.split_states()} across ranks "
+                                 "but no split groups were given (partition.split_groups)")
+            if "member" not in agents:
+                raise ValueError("YearLoop: the plan splits states across ranks but agents['member'] "
+                                 "(each agent's index within its state) is missing")
         self.eng, self.tables = engine, tables
         self.first_year = int(first_year)
         self.hourly_export, self.hourly_chunk = bool(hourly_export), hourly_chunk

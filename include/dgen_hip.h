@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 10
+#define DGEN_ABI_VERSION 11
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_DEFAULT_HOURLY_SPLIT 2   /* parts of a chunk's hourly scan, each on its own stream */
@@ -532,6 +532,19 @@ int32_t dgen_finance_series(dgen_ctx* ctx, const dgen_outputs* O, const int32_t*
  * call's chunks (HIP events recorded on the stream each kernel runs on).
  * Returns the number of calls averaged (>= 0) or an error code.              */
 int32_t dgen_kernel_times(dgen_ctx* ctx, double* ms_size, double* ms_hourly, double* ms_finance);
+
+/* The record forms the last dgen_size_agents call on ctx took, as the call
+ * decided them from its tables, settings and LDS limits (ABI 11): out[0] the
+ * battery case's net-billing split built in the scan (dgen_set_nb_scan),
+ * out[1] battery-case demand records (dgen_set_dc_records), out[2] the TS
+ * sell-rate agents' own split scan, out[3] the demand machinery on (demand
+ * charges billed or kWh/kW tier peaks), out[4] the period count the kernels'
+ * LDS is laid out for (the tables' max_periods after the call's adjustments),
+ * out[5] the demand periods per record.  Writes min(n_out, DGEN_PATHS_N)
+ * values; returns DGEN_PATHS_N.  For byte accounting (bench.py); replaces
+ * nothing in the reference.                                                 */
+#define DGEN_PATHS_N 6
+int32_t dgen_last_paths(dgen_ctx* ctx, int32_t* out, int32_t n_out);
 
 /* Pipeline depth of dgen_size_agents: the batch is cut into `chunks` pieces;
  * k_size of piece j+1 runs on the caller's stream while k_hourly_batt and

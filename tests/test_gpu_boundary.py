@@ -209,3 +209,63 @@ def test_device_mode_export_reduces_planes_in_place():
     j = len(df) // 2
     assert np.array_equal(np.asarray(dv["adopter_net_hourly_with_batt"].iloc[j]),
                           np.asarray(arr["adopter_net_hourly_with_batt"].iloc[j]))
+
+
+def test_sub_batched_frame_equals_one_call():
+    """A frame larger than the device budget (forced: 50k rows) is sized in
+    consecutive sub-batches (financial_functions._run_device): every output --
+    scalars, yearly lists, the three fp64 hourly planes, the rewritten tariff
+    columns -- bit-identical to one call over the whole frame; size_chunk's
+    net_sum_kw (a sum over the sub-batches' sums) within 1e-12 relative."""
+    from dgen_amd.synth import reference_frame
+    df, store, table = reference_frame(200_000)
+    ff._worker_conn = store
+    tm1, tm4 = {}, {}
+    one, agg1 = ff.size_chunk(df, None, table, "simple", timing=tm1, max_rows=len(df))
+    sub, agg4 = ff.size_chunk(df, None, table, "simple", timing=tm4, max_rows=50_000)
+    assert "sub_batches" not in tm1 and tm4["sub_batches"] == 4
+    assert list(sub.index) == list(df.index) and list(sub.columns) == list(one.columns)
+    for k in SCALARS + ["payback_period", "tariff_id", "nem_system_kw_limit"]:
+        assert np.array_equal(one[k].to_numpy(), sub[k].to_numpy()), k
+    for k in ARRAYS:
+        assert np.array_equal(one[k].array.to_2d(), sub[k].array.to_2d()), k
+    for k in ("baseline_net_hourly", "adopter_net_hourly_pvonly", "adopter_net_hourly_with_batt"):
+        a = one[k].array.to_2d()
+        seg = sub[k].array._plane
+        assert len(seg.parts) == 4
+        for (p, idx, _), lo in zip(seg.parts, seg.off[:-1]):
+            assert np.array_equal(p.result()[idx], a[lo:lo + idx.shape[0]]), k
+        del a
+    n1, n4 = np.asarray(agg1["net_sum_kw"]), np.asarray(agg4["net_sum_kw"])
+    assert np.allclose(n1, n4, rtol=1e-12, atol=0.0)
+    # the per-row form reads the same cells
+    j = 123_457
+    assert np.array_equal(np.asarray(sub["adopter_net_hourly_with_batt"].iloc[j]),
+                          np.asarray(one["adopter_net_hourly_with_batt"].iloc[j]))
+
+
+def test_device_mode_export_with_repeated_rows_uses_host_sums():
+    """A frame whose rows repeat a plane column (pd.concat([df, df])): the
+    device export cannot scatter two rows' weights into one column, so it
+    takes the host path -- the same records as the array mode's frame."""
+    from dgen_amd import attachment as ga
+    from dgen_amd.synth import reference_frame
+    df, store, table = reference_frame(600)
+    ff._worker_conn = store
+    arr, _ = ff.size_chunk(df, None, table, "simple", hourly="array")
+    dv, _ = ff.size_chunk(df, None, table, "simple", hourly="device")
+    rng = np.random.default_rng(5)
+    recs = []
+    w = {"customers_in_bin": rng.uniform(10, 400, 2 * len(df)),
+         "number_of_adopters": rng.uniform(0, 20, 2 * len(df)),
+         "batt_kw_cum_last_year": rng.uniform(0, 30, 2 * len(df)),
+         "batt_adopters_added_this_year": rng.integers(0, 3, 2 * len(df))}
+    for frame in (arr, dv):
+        f = pd.concat([frame, frame])
+        for k, v in w.items():
+            f[k] = v
+        recs.append(ga.export_state_hourly_with_storage_mix("eng", "s", "o", 2027, f))
+    a, d = recs
+    assert a["state_abbr"].tolist() == d["state_abbr"].tolist()
+    for x, y in zip(a["net_sum"], d["net_sum"]):
+        assert np.array_equal(np.asarray(x), np.asarray(y))

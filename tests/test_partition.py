@@ -202,3 +202,28 @@ def test_split_states_gloo_world2_match_one_pool():
         merged.update(added)
     assert merged == ref_added
     assert sum(ref_added.values()) > 0
+
+
+def test_year_loop_rejects_plan_split_misuse():
+    """YearLoop needs plan and split groups together when the plan cuts a
+    state, and the members' within-state numbering from the plan:
+    each misuse raises before anything touches the device."""
+    import types
+
+    import pytest
+
+    from dgen_amd.year_loop import YearLoop
+    sizes = P.census_sizes(SIZES_N)
+    cost = np.ones(sizes.size)
+    cost[STATES.index("CA")] = 50.0
+    plan = P.plan_partition(sizes, cost, 2, chunk=CHUNK, tol=0.0)
+    assert plan.split_states()
+    pop = types.SimpleNamespace(cols={"load_kwh": np.zeros(4)})
+    ag = {"state": np.zeros(4, np.int64), "member": np.arange(4)}
+    sg = object()
+    with pytest.raises(ValueError, match="no split groups"):
+        YearLoop(None, pop, ag, None, plan=plan, split=None)
+    with pytest.raises(ValueError, match="without the plan"):
+        YearLoop(None, pop, ag, None, plan=None, split=sg)
+    with pytest.raises(ValueError, match="member"):
+        YearLoop(None, pop, {"state": ag["state"]}, None, plan=plan, split=sg)
