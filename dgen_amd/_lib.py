@@ -113,7 +113,7 @@ DEFAULT_HOURLY_SPLIT = 2   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_SPLIT
 EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
-    "dgen_kernel_times", "dgen_last_paths", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
+    "dgen_kernel_times", "dgen_last_paths", "dgen_set_dc_prebuild", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
     "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_set_ts_rows", "dgen_set_dc_records", "dgen_hourly_planes", "dgen_export_plane", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
     "dgen_finance_series", "dgen_year_inputs", "dgen_initial_market_shares", "dgen_rows_seq_sum",
 ]
@@ -154,6 +154,8 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.dgen_brent_selftest.restype = _i32
     L.dgen_brent_selftest.argtypes = [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i32, _vp,
                                       _vp, _vp]
+    L.dgen_set_dc_prebuild.restype = _i32
+    L.dgen_set_dc_prebuild.argtypes = [_vp, _i32]
     L.dgen_last_paths.restype = _i32
     L.dgen_last_paths.argtypes = [_vp, ctypes.POINTER(_i32), _i32]
     L.dgen_kernel_times.restype = _i32

@@ -2391,6 +2391,7 @@ struct DcEnv {
     double2* lines;   // [12][DCP][DC_NL] (L, g)
     double* maxl;     // [12][DCP] max load (the no-system peak)
     int* cnt;         // [12][DCP] lines kept (0 = period absent from the month)
+    int* tag;         // k_dc_env: 1 + the tariff built for, -(1 + it) when a group overflowed, 0 none
 };
 constexpr size_t DCW_BYTES = (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double) + sizeof(int)) + 16;
 
@@ -2400,6 +2401,7 @@ __device__ __forceinline__ DcEnv dc_env_at(void* base, int64_t i) {
     e.lines = reinterpret_cast<double2*>(b);
     e.maxl = reinterpret_cast<double*>(b + (size_t)12 * DCP * DC_NL * sizeof(double2));
     e.cnt = reinterpret_cast<int*>(b + (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double)));
+    e.tag = reinterpret_cast<int*>(b + (size_t)12 * DCP * (DC_NL * sizeof(double2) + sizeof(double) + sizeof(int)));
     return e;
 }
 
@@ -3188,8 +3190,7 @@ __device__ __forceinline__ void yl_build_bins(const dgen_tariff& t, const double
 struct YLoan {
     int N, term, market, sl_years, depr_type;
     double r_loan, loan_f, itc_pct, itc_max, ins_rate, debt_frac, fed, sta, rr;
-    // lane (year y = lane + 1) factors
-    double df;        // rr^y
+    // lane (year y = lane + 1) factor
     double ins_esc;   // (1 + infl)^(y - 1)
 };
 
@@ -3214,7 +3215,6 @@ __device__ __forceinline__ YLoan yl_make_loan(const dgen_agents& A, const dgen_c
     L.debt_frac = (100.0 - (A.down_payment[i] * 100.0)) * 0.01;
     L.sl_years = cfg.depr_sl_years;
     L.depr_type = is_res ? 0 : 2;
-    L.df = pow_seq(L.rr, y);
     L.ins_esc = pow_seq(1.0 + infl, y - 1);
     return L;
 }
@@ -3226,7 +3226,7 @@ struct YFlow {
 // Cash flow of one lane's year + the wave reductions (Cashloan subset).
 template <int LPA>
 __device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev, int y,
-                                             const Seg<LPA>& g, bool active) {
+                                             const Seg<LPA>& g, bool active, const YLds& S) {
     double debt = L.debt_frac * C;
     double pmt = 0.0;
     if (L.term > 0 && debt != 0.0) {
@@ -3259,8 +3259,29 @@ __device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev
     double pb = ev - oe + taxsav;
     if (!active) { atcf = 0.0; pb = 0.0; }
     YFlow f;
-    f.npv = -(C - debt) + g.sum(atcf * L.df);
-    double cum = -C + g.incl_scan(pb);
+    // NPV and the payback's cumulative flow in the oracle's order, which is
+    // SSC's (libfin::npv: acc = rr acc + atcf_y for y = N .. 1, npv = atcf_0 +
+    // acc rr; the cumulative sum year by year from -C), so the search's
+    // objective carries no re-association of its own: scipy's parabolic step
+    // divides differences of nearly equal objectives and amplifies a few ulps
+    // into a different Brent path.  The lanes' flows go
+    // through two rows of the lane area (free between bills) and every lane
+    // of the segment runs the chains on broadcast reads; lanes past the
+    // analysis period hold 0, so chaining over all LPA lanes gives the same bits.
+    wave_lds_sync();                          // the bill's last reads of the lane area
+    S.lane[0] = atcf;
+    S.lane[WAVE] = pb;
+    wave_lds_sync();
+    const double* col = S.lane - g.lane + g.base;
+    double acc = 0.0, run = -C, cum = -C;
+#pragma unroll 8
+    for (int k = LPA - 1; k >= 0; k--) acc = L.rr * acc + col[k];
+#pragma unroll 8
+    for (int k = 0; k < LPA; k++) {
+        run = run + col[WAVE + k];
+        cum = (g.sl == k) ? run : cum;
+    }
+    f.npv = -(C - debt) + acc * L.rr;
     const int k = g.first(active && cum > 0.0);          // first paying year - 1
     f.payback = 1e99;
     if (k >= 0) {
@@ -3325,6 +3346,7 @@ template <int LPA>
 __device__ __forceinline__ bool yl_dc_ready(YCtx<LPA>& c, const DcEnv& E, DcStage* st, const Seg<LPA>& g) {
     if (!E.lines) return false;
     if (c.env_tag == c.tariff + 1) return true;
+    if (c.env_tag == -(c.tariff + 1)) return false;        // k_dc_env found a group over DC_NL lines
     const bool ok = yl_dc_build_any(c.dem, c.src, c.tlo, c.thi, E, st, g);
     c.env_tag = ok ? c.tariff + 1 : 0;
     return ok;
@@ -3479,7 +3501,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
     double wo = c.wo1 * c.r_y;
     double ev = wo - w;
     PH_T0(tc);
-    YFlow f = yl_cashflow(c.loan, total, ev, c.y, c.g, c.active);
+    YFlow f = yl_cashflow(c.loan, total, ev, c.y, c.g, c.active, c.S);
     PH_ADD_KS(14, tc, c.g.sl == 0);            // cash flow + NPV + payback
     c.last.total = total;
     c.last.ev = ev;
@@ -3505,7 +3527,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 template <int LPA, bool DC, bool NET, bool PK>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
-         void* dcws, char* nbws) {
+         void* dcws, char* nbws, int dc_pre) {
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -3530,7 +3552,10 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     c.env_tag = 0;
     c.dc_nq = (T.max_dc_periods > 0 && T.max_dc_periods <= DCP) ? T.max_dc_periods : DCP;
     if constexpr (DC) {
-        if (dcws) c.env = dc_env_at(dcws, i);
+        if (dcws) {
+            c.env = dc_env_at(dcws, i);
+            c.env_tag = dc_pre ? *c.env.tag : 0;          // k_dc_env's, this call
+        }
         // the segment's envelope stage sits after the year-lane layout
         c.stg = reinterpret_cast<DcStage*>(reinterpret_cast<char*>(dyn_lds) +
                                            ylds_bytes(half, LPA, PK && T.peak_units != 0)) + lane / LPA;
@@ -3679,6 +3704,248 @@ __device__ __forceinline__ int first_eval_tariff(const dgen_tables& T, const dge
         if (nt >= 0) t = nt;
     }
     return t;
+}
+
+// ---------------------------------------------------------------------------
+// Demand envelopes of every agent's first-evaluation tariff (first_eval_tariff),
+// built ahead of k_size by day lanes (k_dc_env).  The hour-lane build inside
+// k_size (yl_dc_build_coop) reads each profile value with its own 4-byte load
+// and walks the year twice; at k_size's 256 VGPRs and 2 waves per SIMD those
+// walks wait on their loads (C4 200k: build + stage 55 % of k_size's cycles).
+// Here one wave takes one agent and two months at a time: lane l of half h
+// holds day l of month 2j + h, the day's 24 hours of load shape and cf come
+// in as 6 + 6 16-B loads (consecutive lanes read consecutive 96-B days of the
+// row), both passes run on those registers, and the reductions over a month's
+// days are 32-lane butterflies.  Same rule as yl_dc_build: per (month, demand
+// period) A and B are the first maximisers (ties to the earlier hour) of the
+// import at tlo and at thi, the lines kept are A, B and every other hour above
+// their hull at the crossing less the 1e-10 slack, more than DC_NL lines is an
+// overflow (tag < 0: k_size then bills that agent with the hourly pass without
+// rebuilding).  An evaluation takes the max over the kept lines, so results do
+// not depend on which build ran (the kept set is the same; its order is hour
+// order here).  k_size uses the envelopes when its tariff is the tag's.
+// ---------------------------------------------------------------------------
+constexpr int DCE_WPB = 4;          // agents (one wave each) per block
+
+// cf_per_kw's common path (|x| <= 2e7, where it equals x / 1e6 exactly); the
+// kernel checks the range per day and leaves an agent with a larger value to
+// k_size's build
+__device__ __forceinline__ double cf_per_kw_fast(int32_t x) {
+    const double a = (double)x;
+    constexpr double inv = 1.0 / 1e6;
+    const double q = a * inv;
+    const double r = __builtin_fma(-q, 1e6, a);
+    return __builtin_fma(r, inv, q);
+}
+
+// first maximiser over the lane's 32-lane half: larger value, ties to the
+// earlier hour
+__device__ __forceinline__ void dce_first_max(double& v, int& h) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o, WAVE);
+        const int oh = __shfl_xor(h, o, WAVE);
+        const bool t = (ov > v) | ((ov == v) & (oh < h));    // selects, no branch
+        v = t ? ov : v;
+        h = t ? oh : h;
+    }
+}
+
+template <int NQ>
+__global__ void __launch_bounds__(WAVE * DCE_WPB) __attribute__((amdgpu_waves_per_eu(NQ <= 4 ? 3 : 2)))
+k_dc_env(dgen_tables T, dgen_agents A, dgen_cfg cfg, int64_t i0, int64_t i1, void* dcws) {
+    const int lane = threadIdx.x & (WAVE - 1);
+    // the wave's agent: wave-uniform (readfirstlane), so its scalars and
+    // addresses live in SGPRs
+    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int64_t i = i0 + (int64_t)blockIdx.x * DCE_WPB + wid;
+    if (i >= i1) return;
+    const DcEnv E = dc_env_at(dcws, i);
+    const int lr = A.load_row[i], cr = A.cf_row[i];
+    const double kwh = A.load_kwh[i];
+    const double max_load = kwh / T.cf_naep[cr];                    // ff:440-444, as k_size
+    const double low = max_load * 0.8, high = max_load * 1.25;
+    const int N = A.econ_life[i];
+    const int t0 = (isfinite(low) && isfinite(high)) ? first_eval_tariff(T, A, i, low, high) : -1;
+    const dgen_demand* D = nullptr;
+    if (t0 >= 0 && t0 < T.n_tariffs && N >= 1 && N <= MAXY) {
+        // k_size's record for the tariff (yl_set_tariff): the kWh/kW tier
+        // peaks' where the batch bills those (PK kernels), else the charges'
+        const dgen_tariff& t = T.tariffs[t0];
+        D = (T.peak_units && peak_unit(t)) ? tariff_peaks(T.demand, T.n_demand, t)
+                                           : tariff_demand(T.demand, T.n_demand,
+                                                           T.peak_units ? cfg.skip_demand_charges == 0 : true, t);
+    }
+    if (!D) {
+        if (lane == 0) *E.tag = 0;
+        return;
+    }
+    const double sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+    const double sN = pow_seq(sys_base, N - 1);                    // k_size's s_y of year N
+    const double s_lo = sN < 1.0 ? sN : 1.0, s_hi = sN > 1.0 ? sN : 1.0;
+    const double tlo = (((low * 1000.0) * 0.96) / 1000.0) * s_lo;
+    const double thi = (((high * 1000.0) * 0.96) / 1000.0) * s_hi;
+    const double ls = kwh / T.shape_sum[lr];
+    const float* const shp = T.shapes + (int64_t)lr * NH;
+    const int32_t* const cfp = T.cfs + (int64_t)cr * NH;
+    const int nq = (T.max_dc_periods > 0 && T.max_dc_periods <= DCP) ? T.max_dc_periods : DCP;
+    const int dl = lane & 31;
+    bool ok = true;
+#pragma unroll 1
+    for (int j = 0; j < 6; j++) {
+        const int m = 2 * j + (lane >> 5);
+        const int d0 = c_month_start_day[m], d1 = c_month_start_day[m + 1];
+        const bool act = d0 + dl < d1;
+        const int d = act ? d0 + dl : d1 - 1;                      // idle lanes read a real day
+        const uint8_t* sc = ((d % 7) >= 5) ? D->wkend[m] : D->wkday[m];
+        float sh[24];
+        int32_t cv[24];
+        uint32_t pw[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const float4 a = reinterpret_cast<const float4*>(shp + d * 24)[k];
+            const int4 b = reinterpret_cast<const int4*>(cfp + d * 24)[k];
+            sh[4 * k] = a.x; sh[4 * k + 1] = a.y; sh[4 * k + 2] = a.z; sh[4 * k + 3] = a.w;
+            cv[4 * k] = b.x; cv[4 * k + 1] = b.y; cv[4 * k + 2] = b.z; cv[4 * k + 3] = b.w;
+            pw[k] = reinterpret_cast<const uint32_t*>(sc)[k];
+        }
+        bool big = false;
+#pragma unroll
+        for (int hh = 0; hh < 24; hh++) big = big | (cv[hh] > 20000000) | (cv[hh] < -20000000);
+        if (__ballot(big) != 0ull) {           // cf_per_kw's slow path: k_size builds this agent
+            if (lane == 0) *E.tag = 0;
+            return;
+        }
+        // periods present in the month (both day types: every month has both)
+        uint32_t mask = 0;
+#pragma unroll
+        for (int hh = 0; hh < 24; hh++) mask |= 1u << ((pw[hh >> 2] >> (8 * (hh & 3))) & 0xffu);
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) mask |= (uint32_t)__shfl_xor((int)mask, o, WAVE);
+        // pass 1: per period the lane's first maximisers at tlo / thi, max load
+        double av[NQ], bv[NQ], ml[NQ];
+        int ah[NQ], bh[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            av[q] = -INFINITY; bv[q] = -INFINITY; ml[q] = 0.0;
+            ah[q] = 0x7fffffff; bh[q] = 0x7fffffff;
+        }
+#pragma unroll
+        for (int hh = 0; hh < 24; hh++) {
+            const int p = (int)((pw[hh >> 2] >> (8 * (hh & 3))) & 0xffu);
+            const double L = (double)sh[hh] * ls;
+            const double gp = cf_per_kw_fast(cv[hh]);
+            const double vlo = L - gp * tlo, vhi = L - gp * thi;
+            const int h = d * 24 + hh;
+#pragma unroll
+            for (int q = 0; q < NQ; q++) {          // selects, no branches
+                const bool sel = act & (p == q);
+                const bool ua = sel & (vlo > av[q]), ub = sel & (vhi > bv[q]);
+                ml[q] = (sel & (L > ml[q])) ? L : ml[q];
+                av[q] = ua ? vlo : av[q];
+                ah[q] = ua ? h : ah[q];
+                bv[q] = ub ? vhi : bv[q];
+                bh[q] = ub ? h : bh[q];
+            }
+        }
+        // the month's maximisers, crossings and bounds per period
+        double ts[NQ], Ms[NQ];
+        int tot[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            dce_first_max(av[q], ah[q]);
+            dce_first_max(bv[q], bh[q]);
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) {
+                const double x = __shfl_xor(ml[q], o, WAVE);
+                ml[q] = x > ml[q] ? x : ml[q];
+            }
+            const bool here = q < nq && ((mask >> q) & 1u) && ah[q] != 0x7fffffff && bh[q] != 0x7fffffff;
+            double AL = 0.0, Ag = 0.0, BL = 0.0, Bg = 0.0;
+            if (here) {      // the maximisers' (L, g), formed as in pass 1 (the same bits)
+                AL = (double)shp[ah[q]] * ls; Ag = cf_per_kw_fast(cfp[ah[q]]);
+                BL = (double)shp[bh[q]] * ls; Bg = cf_per_kw_fast(cfp[bh[q]]);
+            }
+            double t_ = tlo;
+            if (Ag > Bg) {
+                t_ = (AL - BL) / (Ag - Bg);
+                t_ = t_ < tlo ? tlo : (t_ > thi ? thi : t_);
+            }
+            const double va = AL - Ag * t_, vb = BL - Bg * t_;
+            double M_ = va > vb ? va : vb;
+            M_ -= 1e-10 * (fabs(AL) + fabs(BL) + 1.0);               // the slack
+            ts[q] = t_;
+            Ms[q] = here ? M_ : INFINITY;                            // absent: keeps nothing
+            tot[q] = 2;
+            if (here && dl == q) {
+                E.lines[(m * DCP + q) * DC_NL] = make_double2(AL, Ag);
+                E.lines[(m * DCP + q) * DC_NL + 1] = make_double2(BL, Bg);
+            }
+        }
+        // pass 2: the other hours above the bound, written in hour order
+        uint32_t keep = 0;
+        int cnt[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) cnt[q] = 0;
+#pragma unroll
+        for (int hh = 0; hh < 24; hh++) {
+            const int p = (int)((pw[hh >> 2] >> (8 * (hh & 3))) & 0xffu);
+            const double L = (double)opaque_f(sh[hh]) * ls;   // recomputed, not kept from pass 1
+            const double gp = cf_per_kw_fast(opaque_i(cv[hh]));
+            const int h = d * 24 + hh;
+#pragma unroll
+            for (int q = 0; q < NQ; q++) {
+                const bool k = act & (p == q) & (h != ah[q]) & (h != bh[q]) & (L - gp * ts[q] > Ms[q]);
+                keep |= k ? 1u << hh : 0u;
+                cnt[q] += k ? 1 : 0;
+            }
+        }
+        int pos[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            int incl = cnt[q];
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                const int t = __shfl_up(incl, o, WAVE);
+                if (dl >= o) incl += t;
+            }
+            pos[q] = 2 + incl - cnt[q];
+            tot[q] = 2 + __shfl(incl, (lane & 32) + 31, WAVE);
+        }
+        if (keep) {
+#pragma unroll
+            for (int hh = 0; hh < 24; hh++) {
+                if ((keep >> hh) & 1u) {
+                    const int p = (int)((pw[hh >> 2] >> (8 * (hh & 3))) & 0xffu);
+                    const double L = (double)opaque_f(sh[hh]) * ls;   // recomputed, not kept from pass 1
+                    const double gp = cf_per_kw_fast(opaque_i(cv[hh]));
+#pragma unroll
+                    for (int q = 0; q < NQ; q++) {
+                        if (p == q) {
+                            if (pos[q] < DC_NL) E.lines[(m * DCP + q) * DC_NL + pos[q]] = make_double2(L, gp);
+                            pos[q]++;
+                        }
+                    }
+                }
+            }
+        }
+        // the month's counts and max loads (lane q of the half writes period q)
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const bool here = q < nq && ((mask >> q) & 1u) && Ms[q] != INFINITY;
+            if (here && tot[q] > DC_NL) ok = false;
+            if (dl == q) {
+                E.cnt[m * DCP + q] = here ? (tot[q] < DC_NL ? tot[q] : DC_NL) : 0;
+                E.maxl[m * DCP + q] = here ? ml[q] : 0.0;
+            }
+        }
+        if (dl >= NQ && dl < DCP) {            // periods past the batch's: absent
+            E.cnt[m * DCP + dl] = 0;
+            E.maxl[m * DCP + dl] = 0.0;
+        }
+    }
+    const bool bad = __ballot(!ok) != 0ull;
+    if (lane == 0) *E.tag = bad ? -(t0 + 1) : t0 + 1;
 }
 
 // The PV-only search's net-billing split of every agent's first-evaluation
@@ -3873,7 +4140,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     double w = wb * r_y;
     double wo = wo1 * r_y;
     double ev = (wo - w) + vor;                                    // ff:275
-    YFlow f = yl_cashflow(L, total, ev, y, g, active);
+    YFlow f = yl_cashflow(L, total, ev, y, g, active, S);
     const int64_t row = i * (MAXY + 1);
     if (g.sl == 0) {
         O.cfev_batt[row] = 0.0;
@@ -4448,6 +4715,7 @@ struct dgen_ctx {
     int hb_split;      // parts of a chunk's hourly scan, each on its own stream (1..4; DGEN_HB_SPLIT)
     int hb_nem;        // 1: batches without scratch slots run the bins-only scan (DGEN_HB_NEM=0: off)
     int ts_scan;       // 1: the TS sell-rate agents' split built in their own scan (DGEN_TS_SCAN=0: off, A/B)
+    int dc_pre;        // 1: the first-evaluation tariff's demand envelopes prebuilt by k_dc_env (DGEN_DC_PREBUILD=0: off)
     int64_t ts_lo, ts_hi;   // the batch rows holding every TS-capable agent (dgen_set_ts_rows)
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
@@ -4551,6 +4819,8 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
         c->hb_nem = (w && w[0] == '0') ? 0 : 1;
         const char* x = getenv("DGEN_TS_SCAN");
         c->ts_scan = (x && x[0] == '0') ? 0 : 1;
+        const char* y = getenv("DGEN_DC_PREBUILD");
+        c->dc_pre = (y && y[0] == '0') ? 0 : 1;
     }
     c->ts_lo = 0;
     c->ts_hi = INT64_MAX;
@@ -4795,6 +5065,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                           (dc ? (size_t)(WAVE / lpa_f) * DEM_STAGE_BYTES : 0);
     hipStream_t s2 = c->s2;
     char* const nbws = n_scratch > 0 ? ws_nb(ws, n, n_scratch) : nullptr;
+    // demand envelopes of the first-evaluation tariffs prebuilt (k_dc_env)
+    const int dc_pre = (dc && c->dc_buf && c->dc_pre) ? 1 : 0;
+    c->last_paths[6] = dc_pre;
     HIP_TRY(hipEventRecord(c->fork, s));
     HIP_TRY(hipStreamWaitEvent(s2, c->fork, 0));
     for (int j = 0; j < nch; j++) {
@@ -4806,6 +5079,15 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         if (n_scratch > 0)
             hipLaunchKernelGGL((k_nb_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE), 4 * WAVE * sizeof(double), s,
                                *T, *A, i0, i1, nbws);
+        if (dc_pre) {
+            const dim3 eg((unsigned)((m + DCE_WPB - 1) / DCE_WPB));
+            if (dc_nq <= 2)
+                hipLaunchKernelGGL((k_dc_env<2>), eg, dim3(WAVE * DCE_WPB), 0, s, *T, *A, c->cfg, i0, i1, c->dc_buf);
+            else if (dc_nq <= 4)
+                hipLaunchKernelGGL((k_dc_env<4>), eg, dim3(WAVE * DCE_WPB), 0, s, *T, *A, c->cfg, i0, i1, c->dc_buf);
+            else
+                hipLaunchKernelGGL((k_dc_env<DCP>), eg, dim3(WAVE * DCE_WPB), 0, s, *T, *A, c->cfg, i0, i1, c->dc_buf);
+        }
         // agents per year-lane block: WAVE / lpa
         const dim3 ygrid_s((unsigned)((m + WAVE / lpa_s - 1) / (WAVE / lpa_s)));
         const dim3 ygrid_f((unsigned)((m + WAVE / lpa_f - 1) / (WAVE / lpa_f)));
@@ -4816,34 +5098,34 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
 #if !DGEN_NO2_SIZE
             if (net)
                 hipLaunchKernelGGL((k_size_w<32, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
-                                   n, i0, i1, nullptr, nbws);
+                                   n, i0, i1, nullptr, nbws, 0);
             else
                 hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws);
+                                   c->cfg, n, i0, i1, nullptr, nbws, 0);
 #endif
         } else if (lpa_s == 32 && !pk) {
 #if !DGEN_NO2_SIZE_DC
             hipLaunchKernelGGL((k_size_w<32, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, dc_pre);
 #endif
         } else if (lpa_s == 32) {
 #if !DGEN_NO2_SIZE_PK
             hipLaunchKernelGGL((k_size_w<32, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, dc_pre);
 #endif
         } else if (!dc) {
             if (net)
                 hipLaunchKernelGGL((k_size_w<WAVE, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws);
+                                   c->cfg, n, i0, i1, nullptr, nbws, 0);
             else
                 hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws);
+                                   c->cfg, n, i0, i1, nullptr, nbws, 0);
         } else if (!pk) {
             hipLaunchKernelGGL((k_size_w<WAVE, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, dc_pre);
         } else {
             hipLaunchKernelGGL((k_size_w<WAVE, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, dc_pre);
         }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
@@ -5148,6 +5430,12 @@ int32_t dgen_set_pipeline(dgen_ctx* c, int32_t chunks) {
         return DGEN_E_ARG;
     }
     c->chunks = chunks;
+    return DGEN_OK;
+}
+
+int32_t dgen_set_dc_prebuild(dgen_ctx* c, int32_t on) {
+    if (!c || (on != 0 && on != 1)) { set_err("dgen_set_dc_prebuild: on must be 0 or 1"); return DGEN_E_ARG; }
+    c->dc_pre = on;
     return DGEN_OK;
 }
 

@@ -404,12 +404,18 @@ class Engine:
         c = _lib.DCR_CAP if cap is True else int(cap)
         _lib.check(self.lib.dgen_set_dc_records(self.ctx, c), "dgen_set_dc_records")
 
+    def set_dc_prebuild(self, on: bool = True):
+        """Demand envelopes of the first-evaluation tariffs prebuilt by their
+        own kernel (default) or built inside the search (dgen_set_dc_prebuild;
+        bit-identical results)."""
+        _lib.check(self.lib.dgen_set_dc_prebuild(self.ctx, 1 if on else 0), "dgen_set_dc_prebuild")
+
     def last_paths(self) -> Dict[str, int]:
         """The record forms the last size() call took (dgen_last_paths): what
         the kernels actually did, for the bench's byte accounting."""
-        a = (ctypes.c_int32 * 6)()
-        _lib.check(self.lib.dgen_last_paths(self.ctx, a, 6), "dgen_last_paths")
-        keys = ("nb_scan", "dcr_on", "ts_split", "dc", "max_periods", "dc_periods")
+        a = (ctypes.c_int32 * 7)()
+        _lib.check(self.lib.dgen_last_paths(self.ctx, a, 7), "dgen_last_paths")
+        keys = ("nb_scan", "dcr_on", "ts_split", "dc", "max_periods", "dc_periods", "dc_prebuild")
         return dict(zip(keys, (int(v) for v in a)))
 
     def kernel_times(self):

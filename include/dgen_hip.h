@@ -540,11 +540,22 @@ int32_t dgen_kernel_times(dgen_ctx* ctx, double* ms_size, double* ms_hourly, dou
  * sell-rate agents' own split scan, out[3] the demand machinery on (demand
  * charges billed or kWh/kW tier peaks), out[4] the period count the kernels'
  * LDS is laid out for (the tables' max_periods after the call's adjustments),
- * out[5] the demand periods per record.  Writes min(n_out, DGEN_PATHS_N)
- * values; returns DGEN_PATHS_N.  For byte accounting (bench.py); replaces
- * nothing in the reference.                                                 */
-#define DGEN_PATHS_N 6
+ * out[5] the demand periods per record, out[6] the demand envelopes of the
+ * first-evaluation tariffs prebuilt by their own kernel (k_dc_env).  Writes
+ * min(n_out, DGEN_PATHS_N) values; returns DGEN_PATHS_N.  For byte
+ * accounting (bench.py); replaces nothing in the reference.                 */
+#define DGEN_PATHS_N 7
 int32_t dgen_last_paths(dgen_ctx* ctx, int32_t* out, int32_t n_out);
+
+/* Demand envelopes (the PV-only search's per-(month, demand period) import
+ * lines, demand-charge and kWh/kW-tier batches) of every agent's
+ * first-evaluation tariff prebuilt by their own kernel ahead of the search
+ * (1, default; k_dc_env: day lanes, coalesced 16-B profile loads) or built by
+ * the search kernel at the first evaluation that bills the tariff (0; the
+ * DGEN_DC_PREBUILD=0 environment setting at dgen_open does the same).  The
+ * kept lines are the same set either way and an evaluation takes their max,
+ * so results are bit-identical (ABI 11).  Replaces nothing in the reference. */
+int32_t dgen_set_dc_prebuild(dgen_ctx* ctx, int32_t on);
 
 /* Pipeline depth of dgen_size_agents: the batch is cut into `chunks` pieces;
  * k_size of piece j+1 runs on the caller's stream while k_hourly_batt and

@@ -168,6 +168,9 @@ def lib():
         L.orc_size_batch.argtypes = [ctypes.POINTER(Agent), ctypes.c_int64, ctypes.POINTER(Tariff),
                                      ctypes.c_int, ctypes.POINTER(Cfg), ctypes.POINTER(Result),
                                      ctypes.c_int]
+        L.orc_set_trace.restype = None
+        L.orc_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_trace_count.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -322,3 +325,17 @@ def result_to_dict(r: Result, n_years: int, hourly=None) -> dict:
     if hourly is not None:
         d["baseline_net_hourly"], d["adopter_net_hourly_pvonly"], d["adopter_net_hourly_with_batt"] = hourly
     return d
+
+
+def brent_trace(opop, cfg: Cfg, i: int, maxn: int = 600):
+    """Diagnostics: size agent i of `opop` (an OraclePopulation) and return the
+    (x, f) pairs of its bounded-Brent evaluations, in order."""
+    buf = np.zeros(2 * maxn)
+    L = lib()
+    L.orc_set_trace(buf.ctypes.data, maxn)
+    try:
+        res = opop.run(cfg, idx=[i])
+        n = min(L.orc_trace_count(), maxn)
+    finally:
+        L.orc_set_trace(None, 0)
+    return buf[:2 * n].reshape(n, 2), res

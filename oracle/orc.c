@@ -368,6 +368,10 @@ static double depr_frac(int type, int year, int sl_years) {
 /* cmod_cashloan as driven at ff:272-288,385-421: after-tax cash flows, NPV at
  * the nominal discount rate (Horner form of SSC libfin::npv), payback from the
  * cumulative cf_payback_with_expenses (SSC compute_payback, 1e99 if none). */
+/* NPV association (diagnostics only): 0 = SSC's libfin::npv order (default) */
+int orc_npv_order = 0;
+void orc_set_npv_order(int k) { orc_npv_order = k; }
+
 int orc_cashloan(const orc_loan_in* in, const orc_cfg* cfg, const double* aev, double* npv,
                  double* payback, double* cf_payback, double* cf_energy_value) {
     int N = in->nyears;
@@ -423,8 +427,26 @@ int orc_cashloan(const orc_loan_in* in, const orc_cfg* cfg, const double* aev, d
     }
     double rr = 1.0 / (1.0 + nom);
     double acc = 0.0;
-    for (int i = N; i > 0; i--) acc = rr * acc + atcf[i];
-    *npv = atcf[0] + acc * rr;
+    if (orc_npv_order == 1) {
+        /* diagnostics only: the association of a 32/64-lane xor butterfly
+         * over atcf_y rr^y (the device's round-4 form) */
+        int W = N <= 32 ? 32 : 64;
+        double v[64];
+        for (int k = 0; k < W; k++) {
+            double df = 1.0;
+            for (int j = 0; j <= k; j++) df *= rr;
+            v[k] = (k < N) ? atcf[k + 1] * df : 0.0;
+        }
+        for (int o = W / 2; o > 0; o >>= 1) {
+            double t[64];
+            for (int k = 0; k < W; k++) t[k] = v[k] + v[k ^ o];
+            for (int k = 0; k < W; k++) v[k] = t[k];
+        }
+        *npv = -(C - debt) + v[0];
+    } else {
+        for (int i = N; i > 0; i--) acc = rr * acc + atcf[i];
+        *npv = atcf[0] + acc * rr;
+    }
 
     double cum = cf_payback[0];
     double pb = 1e99;
@@ -673,6 +695,22 @@ typedef double (*orc_obj_fn)(double x, void* ctx);
 
 static double np_sign(double v) { return (v > 0.0) ? 1.0 : ((v < 0.0) ? -1.0 : 0.0); }
 
+/* Optional evaluation trace (diagnostics only, this thread): (x, f) pairs of
+ * every bounded-Brent evaluation, set with orc_set_trace(buf, max). */
+static __thread double* orc_trace_buf = 0;
+static __thread int orc_trace_max = 0, orc_trace_n = 0;
+void orc_set_trace(double* buf, int max) { orc_trace_buf = buf; orc_trace_max = max; orc_trace_n = 0; }
+int orc_trace_count(void) { return orc_trace_n; }
+static double traced(orc_obj_fn f, void* ctx, double x) {
+    double v = f(x, ctx);
+    if (orc_trace_buf && orc_trace_n < orc_trace_max) {
+        orc_trace_buf[2 * orc_trace_n] = x;
+        orc_trace_buf[2 * orc_trace_n + 1] = v;
+    }
+    if (orc_trace_buf) orc_trace_n++;
+    return v;
+}
+
 static double brent_bounded(orc_obj_fn f, void* ctx, double x1, double x2, double xatol,
                             int maxfun, int* nfev) {
     const double sqrt_eps = sqrt(2.2e-16);
@@ -682,7 +720,7 @@ static double brent_bounded(orc_obj_fn f, void* ctx, double x1, double x2, doubl
     double nfc = fulc, xf = fulc;
     double rat = 0.0, e = 0.0;
     double x = xf;
-    double fx = f(x, ctx);
+    double fx = traced(f, ctx, x);
     int num = 1;
     double ffulc = fx, fnfc = fx;
     double xm = 0.5 * (a + b);
@@ -718,7 +756,7 @@ static double brent_bounded(orc_obj_fn f, void* ctx, double x1, double x2, doubl
         double si = np_sign(rat) + ((rat == 0.0) ? 1.0 : 0.0);
         double ar = fabs(rat);
         x = xf + si * (ar > tol1 ? ar : tol1);   /* np.maximum(|rat|, tol1) */
-        double fu = f(x, ctx);
+        double fu = traced(f, ctx, x);
         num += 1;
         if (fu <= fx) {
             if (x >= xf) a = xf; else b = xf;

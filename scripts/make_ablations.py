@@ -248,6 +248,28 @@ VARIANTS = {
                     "            nb_ok = true; wb = 1000.0 * s_y + (double)(size_t)nbp * 0.0;")],
 }
 
+# Brent evaluation trace of one agent in k_size (diagnostics, results
+# unchanged): per evaluation (kW, -NPV, net-billing split used, envelope used
+# | staged << 1); dgen_bt_set(agent) / dgen_bt_read(out[256]) -> count
+BTRACE = [("template <int LPA, bool DC, bool NET, bool PK>\n__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))\nk_size_w(",
+           "__device__ long long g_bt_agent = -1;\n__device__ int g_bt_n = 0;\n__device__ double g_bt[256];\n"
+           "template <int LPA, bool DC, bool NET, bool PK>\n__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))\nk_size_w("),
+          ("            return yl_objective<LPA, DC, NET, PK>(c, x);\n",
+           "            const double v_ = yl_objective<LPA, DC, NET, PK>(c, x);\n"
+           "            if (i == g_bt_agent && sl == 0) { const int k_ = g_bt_n; if (k_ < 64) { g_bt[4 * k_] = x; g_bt[4 * k_ + 1] = v_;"
+           " g_bt[4 * k_ + 2] = c.nb_ok ? 1.0 : 0.0; g_bt[4 * k_ + 3] = (c.env_ok ? 1.0 : 0.0) + (c.stg_ok ? 2.0 : 0.0); } g_bt_n = k_ + 1; }\n"
+           "            return v_;\n"),
+          ("int32_t dgen_last_paths(dgen_ctx* c, int32_t* out, int32_t n_out) {",
+           "extern \"C\" int32_t dgen_bt_set(long long agent) {\n    int z = 0;\n"
+           "    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bt_agent), &agent, sizeof(agent)) != hipSuccess) return -1;\n"
+           "    return hipMemcpyToSymbol(HIP_SYMBOL(g_bt_n), &z, sizeof(z)) == hipSuccess ? 0 : -1;\n}\n"
+           "extern \"C\" int32_t dgen_bt_read(double* out) {\n    int n = 0;\n"
+           "    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_bt_n), sizeof(n)) != hipSuccess) return -1;\n"
+           "    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bt), sizeof(double) * 256) != hipSuccess) return -1;\n"
+           "    return n;\n}\n"
+           "int32_t dgen_last_paths(dgen_ctx* c, int32_t* out, int32_t n_out) {")]
+VARIANTS["btrace"] = BTRACE
+
 # in-kernel clock of k_hourly_batt (MI355X_MICROARCH.md DVFS item 6): thread 0 of
 # each block stamps s_memtime / s_memrealtime at its start and after its month
 # loop into a buffer of its own; bench.py prints the median clock (run with

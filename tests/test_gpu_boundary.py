@@ -226,7 +226,7 @@ def test_sub_batched_frame_equals_one_call():
     assert "sub_batches" not in tm1 and tm4["sub_batches"] == 4
     assert list(sub.index) == list(df.index) and list(sub.columns) == list(one.columns)
     for k in SCALARS + ["payback_period", "tariff_id", "nem_system_kw_limit"]:
-        assert np.array_equal(one[k].to_numpy(), sub[k].to_numpy()), k
+        assert one[k].equals(sub[k]), k              # NaN == NaN (no switch: the limit stays NaN)
     for k in ARRAYS:
         assert np.array_equal(one[k].array.to_2d(), sub[k].array.to_2d()), k
     for k in ("baseline_net_hourly", "adopter_net_hourly_pvonly", "adopter_net_hourly_with_batt"):

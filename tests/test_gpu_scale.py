@@ -120,10 +120,12 @@ def test_national_200k_sample_vs_oracle(engine):
 
 def test_c4_commercial_dc_1m_sample_vs_oracle(engine_dc):
     """C4 per GPU (8M commercial agents over 8 GPUs): demand charges billed
-    (extension mode), battery run.  Demand charges make the objective
-    piecewise linear in kW, and the device's re-associated sums may flip a
-    Brent comparison at a kink; a flipped agent's kW
-    must still be within scipy's xatol, and flips must be rare."""
+    (extension mode), battery run, 1000 sampled agents against the oracle --
+    every agent on the oracle's Brent path (nfev, system kW to 1e-9), so NPV,
+    payback, bills and planes are compared for each.  A path diverges only if
+    the objective differs by a few ulps somewhere and scipy's parabolic step
+    amplifies it; the device computes NPV and the payback
+    sums in the oracle's (SSC's) order so that does not happen."""
     eng = engine_dc
     n = 1_000_000
     pop = make_population("com_dc_batt", n, seed=20260000 + 4 + 101)
@@ -136,26 +138,16 @@ def test_c4_commercial_dc_1m_sample_vs_oracle(engine_dc):
     torch.cuda.synchronize()
     st = out["status"].cpu().numpy()
     assert (st == 0).all(), np.unique(st)
-    idx = np.sort(np.random.default_rng(13).choice(n, SAMPLE, replace=False))
+    k = 1000
+    idx = np.sort(np.random.default_rng(13).choice(n, k, replace=False))
     from dgen_amd.synth import subset
     sample = _device_sample(out, idx)
     del out, batch                       # the 1M-agent planes (105 GB) before the next test
     torch.cuda.empty_cache()
-    flips = _check_sample(subset(pop, idx), sample, np.arange(SAMPLE), orc.make_cfg(),
+    flips = _check_sample(subset(pop, idx), sample, np.arange(k), orc.make_cfg(),
                           demand=pop.demand, tag="C4")
-    print(f"\nC4 1M sample: demand-charge Brent path flips {len(flips)} of {SAMPLE} (allowed <= 2): {flips}",
-          flush=True)
-    assert len(flips) <= 2, flips
-    if flips:                            # positions in the sample
-        opop = helpers.oracle_population({k: v[idx] for k, v in pop.cols.items()}, pop.tariffs, pop.switches,
-                                         pop.shapes, pop.cfs, pop.wholesale, demand=pop.demand)
-        ref = opop.run(orc.make_cfg())
-        kw = sample["system_kw"].cpu().numpy()
-        for j in flips:
-            a = idx[j]
-            L = pop.cols["load_kwh"][a] / (pop.cfs[pop.cols["cf_row"][a]].sum() / 1e6)
-            xatol = max(2.0, np.floor(max(0.45 * L, 1.0) * 1e-3))
-            assert abs(kw[j] - ref[j]["system_kw"]) <= xatol, (a, kw[j], ref[j]["system_kw"], xatol)
+    print(f"\nC4 1M sample: Brent path divergences {len(flips)} of {k}: {flips}", flush=True)
+    assert not flips, flips
 
 
 def test_c5_loop_2p5m_sample_vs_oracle(engine):
