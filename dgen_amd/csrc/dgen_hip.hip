@@ -3912,20 +3912,20 @@ k_dc_env(dgen_tables T, dgen_agents A, dgen_cfg cfg, int64_t i0, int64_t i1, voi
             pos[q] = 2 + incl - cnt[q];
             tot[q] = 2 + __shfl(incl, (lane & 32) + 31, WAVE);
         }
-        if (keep) {
+        // the kept hours (a few per month and period), one at a time from the
+        // lane's bit mask; their values re-read from the (cache-hot) rows
+        while (keep) {
+            const int hh = __builtin_ctz(keep);
+            keep &= keep - 1u;
+            const int h = d * 24 + hh;
+            const int p = (int)sc[hh];
+            const double L = (double)shp[h] * ls;
+            const double gp = cf_per_kw_fast(cfp[h]);
 #pragma unroll
-            for (int hh = 0; hh < 24; hh++) {
-                if ((keep >> hh) & 1u) {
-                    const int p = (int)((pw[hh >> 2] >> (8 * (hh & 3))) & 0xffu);
-                    const double L = (double)opaque_f(sh[hh]) * ls;   // recomputed, not kept from pass 1
-                    const double gp = cf_per_kw_fast(opaque_i(cv[hh]));
-#pragma unroll
-                    for (int q = 0; q < NQ; q++) {
-                        if (p == q) {
-                            if (pos[q] < DC_NL) E.lines[(m * DCP + q) * DC_NL + pos[q]] = make_double2(L, gp);
-                            pos[q]++;
-                        }
-                    }
+            for (int q = 0; q < NQ; q++) {
+                if (p == q) {
+                    if (pos[q] < DC_NL) E.lines[(m * DCP + q) * DC_NL + pos[q]] = make_double2(L, gp);
+                    pos[q]++;
                 }
             }
         }

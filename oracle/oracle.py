@@ -168,6 +168,10 @@ def lib():
         L.orc_size_batch.argtypes = [ctypes.POINTER(Agent), ctypes.c_int64, ctypes.POINTER(Tariff),
                                      ctypes.c_int, ctypes.POINTER(Cfg), ctypes.POINTER(Result),
                                      ctypes.c_int]
+        L.orc_eval_at.restype = ctypes.c_int
+        L.orc_eval_at.argtypes = [ctypes.POINTER(Agent), ctypes.POINTER(Tariff), ctypes.c_int,
+                                  ctypes.POINTER(Cfg), _c_double, _c_double, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(Result)]
         L.orc_set_trace.restype = None
         L.orc_set_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.orc_trace_count.restype = ctypes.c_int
@@ -306,6 +310,23 @@ class Population:
                                  ctypes.byref(cfg), ctypes.byref(r))
             out.append(result_to_dict(r, int(self.agents[i].econ_life), bufs))
         return out
+
+    def eval_at(self, cfg: Cfg, i: int, kw_star: float, x_last: float, tariff: int, switched: int,
+                hourly: bool = False) -> dict:
+        """Agent i's driver outputs for a search that ended at (kw_star,
+        x_last) with the given sticky tariff state (orc_eval_at)."""
+        r = Result()
+        bufs = None
+        if hourly:
+            bufs = [np.zeros(NH), np.zeros(NH), np.zeros(NH)]
+            r.baseline = bufs[0].ctypes.data_as(_dp)
+            r.net_pvonly = bufs[1].ctypes.data_as(_dp)
+            r.net_with_batt = bufs[2].ctypes.data_as(_dp)
+        rc = lib().orc_eval_at(ctypes.byref(self.agents[i]), self.tariffs, self.n_tariffs, ctypes.byref(cfg),
+                               float(kw_star), float(x_last), int(tariff), int(switched), ctypes.byref(r))
+        if rc < -3:
+            raise ValueError(f"orc_eval_at failed: {rc}")
+        return result_to_dict(r, int(self.agents[i].econ_life), bufs)
 
     def run_batch_timed(self, cfg: Cfg, threads: int, idx: Sequence[int]):
         """Batch entry used for the CPU baseline (OpenMP over `threads`)."""

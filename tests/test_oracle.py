@@ -415,3 +415,25 @@ def test_month_floor_option(hourly):
     # on the low days the floored dispatch discharges less (it keeps energy)
     low = (day % 30) >= 10
     assert (b[0] - pv)[low].clip(min=0).sum() <= (a[0] - pv)[low].clip(min=0).sum() + 1e-9
+
+
+def test_eval_at_reproduces_the_search_end():
+    """orc_eval_at (the knife-edge check, helpers.at_device_point): the driver
+    evaluated where a search ended -- (kW, last x, sticky tariff) -- gives that
+    search's outputs bit for bit; and the Brent trace lists the search's
+    evaluations, ending at its last x."""
+    from dgen_amd.synth import make_population
+    pop = make_population("national_mixed", 40, n_res_shapes=16, n_com_shapes=16, n_cf=16, n_counties=8,
+                          n_tariffs=24)
+    opop = helpers.oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs, pop.wholesale)
+    cfg = orc.make_cfg()
+    ref = opop.run(cfg, hourly=True)
+    for i, r in enumerate(ref):
+        e = opop.eval_at(cfg, i, r["system_kw"], r["x_last"], r["tariff_final"], r["switched"], hourly=True)
+        for k in ("npv", "payback_raw", "npv_pv_batt", "first_with", "first_without", "batt_kwh",
+                  "annual_kwh", "system_kw", "tariff_final"):
+            assert e[k] == r[k], (i, k)
+        for k in ("cash_flow", "bill_w_pv_only", "bill_w_pv_batt", "adopter_net_hourly_with_batt"):
+            assert np.array_equal(e[k], r[k]), (i, k)
+        tr, res = orc.brent_trace(opop, cfg, i)
+        assert tr.shape[0] == r["nfev"] and tr[-1, 0] == r["x_last"] and res[0]["npv"] == r["npv"]
