@@ -2949,6 +2949,145 @@ __device__ __forceinline__ bool yl_nb_build(const dgen_tariff& t, const YSrc& sr
     return ok;
 }
 
+// k_nb_env's form of yl_nb_build<false>: the same hour-lane classification,
+// sums and entry order (so the same split, bit for bit), but the rows come
+// through an LDS stage of NBS_DAYS days per agent, filled by coalesced 16-B
+// loads (segment lane k < 16: day k's 96 B of shape and of cf; lane 16 + k:
+// day k's 24 float32 sell weights from the 192 B of its TS row) instead of
+// one 4-B load per hour lane and day (C2 200k: k_nb_env was 7.5 ms of the
+// 18.6 ms search, waiting on those loads).  Two agents per wave (LPA 32),
+// each segment staging its own agent.
+constexpr int NBS_DAYS = 16;
+struct NbStage {                 // one segment's (agent's) days
+    float sh[NBS_DAYS * 24];
+    int32_t cf[NBS_DAYS * 24];
+    float w[NBS_DAYS * 24];
+};
+constexpr size_t NBS_BYTES = sizeof(NbStage);
+static_assert(NBS_BYTES % 16 == 0, "stage keeps 16-B alignment");
+
+template <int LPA>
+__device__ __forceinline__ bool yl_nb_build_stg(const dgen_tariff& t, const YSrc& src, double tlo, double thi,
+                                                char* nbp, const YLds& S, const Seg<LPA>& g, NbStage* st) {
+    static_assert(LPA == 32, "k_nb_env runs two agents per wave");
+    const NbRec R = nb_rec(nbp);
+    const int P = t.P;
+    const int hd = g.sl;
+    const bool act = hd < 24;
+    const int hq = act ? hd : 0;
+    const unsigned long long segm = ((1ull << LPA) - 1ull) << g.base;
+    const unsigned long long below = (1ull << g.lane) - 1ull;
+    double* col0 = S.lane - g.sl;          // the segment's first lane's LDS column
+    bool ok = true;
+    for (int m = 0; m < 12; m++) {
+        const int pd = act ? (int)t.wkday[m][hd] : 0, pe = act ? (int)t.wkend[m][hd] : 0;
+        double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0};
+        int n_m = 0;
+        NbEnt* ent = R.ent + m * NB_CAPM;
+        const int ds = c_month_start_day[m], de = c_month_start_day[m + 1];
+#pragma unroll 1
+        for (int d0 = ds; d0 < de; d0 += NBS_DAYS) {
+            const int nd = de - d0 < NBS_DAYS ? de - d0 : NBS_DAYS;
+            wave_lds_sync();                              // the previous batch's reads
+            {
+                const int k = g.sl & (NBS_DAYS - 1);
+                const int d = d0 + (k < nd ? k : nd - 1);
+                if (g.sl < NBS_DAYS) {
+                    const float4* s4 = reinterpret_cast<const float4*>(src.shape + d * 24);
+                    const int4* c4 = reinterpret_cast<const int4*>(src.cf + d * 24);
+                    float4 sv[6];
+                    int4 cv[6];
+#pragma unroll
+                    for (int q = 0; q < 6; q++) { sv[q] = s4[q]; cv[q] = c4[q]; }
+#pragma unroll
+                    for (int q = 0; q < 6; q++) {
+                        reinterpret_cast<float4*>(st->sh + k * 24)[q] = sv[q];
+                        reinterpret_cast<int4*>(st->cf + k * 24)[q] = cv[q];
+                    }
+                } else if (src.ts) {
+                    const double2* t2 = reinterpret_cast<const double2*>(src.ts + d * 24);
+                    double2 tv[12];
+#pragma unroll
+                    for (int q = 0; q < 12; q++) tv[q] = t2[q];
+#pragma unroll
+                    for (int q = 0; q < 6; q++)
+                        reinterpret_cast<float4*>(st->w + k * 24)[q] =
+                            make_float4((float)(tv[2 * q].x * src.ts_mult), (float)(tv[2 * q].y * src.ts_mult),
+                                        (float)(tv[2 * q + 1].x * src.ts_mult), (float)(tv[2 * q + 1].y * src.ts_mult));
+                }
+            }
+            wave_lds_sync();
+#pragma unroll 4
+            for (int k = 0; k < nd; k++) {
+                const int d = d0 + k;
+                const bool we = (d % 7) >= 5;
+                const double L = (double)st->sh[k * 24 + hq] * src.load_scale;
+                const double gk = cf_per_kw(st->cf[k * 24 + hq]);
+                const float w = src.ts ? st->w[k * 24 + hq] : 1.0f;
+                const double vlo = L - gk * tlo, vhi = L - gk * thi;
+                const double slack = 1e-10 * (fabs(L) + fabs(gk) * thi);
+                const bool imp = act && fmin(vlo, vhi) > slack;              // imports at every t
+                const bool exq = act && !imp && fmax(vlo, vhi) < -slack;     // exports at every t
+                const double wd = (double)w;
+                const double i0 = imp ? L : 0.0, i1 = imp ? gk : 0.0;
+                const double x0 = exq ? gk * wd : 0.0, x1 = exq ? L * wd : 0.0;
+                if (we) {
+                    a1[0] += i0; a1[1] += i1; a1[2] += x0; a1[3] += x1;
+                } else {
+                    a0[0] += i0; a0[1] += i1; a0[2] += x0; a0[3] += x1;
+                }
+                const bool mx = act && !imp && !exq;
+                const unsigned long long bm = __ballot(mx) & segm;
+                if (mx) {
+                    const int pos = n_m + __popcll(bm & below);
+                    if (pos < NB_CAPM) {
+                        NbEnt e;
+                        e.L = L;
+                        e.g = gk;
+                        e.w = w;
+                        e.p = we ? pe : pd;
+                        ent[pos] = e;
+                    }
+                }
+                n_m += __popcll(bm);
+            }
+        }
+        ok = ok && n_m <= NB_CAPM;
+        if (g.sl == 0) R.cnt[m] = n_m;
+        // (hour, day type) partials -> (period, quantity) sums, as yl_nb_build
+        constexpr int NR = (4 * MAXP + LPA - 1) / LPA;
+        double v[NR];
+#pragma unroll
+        for (int k = 0; k < NR; k++) v[k] = 0.0;
+        for (int dt = 0; dt < 2; dt++) {
+            wave_lds_sync();
+#pragma unroll
+            for (int q = 0; q < 4; q++) S.at(q) = dt ? a1[q] : a0[q];
+            wave_lds_sync();
+            const uint8_t* sc = dt ? t.wkend[m] : t.wkday[m];
+#pragma unroll
+            for (int k = 0; k < NR; k++) {
+                const int r = g.sl + k * LPA;
+                if (r < 4 * P) {
+                    const int p = r >> 2, q = r & 3;
+                    for (int hh = 0; hh < 24; hh++)
+                        if ((int)sc[hh] == p) v[k] += col0[q * WAVE + hh];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NR; k++) {
+            const int r = g.sl + k * LPA;
+            if (r < 4 * P) R.sums[(m * MAXP + (r >> 2)) * 4 + (r & 3)] = v[k];
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    wave_lds_sync();
+    return ok;
+}
+
 // Net-billing bill of the lane's year from the split (generation kW' =
 // src.gen_scale, degradation factor s; battery case: src.sysgen with
 // gen_scale 1): yl_bill_mo2's result up to the rounding of the re-associated
@@ -3995,7 +4134,8 @@ k_nb_env(dgen_tables T, dgen_agents A, int64_t i0, int64_t i1, char* nbws) {
             S.L = S.G = S.pk = nullptr;
             S.half = 0;
             S.lane = dyn_lds + lane;
-            if (yl_nb_build<false>(t, src, tlo, thi, nbp, S, g)) tag = t0 + 1;
+            NbStage* const stg = reinterpret_cast<NbStage*>(dyn_lds + 4 * WAVE) + lane / LPA;
+            if (yl_nb_build_stg<LPA>(t, src, tlo, thi, nbp, S, g, stg)) tag = t0 + 1;
         }
     }
     if (g.sl == 0) nbr_tag(nbp) = tag;
@@ -5077,7 +5217,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         // net-billing splits and demand envelopes of the initial tariffs
         // (counted in k_size's time)
         if (n_scratch > 0)
-            hipLaunchKernelGGL((k_nb_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE), 4 * WAVE * sizeof(double), s,
+            hipLaunchKernelGGL((k_nb_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE),
+                               4 * WAVE * sizeof(double) + 2 * NBS_BYTES, s,
                                *T, *A, i0, i1, nbws);
         if (dc_pre) {
             const dim3 eg((unsigned)((m + DCE_WPB - 1) / DCE_WPB));
