@@ -222,16 +222,47 @@ def cpu_baseline(pop, seconds: float, threads: int, replan_hours: int = 24):
             el = time.perf_counter() - t0
             if el >= secs:
                 return done, el
+    quota = cgroup_cpus()
     done, el = window(threads, seconds)
-    res = {"value": done / el, "unit": "agents/s", "cores": threads, "kind": "port",
-           "host_cpus": os.cpu_count(), "affinity_cpus": avail, "omp_num_threads_env": omp or None,
-           "sample": f"{done} agent sizings over the first {n_take} agents of the same synthetic workload "
-                     f"({pop.config}), oracle/orc.c full per-agent driver, OpenMP x{threads}, {el:.1f} s"}
-    if share != threads:
-        d2, e2 = window(share, max(5.0, seconds / 3))
-        res["omp_share"] = {"value": d2 / e2, "cores": share,
-                            "sample": f"{d2} agent sizings, OpenMP x{share} (OMP_NUM_THREADS), {e2:.1f} s"}
+    runs = {threads: (done, el)}
+    # the box's CPU allotment (cgroup quota / OMP_NUM_THREADS) can be far below
+    # its affinity set: time that thread count too and report the faster one
+    alt = min(x for x in (share, quota or share) if x)
+    if alt != threads:
+        runs[alt] = window(alt, max(5.0, seconds / 3))
+    best = max(runs, key=lambda k: runs[k][0] / runs[k][1])
+    d, e = runs[best]
+    res = {"value": d / e, "unit": "agents/s", "cores": best, "kind": "port",
+           "host_cpus": os.cpu_count(), "affinity_cpus": avail, "cgroup_cpu_quota": quota,
+           "omp_num_threads_env": omp or None,
+           "by_threads": {str(k): {"agents_per_s": v[0] / v[1], "agents": v[0], "seconds": round(v[1], 2)}
+                          for k, v in runs.items()},
+           "sample": f"{d} agent sizings over the first {n_take} agents of the same synthetic workload "
+                     f"({pop.config}), oracle/orc.c full per-agent driver, OpenMP x{best} (the faster of "
+                     f"{sorted(runs)} threads: all {avail} affinity CPUs and the box's CPU allotment), {e:.1f} s"}
     return res
+
+
+def cgroup_cpus():
+    """CPUs the cgroup quota allows (cpu.max quota / period), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                return max(1, int(round(int(q) / int(per))))
+        except Exception:
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return max(1, int(round(q / per)))
+    except Exception:
+        pass
+    return None
 
 
 def timed_region(step, steps: int, sync, dist_mod=None, device=None) -> float:
