@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--hourly-chunk", type=int, default=None,
                     help="re-size chunks of this many agents for the state export")
     ap.add_argument("--no-export", action="store_true", help="skip the per-state hourly export")
+    ap.add_argument("--export", default="auto", choices=["auto", "with_batt", "planes", "chunked"],
+                    help="how the per-state rows are made (YearLoop export; auto: the with-battery plane alone "
+                         "where it fits, else --hourly-chunk's re-run scans)")
     ap.add_argument("--cut-tol", type=float, default=0.02,
                     help="plan_partition tol: a rank cut snaps to a state boundary within this share of "
                          "the per-rank cost (0: cut inside states wherever balance puts the cut)")
@@ -105,7 +108,8 @@ def main():
     eng.set_tariffs(pop.tariffs)
     eng.set_switches(pop.switches)
     loop = YearLoop(eng, pop, ag, LoopTables.synthetic(), first_year=args.first_year,
-                    hourly_export=not args.no_export, hourly_chunk=args.hourly_chunk, plan=plan, split=sg)
+                    hourly_export=not args.no_export, hourly_chunk=args.hourly_chunk, plan=plan, split=sg,
+                    export=args.export)
     del pop
     setup_s = time.perf_counter() - t_setup
     for k in range(args.warmup):
@@ -166,6 +170,7 @@ def main():
                                     "measured_max_over_mean": (max(r_[0] for r_ in per_rank) /
                                                                (sum(r_[0] for r_ in per_rank) / len(per_rank)))},
                        "state_export": not args.no_export, "hourly_chunk": args.hourly_chunk,
+                       "export_mode": loop.export_mode,
                        "parallelism": f"dp{ws} (state pieces per rank; split groups gathered, one all-reduce of state rows per year)"},
             "sizing_kernel_ms_per_call": {"k_size": ms_size, "k_hourly_batt": ms_hourly,
                                           "k_batt_finance": ms_fin, "launch_samples": cnt},

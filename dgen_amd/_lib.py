@@ -114,7 +114,7 @@ EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
     "dgen_kernel_times", "dgen_last_paths", "dgen_set_dc_prebuild", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
-    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_set_ts_rows", "dgen_set_dc_records", "dgen_hourly_planes", "dgen_export_plane", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
+    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_set_ts_rows", "dgen_set_dc_records", "dgen_hourly_planes", "dgen_export_plane", "dgen_state_hourly_rows", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
     "dgen_finance_series", "dgen_year_inputs", "dgen_initial_market_shares", "dgen_rows_seq_sum",
 ]
 
@@ -180,6 +180,9 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.dgen_export_plane.restype = _i32
     L.dgen_export_plane.argtypes = [_vp, ctypes.POINTER(Tables), ctypes.POINTER(Agents), ctypes.POINTER(Outputs),
                                     _vp, _vp, _vp, _vp, _i64, _vp, ctypes.c_size_t, _i64, _vp]
+    L.dgen_state_hourly_rows.restype = _i32
+    L.dgen_state_hourly_rows.argtypes = [_vp, ctypes.POINTER(Tables), ctypes.POINTER(Agents), ctypes.POINTER(Outputs),
+                                         _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp]
     L.dgen_segment_sums.restype = _i32
     L.dgen_segment_sums.argtypes = [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i64, _vp, _i64, _vp, _vp]
     L.dgen_rows_seq_sum.restype = _i32

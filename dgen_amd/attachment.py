@@ -262,6 +262,51 @@ def state_hourly_combined(engine, plane, idx, seg_off):
     return out
 
 
+def state_hourly_rows(engine, batch, c_out, with_batt, weights, idx, seg_off):
+    """The per-state rows of a batch sized with the with-battery plane alone
+    (Engine.alloc_outputs(..., hourly="with_batt"), float32 hour-quad tiles):
+    dgen_state_hourly_rows recomputes each agent-hour's load and PV-only net
+    load from the profile rows as the scan forms them, so the rows are
+    state_hourly's over the three planes, bit for bit.  idx / seg_off as in
+    state_hourly; returns a [S, 8760] float64 device tensor in MW."""
+    import torch
+    eng = _engine(engine)
+    if with_batt.dtype != torch.float32 or with_batt.dim() != 3 or with_batt.shape[2] != 4:
+        raise ValueError("state_hourly_rows: the with-battery plane is float32 hour-quad tiles [8760/4, n, 4]")
+    nh, n = with_batt.shape[0] * 4, with_batt.shape[1]
+    if nh != NH_FULL or n != batch.n:
+        raise ValueError("state_hourly_rows: one 8760-h plane column per batch agent")
+    w = [x.contiguous() for x in weights]
+    if any(x.numel() != n for x in w):
+        raise ValueError("state_hourly_rows: one weight per agent")
+    so = np.asarray(seg_off, dtype=np.int64)
+    m = int(so[-1]) if len(so) else 0
+    if len(so) < 1 or so[0] != 0 or np.any(np.diff(so) < 0):
+        raise ValueError("segment offsets must start at 0 and be non-decreasing")
+    ti = None
+    if isinstance(idx, torch.Tensor):            # a device index kept by the caller (checked once there)
+        if idx.dtype != torch.int64 or idx.device != eng.dev or idx.numel() != m:
+            raise ValueError("state_hourly_rows: a device idx is int64, one entry per segment member")
+        ti = idx.contiguous()
+    elif idx is not None:
+        ix = np.asarray(idx, dtype=np.int64)
+        if len(ix) != m or (m and (ix.min() < 0 or ix.max() >= n)):
+            raise ValueError("state_hourly_rows: idx out of range")
+        ti = eng._to_dev(ix, torch.int64)
+    elif m > n:
+        raise ValueError("state_hourly_rows: segments exceed the batch")
+    S = len(so) - 1
+    out = torch.empty((S, nh), dtype=torch.float64, device=eng.dev)
+    t_off = eng._to_dev(so, torch.int64)
+    _lib.check(eng.lib.dgen_state_hourly_rows(eng.ctx, ctypes.byref(eng.tables), ctypes.byref(batch.c_agents),
+                                              ctypes.byref(c_out), with_batt.data_ptr(), w[0].data_ptr(),
+                                              w[1].data_ptr(), w[2].data_ptr(),
+                                              None if ti is None else ti.data_ptr(), n, t_off.data_ptr(), S,
+                                              out.data_ptr(), eng.stream_handle()), "dgen_state_hourly_rows")
+    torch.cuda.current_stream(eng.dev).synchronize()
+    return out
+
+
 def _len_safe(x) -> int:
     try:
         return len(x)

@@ -892,8 +892,12 @@ __device__ __forceinline__ void day_reread(uint32_t a, DayRaw& r) {
 // adds, ((double)pvo x w_pvo + (double)wbt x w_batt) + (double)base x w_non of
 // the float32-rounded plane values, in hour-quad tiles [h / 4][n][4] (8 B per
 // agent-hour instead of 12, and k_state_hourly reads one plane, bit-identical)
+// WO (with HOURLY, f32, daily plan): the with-battery plane alone (the
+// model-year loop's per-state export recomputes the load and PV-only net load
+// from the profile rows, dgen_state_hourly_rows): 4 B per agent-hour written
+// instead of 12.
 template <bool HOURLY, bool F64, bool NB, bool ROLL, bool DCR, bool LOSS = false, bool NEM = false, bool TS = false,
-          bool XP = false>
+          bool XP = false, bool WO = false>
 __global__ void __launch_bounds__(BLOCK, (ROLL || TS) ? 1 : 2)
 k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, void* ws,
               int64_t n_scratch, int64_t i0, int64_t i1, int m_lo, int m_hi, int batt_on, int nb_cap,
@@ -1167,7 +1171,7 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
         __builtin_amdgcn_s_waitcnt(0x0f70);                  // vmcnt(0)
         for (int d = c_month_start_day[m]; d < c_month_start_day[m + 1]; d++) {
             if (ROLL && d > d_lo) day_reread(dlane, r);    // the DMA was waited for yesterday
-            else if (HOURLY && d > d_lo) day_read<XP ? 12 : HB_STORES_AFTER_DMA * (F64 ? 2 : 1)>(dlane, r);
+            else if (HOURLY && d > d_lo) day_read<XP ? 12 : (WO ? 6 : HB_STORES_AFTER_DMA * (F64 ? 2 : 1))>(dlane, r);
             else day_read<0>(dlane, r);
             const bool wkend = (d % 7) >= 5;
             const uint64_t sched[3] = {wkend ? swe[0] : swd[0], wkend ? swe[1] : swd[1],
@@ -1292,6 +1296,8 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
                             for (int u = 0; u < 4; u++)
                                 xv[u] = ((double)qp[u] * xa + (double)qw[u] * xb) + (double)qb[u] * xd;
                             st_f32x4(ox + q16, off16, xv);
+                        } else if constexpr (WO) {
+                            st_f32x4(ow + q16, off16, qw);
                         } else {
                             st_f32x4(ob + q16, off16, qb);
                             st_f32x4(op + q16, off16, qp);
@@ -3412,11 +3418,22 @@ __device__ __forceinline__ YFlow yl_cashflow(const YLoan& L, double C, double ev
     S.lane[WAVE] = pb;
     wave_lds_sync();
     const double* col = S.lane - g.lane + g.base;
+    // the chains start at the wave's longest analysis period (wave-uniform
+    // trip count; a segment's lanes past its own period hold 0).  The other
+    // segment may be inactive here (diverged Brent paths): whatever its lane
+    // returns, the count stays within [own period, LPA], where every extra
+    // step adds an exact zero
+    int nmax = L.N < LPA ? L.N : LPA;
+    if constexpr (LPA < WAVE) {
+        const int o = __shfl_xor(nmax, LPA, WAVE);
+        nmax = o > nmax ? (o < LPA ? o : LPA) : nmax;
+    }
+    nmax = __builtin_amdgcn_readfirstlane(nmax);
     double acc = 0.0, run = -C, cum = -C;
-#pragma unroll 8
-    for (int k = LPA - 1; k >= 0; k--) acc = L.rr * acc + col[k];
-#pragma unroll 8
-    for (int k = 0; k < LPA; k++) {
+#pragma unroll 4
+    for (int k = nmax - 1; k >= 0; k--) acc = L.rr * acc + col[k];
+#pragma unroll 4
+    for (int k = 0; k < nmax; k++) {
         run = run + col[WAVE + k];
         cum = (g.sl == k) ? run : cum;
     }
@@ -4697,6 +4714,72 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
             (((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x]) / 1000.0;
 }
 
+// Per-state hourly export from the with-battery plane alone (the model-year
+// loop's form: dgen_size_agents with only the with-battery plane, WO): the
+// load and PV-only net load of agent-hour (i, h) are recomputed from the
+// profile rows exactly as k_hourly_batt forms them -- ld = shape x ls, pl = cf
+// x cl6, the float32 roundings of ld and max(ld - pl, 0) -- so every term, and
+// the sums (k_state_hourly's tiled order), are the three-plane form's, bit for
+// bit, from 4 B of plane per agent-hour instead of 12 (or a re-run scan).
+__global__ void __launch_bounds__(256)
+k_state_hourly_rows(dgen_tables T, dgen_agents A, dgen_outputs O, const float* __restrict__ wbt,
+                    const double* __restrict__ w_pvo, const double* __restrict__ w_batt,
+                    const double* __restrict__ w_non, const int64_t* __restrict__ idx, int64_t n,
+                    const int64_t* __restrict__ seg_off, int64_t n_seg, double* __restrict__ out) {
+    __shared__ double red[4][SH_TILE];
+    const int64_t s = blockIdx.x;
+    const int h0 = blockIdx.y * SH_TILE;
+    if (s >= n_seg || h0 >= NH) return;
+    const int nt = NH - h0 < SH_TILE ? NH - h0 : SH_TILE;
+    const int64_t lo = seg_off[s], hi = seg_off[s + 1];
+    double acc[SH_TILE];
+#pragma unroll
+    for (int t = 0; t < SH_TILE; t++) acc[t] = 0.0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += 256) {
+        const int64_t c = idx ? idx[i] : i;
+        const double a = w_pvo[c], b = w_batt[c], d = w_non[c];
+        const int lr = A.load_row[c], cr = A.cf_row[c];
+        const double ls = A.load_kwh[c] / T.shape_sum[lr];
+        const bool unsized = (O.status[c] & DGEN_ST_UNIT) != 0;
+        const double x_last = unsized ? 0.0 : O.x_last[c];
+        const double cl6 = (((x_last * 1000.0) * 0.96) / 1000.0) / 1e6;
+        const float* shp = T.shapes + (int64_t)lr * NH + h0;
+        const int32_t* cfp = T.cfs + (int64_t)cr * NH + h0;
+#pragma unroll
+        for (int q = 0; q < SH_TILE / 4; q++) {
+            if (4 * q < nt) {
+                const int64_t r = (((int64_t)(h0 >> 2) + q) * n + c) * 4;
+                const f32x4 xw = *reinterpret_cast<const f32x4*>(wbt + r);
+                const float4 sv = reinterpret_cast<const float4*>(shp)[q];
+                const int4 cv = reinterpret_cast<const int4*>(cfp)[q];
+                const float sh4[4] = {sv.x, sv.y, sv.z, sv.w};
+                const int32_t cf4[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const double ld = (double)sh4[u] * ls;
+                    const double pl = (double)cf4[u] * cl6;
+                    const double vb = (double)(float)ld;
+                    const double vp = (double)(float)fmax(ld - pl, 0.0);
+                    const double vw = (double)xw[u];
+                    acc[4 * q + u] += (vp * a + vw * b) + vb * d;
+                }
+            }
+        }
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int t = 0; t < SH_TILE; t++) {
+        double v = acc[t];
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+        if (lane == 0) red[wv][t] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < nt)
+        out[s * NH + h0 + threadIdx.x] =
+            (((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x]) / 1000.0;
+}
+
 // ---------------------------------------------------------------------------
 // Per-year agent attributes: the elec.apply_* left merges as
 // gathers from host-compiled per-year tables (include/dgen_hip.h
@@ -5081,14 +5164,21 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                            O->bill_w_batt, O->bill_wo_batt};
     for (const void* p : req_o)
         if (!p) { set_err("dgen_size_agents: missing output column"); return DGEN_E_ARG; }
+    // WO: the with-battery plane alone (float32 tiles; daily plan, no loss
+    // model, no demand machinery): the model-year loop's export form
+    const bool wo = O->baseline == nullptr && O->net_pvonly == nullptr && O->net_with_batt != nullptr;
     const bool hourly = O->baseline != nullptr;
-    if ((O->net_pvonly != nullptr) != hourly || (O->net_with_batt != nullptr) != hourly) {
-        set_err("dgen_size_agents: hourly planes must be all set or all NULL");
+    if (!wo && ((O->net_pvonly != nullptr) != hourly || (O->net_with_batt != nullptr) != hourly)) {
+        set_err("dgen_size_agents: hourly planes must be all set, all NULL, or the with-battery plane alone");
+        return DGEN_E_ARG;
+    }
+    if (wo && (O->hourly_f64 || c->cfg.batt_loss_model == 1 || c->cfg.batt_update_hours != 24)) {
+        set_err("dgen_size_agents: the with-battery plane alone is float32, daily plan, no loss model");
         return DGEN_E_ARG;
     }
     // k_hourly_batt forms a 32-bit per-lane byte offset i x 16 into the hourly tiles
     if (n >= ((int64_t)1 << 29) || n_scratch >= ((int64_t)1 << 28) ||
-        (hourly && n >= ((int64_t)1 << (O->hourly_f64 ? 27 : 28)))) {
+        ((hourly || wo) && n >= ((int64_t)1 << (O->hourly_f64 ? 27 : 28)))) {
         set_err("dgen_size_agents: batch too large (n < 2^29, n < 2^28 with f32 hourly planes, "
                 "2^27 with f64, n_scratch < 2^28 per call)");
         return DGEN_E_ARG;
@@ -5103,6 +5193,10 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     dgen_tables Tk = *T;
     // the demand machinery also supplies the month peaks of kWh/kW tier units
     const bool dc = (c->cfg.skip_demand_charges == 0 && Tk.n_demand > 0) || (Tk.peak_units && Tk.n_demand > 0);
+    if (wo && dc) {
+        set_err("dgen_size_agents: the with-battery plane alone is not built with demand charges / kWh/kW tiers");
+        return DGEN_E_ARG;
+    }
     if (dc && 4 * lds_half(Tk.max_periods) < DCP) Tk.max_periods = (DCP + 3) / 4;
     // yl_bill_nb stages its entries and month sums in slots 2 half .. 2 half + 4
     if (n_scratch > 0 && lds_half(Tk.max_periods) < 3) Tk.max_periods = 3;
@@ -5337,7 +5431,20 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         else if (c->cfg.batt_update_hours == 1) DGEN_HB_LAUNCH_R(H, F, REP, true);                \
         else DGEN_HB_LAUNCH_R(H, F, REP, false);                                                  \
     } while (0)
-            if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, false);
+            if (wo) {
+                if (nem_only)
+                    hipLaunchKernelGGL((k_hourly_batt<true, false, false, false, false, false, true, false, false, true>),
+                                       hgrid, block, lds, hs, *T, *A, *O, c->cfg, n, ws, n_scratch, ha, hb, m0, m1,
+                                       c->battery, 0, 0, nullptr, 0, 0);
+                else if (nb_scan)
+                    hipLaunchKernelGGL((k_hourly_batt<true, false, true, false, false, false, false, false, false, true>),
+                                       hgrid, block, lds, hs, *T, *A, *O, c->cfg, n, ws, n_scratch, ha, hb, m0, m1,
+                                       c->battery, c->nb_scan, 0, nullptr, 0, 0);
+                else
+                    hipLaunchKernelGGL((k_hourly_batt<true, false, false, false, false, false, false, false, false, true>),
+                                       hgrid, block, lds, hs, *T, *A, *O, c->cfg, n, ws, n_scratch, ha, hb, m0, m1,
+                                       c->battery, 0, 0, nullptr, 0, 0);
+            } else if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, false);
             else if (hourly) DGEN_HB_LAUNCH(true, false, false);
             else DGEN_HB_LAUNCH(false, false, false);
         }
@@ -5769,6 +5876,25 @@ int32_t dgen_state_hourly(dgen_ctx* c, const void* baseline, const void* pvonly,
         hipLaunchKernelGGL((k_state_hourly<double, false>), grid, dim3(256), 0, (hipStream_t)stream,
                            (const double*)baseline, (const double*)pvonly, (const double*)with_batt,
                            w_pvo, w_batt, w_non, idx, n, (int)n_hours, seg_off, n_seg, out);
+    HIP_TRY(hipGetLastError());
+    return DGEN_OK;
+}
+
+int32_t dgen_state_hourly_rows(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A, const dgen_outputs* O,
+                               const float* with_batt, const double* w_pvo, const double* w_batt,
+                               const double* w_non, const int64_t* idx, int64_t n, const int64_t* seg_off,
+                               int64_t n_seg, double* out, void* stream) {
+    if (!c || !T || !A || !O || !with_batt || !w_pvo || !w_batt || !w_non || !seg_off || !out || n < 0 ||
+        n_seg < 0 || n_seg > 0x7fffffff || !A->load_row || !A->cf_row || !A->load_kwh || !O->x_last ||
+        !O->status || !T->shapes || !T->cfs || !T->shape_sum) {
+        set_err("dgen_state_hourly_rows: bad argument");
+        return DGEN_E_ARG;
+    }
+    if (n_seg == 0) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    const dim3 grid((unsigned)n_seg, (unsigned)((NH + SH_TILE - 1) / SH_TILE));
+    hipLaunchKernelGGL(k_state_hourly_rows, grid, dim3(256), 0, (hipStream_t)stream, *T, *A, *O, with_batt,
+                       w_pvo, w_batt, w_non, idx, n, seg_off, n_seg, out);
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
 }

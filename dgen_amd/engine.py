@@ -303,10 +303,12 @@ class Engine:
                       or int((off.long() + cnt.long()).max().item()) > T.n_switches):
                 raise ValueError(f"rate-switch ({k}) offsets out of range")
 
-    def alloc_outputs(self, n: int, hourly: bool = True, hourly_f64: bool = False) -> Dict[str, object]:
+    def alloc_outputs(self, n: int, hourly=True, hourly_f64: bool = False) -> Dict[str, object]:
         """Device output buffers for n agents.  hourly_f64: the three hourly
         planes as float64 (the reference's fp64 lists, the kernels' own
-        values) instead of float32 (half the bytes; the default)."""
+        values) instead of float32 (half the bytes; the default).  hourly
+        "with_batt": the with-battery plane alone (float32; the model-year
+        loop's export, attachment.state_hourly_rows)."""
         torch = _torch()
         out = {}
         for name, dt in _lib.OUTPUT_SCALARS:
@@ -316,8 +318,9 @@ class Engine:
             out[name] = torch.zeros((n, _lib.MAXY + 1), dtype=torch.float64, device=self.dev)
         for name in _lib.OUTPUT_HOURLY:
             # hour-quad tiles (include/dgen_hip.h): [NH / 4][n][4]
+            want = hourly is True or (hourly == "with_batt" and name == "net_with_batt")
             out[name] = (torch.empty((_lib.NH // 4, n, 4), dtype=torch.float64 if hourly_f64 else torch.float32,
-                                     device=self.dev) if hourly else None)
+                                     device=self.dev) if want else None)
         return out
 
     @staticmethod

@@ -289,12 +289,20 @@ class YearLoop:
     exports from them in place (105 KB / agent of HBM), an int sizes the shard
     without planes and re-runs only the 8760-h scan (dgen_hourly_planes) in
     chunks of that many agents into a reusable plane buffer for the export
-    (the 2.5M-agents-per-GPU national case)."""
+    (the 2.5M-agents-per-GPU national case).  export: how the per-state
+    8760-h rows are made -- "with_batt" (the sizing scan writes the
+    with-battery plane alone, 35 KB / agent, and the export recomputes the
+    load and PV-only net load from the profile rows: dgen_state_hourly_rows),
+    "planes" (the three planes at sizing), "chunked" (hourly_chunk's re-run
+    scans), or "auto": with_batt where the scan supports it (daily plan, no
+    loss model, no demand machinery) and its plane fits in HBM, else planes
+    / chunked as hourly_chunk says.  Every form gives the same rows, bit for
+    bit."""
 
     def __init__(self, engine, pop, agents: Dict[str, np.ndarray], tables: LoopTables,
                  first_year: int = 2026, hourly_export: bool = True,
                  hourly_chunk: Optional[int] = None, order: Optional[np.ndarray] = None,
-                 plan=None, split: Optional[SplitGroups] = None):
+                 plan=None, split: Optional[SplitGroups] = None, export: str = "auto"):
         import torch
         from .engine import profile_order
         # plan and split come together: a split state's members must be
@@ -431,14 +439,39 @@ class YearLoop:
         self.carry = {k: z() for k in ("market_share_last_year", "adopters_cum_last_year",
                                        "market_value_last_year", "system_kw_cum_last_year",
                                        "batt_kw_cum_last_year", "batt_kwh_cum_last_year")}
-        whole = hourly_export and hourly_chunk is None
-        self.out = engine.alloc_outputs(n, hourly=whole)
+        self.export_mode = self._pick_export(engine, n, hourly_export, hourly_chunk, export)
+        if self.export_mode == "with_batt":
+            self.out = engine.alloc_outputs(n, hourly="with_batt")
+        else:
+            self.out = engine.alloc_outputs(n, hourly=self.export_mode == "planes")
         self.c_out = engine.c_outputs(self.out)
-        if hourly_export and hourly_chunk is not None:
+        if self.export_mode == "chunked":
             ch = min(int(hourly_chunk), max(n, 1))
             self._chunk_planes = {k: torch.empty(_lib.NH * ch, dtype=torch.float32, device=dev)
                                   for k in _lib.OUTPUT_HOURLY}
         self.Ld, self.La = _bind_diff(engine.lib), _bind_attach(engine.lib)
+
+    @staticmethod
+    def _pick_export(engine, n: int, hourly_export: bool, hourly_chunk, export: str) -> str:
+        if not hourly_export:
+            return "none"
+        cfg, T = engine.cfg, engine.tables
+        dc = T.n_demand > 0 and (cfg.skip_demand_charges == 0 or T.peak_units != 0)
+        wo_ok = cfg.batt_loss_model != 1 and cfg.batt_update_hours == 24 and not dc
+        legacy = "planes" if hourly_chunk is None else "chunked"
+        if export == "auto":
+            if not wo_ok:
+                return legacy
+            import torch
+            free, _ = torch.cuda.mem_get_info(engine.dev)
+            return "with_batt" if n * _lib.NH * 4 <= 0.6 * free else legacy
+        if export == "with_batt" and not wo_ok:
+            raise ValueError("export='with_batt' needs the daily plan, no loss model and no demand machinery")
+        if export == "chunked" and hourly_chunk is None:
+            raise ValueError("export='chunked' needs hourly_chunk")
+        if export not in ("with_batt", "planes", "chunked"):
+            raise ValueError(f"unknown export mode {export!r}")
+        return export
 
     # --------------------------------------------------------------- steps
     def apply_year_inputs(self, year: int):
@@ -601,7 +634,11 @@ class YearLoop:
         order (combined per state by partition.combine_rows)."""
         import torch
         eng = self.eng
-        if self.hourly_chunk is None:
+        if self.export_mode == "with_batt":
+            from .attachment import state_hourly_rows
+            return state_hourly_rows(eng, self.batch, self.c_out, self.out["net_with_batt"], w, self.s_dev,
+                                     self.s_off)
+        if self.export_mode == "planes":
             planes = (self.out["baseline"], self.out["net_pvonly"], self.out["net_with_batt"])
             return state_hourly(eng, planes, w, self.s_dev_idx, self.s_off)
         # chunked: runs of device rows get their hourly planes from the scan

@@ -590,6 +590,21 @@ int32_t dgen_hourly_planes(dgen_ctx* ctx, const dgen_tables* tables, const dgen_
  * instead of 12.  Daily plan without the loss model only (DGEN_E_ARG
  * otherwise: use dgen_hourly_planes).  n < 2^27.  Replaces nothing in the
  * reference (attachment_rate_functions.py:151-206 sums the frame's lists).   */
+/* The per-state export from the with-battery plane alone (ABI 11): a batch
+ * sized by dgen_size_agents with only outputs.net_with_batt set (float32
+ * hour-quad tiles; daily plan, no loss model, no demand charges / kWh/kW
+ * tiers) -- the load and PV-only net load of each agent-hour are recomputed
+ * from the profile rows (agents' load_row / cf_row / load_kwh, outputs'
+ * x_last / status) as the scan forms them, so out (per segment, 8760 rows,
+ * MW) equals dgen_state_hourly over the three float32 planes bit for bit,
+ * from 4 B of plane per agent-hour.  idx / seg_off as dgen_state_hourly.
+ * Replaces nothing in the reference (attachment_rate_functions.py:151-206
+ * sums the frame's hourly lists).                                           */
+int32_t dgen_state_hourly_rows(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
+                               const dgen_outputs* outputs, const float* with_batt, const double* w_pvo,
+                               const double* w_batt, const double* w_non, const int64_t* idx, int64_t n,
+                               const int64_t* seg_off, int64_t n_seg, double* out, void* stream);
+
 int32_t dgen_export_plane(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
                           const dgen_outputs* outputs, const double* w_pvo, const double* w_batt,
                           const double* w_non, double* plane, int64_t n, void* workspace,

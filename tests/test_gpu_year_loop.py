@@ -24,7 +24,7 @@ N = 2500
 YEARS = [2026, 2027, 2028]
 
 
-def _setup(engine, hourly_chunk=None, seed=20269001, config="national_mixed", first_year=YEARS[0]):
+def _setup(engine, hourly_chunk=None, seed=20269001, config="national_mixed", first_year=YEARS[0], export="auto"):
     pool = [STATES.index("DE")] if config == "de_res" else None
     pop = make_population(config, N, seed=seed, n_res_shapes=64, n_com_shapes=32,
                           n_cf=32, n_counties=16, n_tariffs=48, state_pool=pool)
@@ -34,7 +34,7 @@ def _setup(engine, hourly_chunk=None, seed=20269001, config="national_mixed", fi
     ag = loop_agents(pop, agent_id0=1000)
     tabs = LoopTables.synthetic()
     return pop, ag, tabs, YearLoop(engine, pop, ag, tabs, first_year=first_year,
-                                   hourly_export=True, hourly_chunk=hourly_chunk)
+                                   hourly_export=True, hourly_chunk=hourly_chunk, export=export)
 
 
 @pytest.mark.parametrize("config,years", [("national_mixed", YEARS),
@@ -42,7 +42,7 @@ def _setup(engine, hourly_chunk=None, seed=20269001, config="national_mixed", fi
                                           ("de_res", [2022, 2024, 2026])])
 def test_year_loop_matches_oracle_chain(engine, config, years):
     YEARS = years
-    pop, ag, tabs, loop = _setup(engine, config=config, first_year=years[0])
+    pop, ag, tabs, loop = _setup(engine, config=config, first_year=years[0], export="planes")
     perm = loop.perm
     inv = np.empty(N, np.int64)
     inv[perm] = np.arange(N)
@@ -117,12 +117,29 @@ def test_year_loop_matches_oracle_chain(engine, config, years):
 def test_chunked_hourly_export_matches_in_place(engine):
     """hourly_chunk re-sizes the shard in chunks (short last chunk included) for
     the export; it must agree with the export from the in-place planes."""
-    *_, whole = _setup(engine)
-    *_, chunked = _setup(engine, hourly_chunk=1000)
+    *_, whole = _setup(engine, export="planes")
+    *_, chunked = _setup(engine, hourly_chunk=1000, export="chunked")
     for y in YEARS[:2]:
         a, b = whole.run_year(y), chunked.run_year(y)
         assert torch.equal(a.totals, b.totals), y
         assert torch.allclose(a.hourly, b.hourly, rtol=1e-12, atol=1e-9), y
+
+
+def test_with_batt_plane_export_is_bit_identical(engine):
+    """export="with_batt" (the default where it fits): the sizing scan writes
+    the with-battery plane alone and dgen_state_hourly_rows recomputes the load
+    and PV-only net load from the rows -- the per-state rows equal the
+    three-plane export's bit for bit (and the chunked re-run's), every year."""
+    *_, planes = _setup(engine, export="planes")
+    *_, wo = _setup(engine, export="with_batt")
+    *_, chunked = _setup(engine, hourly_chunk=1700, export="chunked")
+    assert wo.export_mode == "with_batt" and wo.out["baseline"] is None
+    for y in YEARS:
+        a, b, c = planes.run_year(y), wo.run_year(y), chunked.run_year(y)
+        assert torch.equal(a.totals, b.totals), y
+        assert torch.equal(a.hourly, b.hourly), y
+        assert torch.allclose(c.hourly, b.hourly, rtol=1e-12, atol=1e-9), y
+        assert b.hourly.abs().sum() > 0
 
 
 @pytest.mark.parametrize("world,balanced", [(2, False), (3, True)])
