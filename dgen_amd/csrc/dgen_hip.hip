@@ -118,6 +118,16 @@ __device__ __forceinline__ double cf_per_kw(int32_t x) {
     return __builtin_fma(r, inv, q);
 }
 
+// cf_per_kw's common path (|x| <= 2e7, where it equals cf_per_kw); callers
+// check the range
+__device__ __forceinline__ double cf_per_kw_fast(int32_t x) {
+    const double a = (double)x;
+    constexpr double inv = 1.0 / 1e6;
+    const double q = a * inv;
+    const double r = __builtin_fma(-q, 1e6, a);
+    return __builtin_fma(r, inv, q);
+}
+
 // ---------------------------------------------------------------------------
 // numpy pairwise summation (loops_utils.h.src), chunked by the 8192-element
 // reduction buffer; identical association order => bit-identical to np.sum.
@@ -2800,6 +2810,57 @@ __device__ __forceinline__ float nb_weight_f(const YSrc& src, int h) {
 }
 __device__ __forceinline__ double nb_weight(const YSrc& src, int h) { return (double)nb_weight_f(src, h); }
 
+// (hour, day type) partials -> (period, quantity) sums at a month's end:
+// lane r = 4 p + q (and r + LPA when 4 MAXP > LPA) adds the hour lanes'
+// partials (their LDS columns) whose period is p, hours in order, weekdays
+// first -- a fixed order, a re-association of the serial hour sums.
+// k_nb_env's form: the month's two 24-hour schedules are read into registers
+// once (6 words each) instead of a byte load per hour, each of which waited
+// for its own round trip (yl_nb_build keeps those loads: inside k_size and
+// k_batt_finance the registers are short, and the register form measured
+// slower there).
+template <int LPA>
+__device__ __forceinline__ void nb_month_sums(const dgen_tariff& t, int m, int P, const Seg<LPA>& g, const YLds& S,
+                                              const double* col0, const double (&a0)[4], const double (&a1)[4],
+                                              const NbRec& R) {
+    constexpr int NR = (4 * MAXP + LPA - 1) / LPA;
+    uint32_t sw[2][6];
+    {
+        const uint32_t* d4 = reinterpret_cast<const uint32_t*>(t.wkday[m]);
+        const uint32_t* e4 = reinterpret_cast<const uint32_t*>(t.wkend[m]);
+#pragma unroll
+        for (int k = 0; k < 6; k++) { sw[0][k] = d4[k]; sw[1][k] = e4[k]; }
+    }
+    double v[NR];
+#pragma unroll
+    for (int k = 0; k < NR; k++) v[k] = 0.0;
+#pragma unroll
+    for (int dt = 0; dt < 2; dt++) {
+        wave_lds_sync();
+#pragma unroll
+        for (int q = 0; q < 4; q++) S.at(q) = dt ? a1[q] : a0[q];
+        wave_lds_sync();
+#pragma unroll
+        for (int k = 0; k < NR; k++) {
+            const int r = g.sl + k * LPA;
+            const bool on = r < 4 * P;
+            const int p = r >> 2;
+            const double* cq = col0 + (on ? (r & 3) : 0) * WAVE;
+#pragma unroll
+            for (int hh = 0; hh < 24; hh++) {
+                const int ph = (int)((sw[dt][hh >> 2] >> (8 * (hh & 3))) & 0xffu);
+                const double x = cq[hh];
+                v[k] = (on && ph == p) ? v[k] + x : v[k];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NR; k++) {
+        const int r = g.sl + k * LPA;
+        if (r < 4 * P) R.sums[(m * MAXP + (r >> 2)) * 4 + (r & 3)] = v[k];
+    }
+}
+
 // The segment builds the split cooperatively: lane k < 24 of the segment
 // takes hour k of every day (all days of a month share one period per hour
 // and day type), so a month is ~30 steps of 24 hours in parallel instead of
@@ -2920,7 +2981,8 @@ __device__ __forceinline__ bool yl_nb_build(const dgen_tariff& t, const YSrc& sr
         ok = ok && n_m <= NB_CAPM;
         if (g.sl == 0) R.cnt[m] = n_m;
         // (hour, day type) partials -> (period, quantity) sums
-        // lane r and (4 MAXP > LPA) lane r + LPA
+        // lane r and (4 MAXP > LPA) lane r + LPA (k_nb_env: nb_month_sums, the
+        // same order)
         constexpr int NR = (4 * MAXP + LPA - 1) / LPA;
         double v[NR];
 #pragma unroll
@@ -2972,6 +3034,70 @@ struct NbStage {                 // one segment's (agent's) days
 constexpr size_t NBS_BYTES = sizeof(NbStage);
 static_assert(NBS_BYTES % 16 == 0, "stage keeps 16-B alignment");
 
+__device__ __forceinline__ bool cf_slow(int32_t x) { return (uint32_t)x + 20000000u > 40000000u; }
+
+// One staged batch of nd days on the segment's hour lanes: the classification,
+// sums and entries of yl_nb_build<false>'s day loop, bit for bit, with the
+// batch's days formed four at a time (branch-free) ahead of their sums, and
+// the sums as a += v x {0, 1} in one fma each (exact: v + a or a; a is never
+// -0).  FAST: every cf value of the batch is in cf_per_kw's fast range.
+template <bool FAST>
+__device__ __forceinline__ void nbs_days(const NbStage* st, int hq, bool act, int nd, int d0, double ls, double tlo,
+                                         double thi, bool ts, int pd, int pe, double (&a0)[4], double (&a1)[4],
+                                         int& n_m, NbEnt* ent, unsigned long long segm, unsigned long long below) {
+    const int dow0 = d0 % 7;
+#pragma unroll 1
+    for (int k0 = 0; k0 < nd; k0 += 4) {
+        double L[4], G[4], mi[4], me[4];
+        float W[4];
+        bool mx[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int o = (k0 + j) * 24 + hq;       // k0 + j < NBS_DAYS: a day past nd is stale, unused
+            const double Lj = (double)st->sh[o] * ls;
+            const double gk = FAST ? cf_per_kw_fast(st->cf[o]) : cf_per_kw(st->cf[o]);
+            const float w = ts ? st->w[o] : 1.0f;
+            const double vlo = Lj - gk * tlo, vhi = Lj - gk * thi;
+            const double slack = 1e-10 * (fabs(Lj) + fabs(gk) * thi);
+            const bool imp = act && fmin(vlo, vhi) > slack;              // imports at every t
+            const bool exq = act && !imp && fmax(vlo, vhi) < -slack;     // exports at every t
+            L[j] = Lj;
+            G[j] = gk;
+            W[j] = w;
+            mi[j] = imp ? 1.0 : 0.0;
+            me[j] = exq ? 1.0 : 0.0;
+            mx[j] = act && !imp && !exq;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (k0 + j >= nd) break;                 // uniform
+            const bool we = ((dow0 + k0 + j) % 7) >= 5;
+            const double wd = (double)W[j];
+            const double x0 = G[j] * wd, x1 = L[j] * wd;
+            if (we) {
+                a1[0] = __builtin_fma(L[j], mi[j], a1[0]); a1[1] = __builtin_fma(G[j], mi[j], a1[1]);
+                a1[2] = __builtin_fma(x0, me[j], a1[2]);   a1[3] = __builtin_fma(x1, me[j], a1[3]);
+            } else {
+                a0[0] = __builtin_fma(L[j], mi[j], a0[0]); a0[1] = __builtin_fma(G[j], mi[j], a0[1]);
+                a0[2] = __builtin_fma(x0, me[j], a0[2]);   a0[3] = __builtin_fma(x1, me[j], a0[3]);
+            }
+            const unsigned long long bm = __ballot(mx[j]) & segm;
+            if (mx[j]) {
+                const int pos = n_m + __popcll(bm & below);
+                if (pos < NB_CAPM) {
+                    NbEnt e;
+                    e.L = L[j];
+                    e.g = G[j];
+                    e.w = W[j];
+                    e.p = we ? pe : pd;
+                    ent[pos] = e;
+                }
+            }
+            n_m += __popcll(bm);
+        }
+    }
+}
+
 template <int LPA>
 __device__ __forceinline__ bool yl_nb_build_stg(const dgen_tariff& t, const YSrc& src, double tlo, double thi,
                                                 char* nbp, const YLds& S, const Seg<LPA>& g, NbStage* st) {
@@ -2995,6 +3121,7 @@ __device__ __forceinline__ bool yl_nb_build_stg(const dgen_tariff& t, const YSrc
         for (int d0 = ds; d0 < de; d0 += NBS_DAYS) {
             const int nd = de - d0 < NBS_DAYS ? de - d0 : NBS_DAYS;
             wave_lds_sync();                              // the previous batch's reads
+            bool bad = false;                             // a cf value outside cf_per_kw's fast range
             {
                 const int k = g.sl & (NBS_DAYS - 1);
                 const int d = d0 + (k < nd ? k : nd - 1);
@@ -3009,6 +3136,7 @@ __device__ __forceinline__ bool yl_nb_build_stg(const dgen_tariff& t, const YSrc
                     for (int q = 0; q < 6; q++) {
                         reinterpret_cast<float4*>(st->sh + k * 24)[q] = sv[q];
                         reinterpret_cast<int4*>(st->cf + k * 24)[q] = cv[q];
+                        bad = bad | cf_slow(cv[q].x) | cf_slow(cv[q].y) | cf_slow(cv[q].z) | cf_slow(cv[q].w);
                     }
                 } else if (src.ts) {
                     const double2* t2 = reinterpret_cast<const double2*>(src.ts + d * 24);
@@ -3023,69 +3151,18 @@ __device__ __forceinline__ bool yl_nb_build_stg(const dgen_tariff& t, const YSrc
                 }
             }
             wave_lds_sync();
-#pragma unroll 4
-            for (int k = 0; k < nd; k++) {
-                const int d = d0 + k;
-                const bool we = (d % 7) >= 5;
-                const double L = (double)st->sh[k * 24 + hq] * src.load_scale;
-                const double gk = cf_per_kw(st->cf[k * 24 + hq]);
-                const float w = src.ts ? st->w[k * 24 + hq] : 1.0f;
-                const double vlo = L - gk * tlo, vhi = L - gk * thi;
-                const double slack = 1e-10 * (fabs(L) + fabs(gk) * thi);
-                const bool imp = act && fmin(vlo, vhi) > slack;              // imports at every t
-                const bool exq = act && !imp && fmax(vlo, vhi) < -slack;     // exports at every t
-                const double wd = (double)w;
-                const double i0 = imp ? L : 0.0, i1 = imp ? gk : 0.0;
-                const double x0 = exq ? gk * wd : 0.0, x1 = exq ? L * wd : 0.0;
-                if (we) {
-                    a1[0] += i0; a1[1] += i1; a1[2] += x0; a1[3] += x1;
-                } else {
-                    a0[0] += i0; a0[1] += i1; a0[2] += x0; a0[3] += x1;
-                }
-                const bool mx = act && !imp && !exq;
-                const unsigned long long bm = __ballot(mx) & segm;
-                if (mx) {
-                    const int pos = n_m + __popcll(bm & below);
-                    if (pos < NB_CAPM) {
-                        NbEnt e;
-                        e.L = L;
-                        e.g = gk;
-                        e.w = w;
-                        e.p = we ? pe : pd;
-                        ent[pos] = e;
-                    }
-                }
-                n_m += __popcll(bm);
-            }
+            // wave-uniform: every staged cf value of both segments takes
+            // cf_per_kw's fast form, so the days run without its branch
+            if (__ballot(bad) == 0)
+                nbs_days<true>(st, hq, act, nd, d0, src.load_scale, tlo, thi, src.ts != nullptr, pd, pe, a0, a1,
+                               n_m, ent, segm, below);
+            else
+                nbs_days<false>(st, hq, act, nd, d0, src.load_scale, tlo, thi, src.ts != nullptr, pd, pe, a0, a1,
+                                n_m, ent, segm, below);
         }
         ok = ok && n_m <= NB_CAPM;
         if (g.sl == 0) R.cnt[m] = n_m;
-        // (hour, day type) partials -> (period, quantity) sums, as yl_nb_build
-        constexpr int NR = (4 * MAXP + LPA - 1) / LPA;
-        double v[NR];
-#pragma unroll
-        for (int k = 0; k < NR; k++) v[k] = 0.0;
-        for (int dt = 0; dt < 2; dt++) {
-            wave_lds_sync();
-#pragma unroll
-            for (int q = 0; q < 4; q++) S.at(q) = dt ? a1[q] : a0[q];
-            wave_lds_sync();
-            const uint8_t* sc = dt ? t.wkend[m] : t.wkday[m];
-#pragma unroll
-            for (int k = 0; k < NR; k++) {
-                const int r = g.sl + k * LPA;
-                if (r < 4 * P) {
-                    const int p = r >> 2, q = r & 3;
-                    for (int hh = 0; hh < 24; hh++)
-                        if ((int)sc[hh] == p) v[k] += col0[q * WAVE + hh];
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NR; k++) {
-            const int r = g.sl + k * LPA;
-            if (r < 4 * P) R.sums[(m * MAXP + (r >> 2)) * 4 + (r & 3)] = v[k];
-        }
+        nb_month_sums<LPA>(t, m, P, g, S, col0, a0, a1, R);
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
@@ -3683,7 +3760,7 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 template <int LPA, bool DC, bool NET, bool PK>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
-         void* dcws, char* nbws, int dc_pre) {
+         void* dcws, char* nbws, int pre) {
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -3710,7 +3787,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     if constexpr (DC) {
         if (dcws) {
             c.env = dc_env_at(dcws, i);
-            c.env_tag = dc_pre ? *c.env.tag : 0;          // k_dc_env's, this call
+            c.env_tag = (pre & 1) ? *c.env.tag : 0;       // k_dc_env's, this call
         }
         // the segment's envelope stage sits after the year-lane layout
         c.stg = reinterpret_cast<DcStage*>(reinterpret_cast<char*>(dyn_lds) +
@@ -3720,7 +3797,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         const int slot = A.scratch_slot[i];
         c.nb = (nbws && slot >= 0) ? nbws + (size_t)slot * NB_BYTES : nullptr;
         c.nb_ok = false;
-        c.nb_tag = c.nb ? nbr_tag(c.nb) : 0;  // k_nb_env's, this step
+        c.nb_tag = (c.nb && (pre & 2)) ? nbr_tag(c.nb) : 0;  // k_nb_env's, this call
         c.nb_pending = false;
     }
     c.sw_rows = T.switches + A.sw_solar_off[i];
@@ -3883,16 +3960,8 @@ __device__ __forceinline__ int first_eval_tariff(const dgen_tables& T, const dge
 // ---------------------------------------------------------------------------
 constexpr int DCE_WPB = 4;          // agents (one wave each) per block
 
-// cf_per_kw's common path (|x| <= 2e7, where it equals x / 1e6 exactly); the
-// kernel checks the range per day and leaves an agent with a larger value to
-// k_size's build
-__device__ __forceinline__ double cf_per_kw_fast(int32_t x) {
-    const double a = (double)x;
-    constexpr double inv = 1.0 / 1e6;
-    const double q = a * inv;
-    const double r = __builtin_fma(-q, 1e6, a);
-    return __builtin_fma(r, inv, q);
-}
+// (k_dc_env takes cf_per_kw_fast after a per-day range check and leaves an
+// agent with a larger value to k_size's build)
 
 // first maximiser over the lane's 32-lane half: larger value, ties to the
 // earlier hour
@@ -4939,6 +5008,7 @@ struct dgen_ctx {
     int hb_nem;        // 1: batches without scratch slots run the bins-only scan (DGEN_HB_NEM=0: off)
     int ts_scan;       // 1: the TS sell-rate agents' split built in their own scan (DGEN_TS_SCAN=0: off, A/B)
     int dc_pre;        // 1: the first-evaluation tariff's demand envelopes prebuilt by k_dc_env (DGEN_DC_PREBUILD=0: off)
+    int nb_pre;        // 1: its net-billing split prebuilt by k_nb_env (DGEN_NB_PREBUILD=0: off, k_size builds it)
     int64_t ts_lo, ts_hi;   // the batch rows holding every TS-capable agent (dgen_set_ts_rows)
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
@@ -5044,6 +5114,8 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
         c->ts_scan = (x && x[0] == '0') ? 0 : 1;
         const char* y = getenv("DGEN_DC_PREBUILD");
         c->dc_pre = (y && y[0] == '0') ? 0 : 1;
+        const char* z = getenv("DGEN_NB_PREBUILD");
+        c->nb_pre = (z && z[0] == '0') ? 0 : 1;
     }
     c->ts_lo = 0;
     c->ts_hi = INT64_MAX;
@@ -5302,6 +5374,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // demand envelopes of the first-evaluation tariffs prebuilt (k_dc_env)
     const int dc_pre = (dc && c->dc_buf && c->dc_pre) ? 1 : 0;
     c->last_paths[6] = dc_pre;
+    const int nb_pre = (n_scratch > 0 && c->nb_pre) ? 1 : 0;
+    const int pre = dc_pre | (nb_pre << 1);     // k_size's view of the two prebuilds
     HIP_TRY(hipEventRecord(c->fork, s));
     HIP_TRY(hipStreamWaitEvent(s2, c->fork, 0));
     for (int j = 0; j < nch; j++) {
@@ -5310,7 +5384,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipEventRecord(e[0], s));
         // net-billing splits and demand envelopes of the initial tariffs
         // (counted in k_size's time)
-        if (n_scratch > 0)
+        if (nb_pre)
             hipLaunchKernelGGL((k_nb_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE),
                                4 * WAVE * sizeof(double) + 2 * NBS_BYTES, s,
                                *T, *A, i0, i1, nbws);
@@ -5333,34 +5407,34 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
 #if !DGEN_NO2_SIZE
             if (net)
                 hipLaunchKernelGGL((k_size_w<32, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
-                                   n, i0, i1, nullptr, nbws, 0);
+                                   n, i0, i1, nullptr, nbws, pre);
             else
                 hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws, 0);
+                                   c->cfg, n, i0, i1, nullptr, nbws, pre);
 #endif
         } else if (lpa_s == 32 && !pk) {
 #if !DGEN_NO2_SIZE_DC
             hipLaunchKernelGGL((k_size_w<32, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws, dc_pre);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
 #endif
         } else if (lpa_s == 32) {
 #if !DGEN_NO2_SIZE_PK
             hipLaunchKernelGGL((k_size_w<32, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws, dc_pre);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
 #endif
         } else if (!dc) {
             if (net)
                 hipLaunchKernelGGL((k_size_w<WAVE, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws, 0);
+                                   c->cfg, n, i0, i1, nullptr, nbws, pre);
             else
                 hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws, 0);
+                                   c->cfg, n, i0, i1, nullptr, nbws, pre);
         } else if (!pk) {
             hipLaunchKernelGGL((k_size_w<WAVE, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws, dc_pre);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
         } else {
             hipLaunchKernelGGL((k_size_w<WAVE, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws, dc_pre);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
         }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));

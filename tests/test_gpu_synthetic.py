@@ -110,6 +110,41 @@ def test_profile_order_is_invisible(engine, cfg, n):
         assert np.array_equal(a[k], b[k], equal_nan=True), k
 
 
+@pytest.mark.parametrize("cfg,n", [("ca_res_storage", 2000), ("national_mixed", 3000)])
+def test_nb_prebuild_is_invisible(engine, cfg, n, monkeypatch):
+    """The first-evaluation tariff's net-billing split built ahead of the
+    search by k_nb_env (its LDS-staged, four-days-at-a-time form) is the split
+    k_size builds itself with the prebuild off (DGEN_NB_PREBUILD=0): every
+    output bit-identical, long lives (one agent per wave) included."""
+    from dgen_amd.engine import Engine
+    pop = _small_pop(cfg, n)
+    life = pop.cols["econ_life"].copy()
+    life[::5] = 33 + (np.arange(life[::5].size) % 18)
+    pop.cols["econ_life"] = life
+    monkeypatch.setenv("DGEN_NB_PREBUILD", "0")
+    off = Engine(0)
+    monkeypatch.delenv("DGEN_NB_PREBUILD")
+    res = []
+    try:
+        for eng in (engine, off):
+            eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+            eng.set_tariffs(pop.tariffs)
+            eng.set_switches(pop.switches)
+            batch = eng.upload_agents(pop.cols, pop.n_scratch)
+            out = eng.alloc_outputs(batch.n, hourly=True)
+            eng.size(batch, out)
+            torch.cuda.synchronize()
+            res.append(outputs_to_host(out))
+            del out, batch
+    finally:
+        off.close()
+    a, b = res
+    for k in a:
+        if a[k] is None:
+            continue
+        assert np.array_equal(a[k], b[k], equal_nan=True), k
+
+
 @pytest.mark.parametrize("cfg,nb_scan", [("national_mixed", None), ("national_mixed", True),
                                          ("ca_res_storage", None)])
 def test_pipeline_depth_is_invisible(engine, cfg, nb_scan):
