@@ -3111,6 +3111,20 @@ __device__ __forceinline__ bool yl_nb_build_stg(const dgen_tariff& t, const YSrc
     const unsigned long long below = (1ull << g.lane) - 1ull;
     double* col0 = S.lane - g.sl;          // the segment's first lane's LDS column
     bool ok = true;
+    // the next batch's rows in flight during the current batch's days: lane
+    // sl < NBS_DAYS holds day sl's 24 shape values, lane NBS_DAYS + k day k's
+    // 24 cf values (16-B loads; a day past the batch repeats its last day)
+    const int kf = g.sl & (NBS_DAYS - 1);
+    const bool pf_cf = g.sl >= NBS_DAYS;
+    uint4 pf[6];
+    auto fetch = [&](int b0, int bn) {
+        const int d = b0 + (kf < bn ? kf : bn - 1);
+        const uint4* p4 = pf_cf ? reinterpret_cast<const uint4*>(src.cf + d * 24)
+                                : reinterpret_cast<const uint4*>(src.shape + d * 24);
+#pragma unroll
+        for (int q = 0; q < 6; q++) pf[q] = p4[q];
+    };
+    fetch(0, NBS_DAYS);
     for (int m = 0; m < 12; m++) {
         const int pd = act ? (int)t.wkday[m][hd] : 0, pe = act ? (int)t.wkend[m][hd] : 0;
         double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0};
@@ -3123,31 +3137,37 @@ __device__ __forceinline__ bool yl_nb_build_stg(const dgen_tariff& t, const YSrc
             wave_lds_sync();                              // the previous batch's reads
             bool bad = false;                             // a cf value outside cf_per_kw's fast range
             {
-                const int k = g.sl & (NBS_DAYS - 1);
+                uint4* dst = reinterpret_cast<uint4*>(pf_cf ? reinterpret_cast<char*>(st->cf + kf * 24)
+                                                            : reinterpret_cast<char*>(st->sh + kf * 24));
+#pragma unroll
+                for (int q = 0; q < 6; q++) {
+                    dst[q] = pf[q];
+                    bad = bad | (pf_cf & (cf_slow((int32_t)pf[q].x) | cf_slow((int32_t)pf[q].y) |
+                                          cf_slow((int32_t)pf[q].z) | cf_slow((int32_t)pf[q].w)));
+                }
+            }
+            if (src.ts) {                                 // sell weights: lane sl = day sl / 2, half sl % 2
+                const int k = g.sl >> 1, hf = g.sl & 1;
                 const int d = d0 + (k < nd ? k : nd - 1);
-                if (g.sl < NBS_DAYS) {
-                    const float4* s4 = reinterpret_cast<const float4*>(src.shape + d * 24);
-                    const int4* c4 = reinterpret_cast<const int4*>(src.cf + d * 24);
-                    float4 sv[6];
-                    int4 cv[6];
+                const double2* t2 = reinterpret_cast<const double2*>(src.ts + d * 24 + hf * 12);
+                double2 tv[6];
 #pragma unroll
-                    for (int q = 0; q < 6; q++) { sv[q] = s4[q]; cv[q] = c4[q]; }
+                for (int q = 0; q < 6; q++) tv[q] = t2[q];
 #pragma unroll
-                    for (int q = 0; q < 6; q++) {
-                        reinterpret_cast<float4*>(st->sh + k * 24)[q] = sv[q];
-                        reinterpret_cast<int4*>(st->cf + k * 24)[q] = cv[q];
-                        bad = bad | cf_slow(cv[q].x) | cf_slow(cv[q].y) | cf_slow(cv[q].z) | cf_slow(cv[q].w);
-                    }
-                } else if (src.ts) {
-                    const double2* t2 = reinterpret_cast<const double2*>(src.ts + d * 24);
-                    double2 tv[12];
-#pragma unroll
-                    for (int q = 0; q < 12; q++) tv[q] = t2[q];
-#pragma unroll
-                    for (int q = 0; q < 6; q++)
-                        reinterpret_cast<float4*>(st->w + k * 24)[q] =
-                            make_float4((float)(tv[2 * q].x * src.ts_mult), (float)(tv[2 * q].y * src.ts_mult),
-                                        (float)(tv[2 * q + 1].x * src.ts_mult), (float)(tv[2 * q + 1].y * src.ts_mult));
+                for (int q = 0; q < 3; q++)
+                    reinterpret_cast<float4*>(st->w + k * 24 + hf * 12)[q] =
+                        make_float4((float)(tv[2 * q].x * src.ts_mult), (float)(tv[2 * q].y * src.ts_mult),
+                                    (float)(tv[2 * q + 1].x * src.ts_mult), (float)(tv[2 * q + 1].y * src.ts_mult));
+            }
+            {                                             // the next batch (maybe next month's first)
+                // drain what is pending (this month's pd / pe bytes): the day
+                // loop uses them, and a value pending at the loop's entry
+                // makes the compiler drain vmcnt there -- the prefetch with it
+                __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0)
+                const int nx = d0 + nd;
+                if (nx < 365) {
+                    const int me = c_month_start_day[(nx < de ? m : m + 1) + 1];
+                    fetch(nx, me - nx < NBS_DAYS ? me - nx : NBS_DAYS);
                 }
             }
             wave_lds_sync();
