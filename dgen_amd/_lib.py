@@ -57,7 +57,7 @@ class Tables(ctypes.Structure):
         ("n_shapes", _i64), ("n_cfs", _i64), ("n_wholesale", _i64), ("n_switches", _i64),
         ("n_tariffs", _i32), ("max_periods", _i32),
         ("demand", _vp), ("n_demand", _i32), ("peak_units", _i32),
-        ("max_dc_periods", _i32), ("pad_t", _i32),
+        ("max_dc_periods", _i32), ("no_net", _i32),
     ]
 
 
@@ -105,7 +105,7 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
-ABI_VERSION = 11   # include/dgen_hip.h DGEN_ABI_VERSION
+ABI_VERSION = 12   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
 DEFAULT_HOURLY_SPLIT = 2   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_SPLIT

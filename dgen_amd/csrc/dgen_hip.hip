@@ -921,6 +921,10 @@ k_hourly_batt(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_
     // running annual PV sum carry between launches in W.carry)
     int64_t i = i0 + (int64_t)blockIdx.x * BLOCK + threadIdx.x;
     if (i >= i1) return;
+    // the TS agents' scan runs one wave per SIMD beside the other parts' waves
+    // and is the national step's critical path: its waves issue first
+    // (national 200k k_hourly_batt 8.5 -> 8.2 ms, profiles/r05/ts_prio)
+    if constexpr (TS) __builtin_amdgcn_s_setprio(3);
     if (O.status[i] & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_YEARS)) return;
     if (ts_mode) {
         const bool ts_cap = A.scratch_slot[i] >= 0 && A.wholesale_row[i] >= 0 && (A.flags[i] & 2) == 0 &&
@@ -5423,6 +5427,10 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         // net billing compiled in only when the batch has scratch slots (an
         // agent whose tariffs can bill net always gets one, assign_scratch)
         const bool net = n_scratch > 0;
+        // demand-charge batches: the net-billing paths only when some tariff
+        // of the table bills net (dgen_tables.no_net; registers: C4 k_size
+        // spills 412 -> 200 B per lane without them)
+        const bool dc_net = T->no_net == 0;
         if (lpa_s == 32 && !dc) {
 #if !DGEN_NO2_SIZE
             if (net)
@@ -5434,8 +5442,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
 #endif
         } else if (lpa_s == 32 && !pk) {
 #if !DGEN_NO2_SIZE_DC
-            hipLaunchKernelGGL((k_size_w<32, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+            if (dc_net)
+                hipLaunchKernelGGL((k_size_w<32, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+            else
+                hipLaunchKernelGGL((k_size_w<32, true, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
 #endif
         } else if (lpa_s == 32) {
 #if !DGEN_NO2_SIZE_PK
@@ -5450,8 +5462,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws, pre);
         } else if (!pk) {
-            hipLaunchKernelGGL((k_size_w<WAVE, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+            if (dc_net)
+                hipLaunchKernelGGL((k_size_w<WAVE, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+            else
+                hipLaunchKernelGGL((k_size_w<WAVE, true, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
         } else {
             hipLaunchKernelGGL((k_size_w<WAVE, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
                                c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
@@ -5584,8 +5600,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
 #endif
         } else if (lpa_f == 32 && !pk) {
 #if !DGEN_NO2_FIN_DC
-            hipLaunchKernelGGL((k_batt_finance_w<32, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                               *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
+            if (dc_net)
+                hipLaunchKernelGGL((k_batt_finance_w<32, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
+            else
+                hipLaunchKernelGGL((k_batt_finance_w<32, true, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
 #endif
         } else if (lpa_f == 32) {
 #if !DGEN_NO2_FIN_PK
@@ -5600,8 +5620,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
                                    *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
         } else if (!pk) {
-            hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
-                               *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
+            if (dc_net)
+                hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
+                                   *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
+            else
+                hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
+                                   *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
         } else {
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
                                *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);

@@ -41,6 +41,8 @@ class AgentBatch:
     nb_scan: bool = True
     # device rows holding every TS-capable agent (dgen_set_ts_rows)
     ts_rows: tuple = (0, 2 ** 62)
+    # no agent can bill net hourly (dgen_tables.no_net, Engine._no_net_of)
+    no_net: bool = False
 
 
 def path_class(cols: Dict[str, np.ndarray]) -> np.ndarray:
@@ -190,6 +192,7 @@ class Engine:
         self.tables.tariffs = _ptr(t)
         self.tables.n_tariffs = int(recs.size)
         self.tables.max_periods = int(recs["P"].max())
+        self.tables.no_net = 0                # set per batch by size() (AgentBatch.no_net)
 
     def set_switches(self, sw: np.ndarray):
         sw = np.ascontiguousarray(sw, dtype=SWITCH_DTYPE)
@@ -200,6 +203,7 @@ class Engine:
         self._keep["switches"] = t
         self.tables.switches = _ptr(t)
         self.tables.n_switches = int(sw.size)
+        self._switch_tariff = sw["tariff"].copy()
 
     def profile_sums(self):
         """(shape row sums, cf naep) as host arrays (for tests / host checks)."""
@@ -246,7 +250,8 @@ class Engine:
         ca = _lib.Agents(**{name: _ptr(dev[name]) for name, _ in _lib.AGENT_COLUMNS})
         ca.max_years = int(dev["econ_life"].max().item()) if n else 0
         return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order,
-                          nb_scan=self._nb_scan_pays(cols, n, n_scratch), ts_rows=self._ts_rows_of(cols, n))
+                          nb_scan=self._nb_scan_pays(cols, n, n_scratch), ts_rows=self._ts_rows_of(cols, n),
+                          no_net=self._no_net_of(cols, n))
 
     def _ts_rows_of(self, cols, n: int):
         """dgen_set_ts_rows: the device rows [lo, hi) holding every agent that
@@ -259,13 +264,50 @@ class Engine:
         ix = np.flatnonzero(pc == 2)
         return (int(ix[0]), int(ix[-1]) + 1) if ix.size else (0, 0)
 
+    def _no_net_of(self, cols, n: int) -> bool:
+        """True when no agent of the batch can bill net hourly (metering
+        options 2, 3): neither its initial tariff nor any rate-switch candidate
+        (solar or storage rows).  dgen_tables.no_net then lets the demand-charge
+        kernels run their instantiations without the net-billing paths (fewer
+        registers; results identical, the paths are unreachable).  False when
+        the tariff or switch table is unknown."""
+        mo = getattr(self, "_tariff_mo", None)
+        if mo is None or n == 0:
+            return False
+        net = np.isin(mo, (2, 3))
+        if not net.any():
+            return True
+        t0 = np.asarray(cols["tariff0"], np.int64)
+        if ((t0 < 0) | (t0 >= net.size)).any() or net[t0].any():
+            return False
+        swt = getattr(self, "_switch_tariff", None)
+        if swt is None:
+            return False
+        sw_net = np.zeros(swt.size, bool)
+        okr = (swt >= 0) & (swt < net.size)
+        sw_net[okr] = net[swt[okr]]
+        csum = np.concatenate([[0], np.cumsum(sw_net.astype(np.int64))])
+        for k in ("solar", "storage"):
+            off = np.asarray(cols[f"sw_{k}_off"], np.int64)
+            cnt = np.asarray(cols[f"sw_{k}_cnt"], np.int64)
+            lo = np.clip(off, 0, swt.size)
+            hi = np.clip(off + cnt, 0, swt.size)
+            if ((csum[hi] - csum[lo]) > 0).any():
+                return False
+        return True
+
     def _nb_scan_pays(self, cols, n: int, n_scratch: int) -> bool:
         """dgen_set_nb_scan: the battery case's net-billing split is built in
         the hourly scan for every agent that bills net (the scan decides per
         agent; profile_order groups those agents into their own waves; the TS
         sell-rate agents get a scan of their own when hourly planes are
         requested, dgen_size_agents' ts_split), so an agent's battery-case
-        outputs do not depend on the other agents of its batch.  The scan form
+        outputs do not depend on the other agents of its batch.  They do
+        depend on the hourly flag for the TS agents: without planes their split
+        comes from k_batt_finance's plane pass, whose sums re-associate (the
+        four battery-case money outputs move by ~1e-9 relative; sizing and
+        every discrete decision are the same bits,
+        test_ts_agent_outputs_with_and_without_planes).  The scan form
         is compiled in only when the batch holds such an agent (its
         instantiation carries the export sums: more registers, and with the
         demand records a spill), which changes no result.  DGEN_NB_SCAN=0 turns it off (A/B: the finance kernel's build
@@ -339,6 +381,7 @@ class Engine:
     def size(self, batch: AgentBatch, out: Dict[str, object], c_out: Optional[_lib.Outputs] = None):
         """Launch the sizing kernels for `batch` on the current stream (async)."""
         co = c_out if c_out is not None else self.c_outputs(out)
+        self.tables.no_net = int(batch.no_net)
         if batch.nb_scan != getattr(self, "_nb_scan", True):
             _lib.check(self.lib.dgen_set_nb_scan(self.ctx, _lib.NB_CAPM if batch.nb_scan else 0),
                        "dgen_set_nb_scan")

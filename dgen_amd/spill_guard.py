@@ -47,9 +47,11 @@ PASS = ("s_", "v_writelane", "v_readlane", "v_mov", "v_accvgpr_read", "v_accvgpr
 REMEDY = {
     "k_size_wILi32ELb0E": "DGEN_NO2_SIZE",
     "k_size_wILi32ELb1ELb1ELb0E": "DGEN_NO2_SIZE_DC",
+    "k_size_wILi32ELb1ELb0ELb0E": "DGEN_NO2_SIZE_DC",
     "k_size_wILi32ELb1ELb1ELb1E": "DGEN_NO2_SIZE_PK",
     "k_batt_finance_wILi32ELb0E": "DGEN_NO2_FIN",
     "k_batt_finance_wILi32ELb1ELb1ELb0E": "DGEN_NO2_FIN_DC",
+    "k_batt_finance_wILi32ELb1ELb0ELb0E": "DGEN_NO2_FIN_DC",
     "k_batt_finance_wILi32ELb1ELb1ELb1E": "DGEN_NO2_FIN_PK",
 }
 

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 11
+#define DGEN_ABI_VERSION 12
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_DEFAULT_HOURLY_SPLIT 2   /* parts of a chunk's hourly scan, each on its own stream */
@@ -184,7 +184,12 @@ typedef struct {
                                    /* peaks per lane (see dgen_tariff.unit)          */
     int32_t max_dc_periods;        /* 1 + the largest period in the demand records' */
                                    /* schedules (sizes LDS; 0 = DGEN_DCP)           */
-    int32_t pad_t;
+    int32_t no_net;                /* 1: no agent of the call can bill net hourly   */
+                                   /* (metering options 2, 3: initial tariff and    */
+                                   /* every rate-switch candidate): the demand-     */
+                                   /* charge kernels run their instantiations       */
+                                   /* without the net-billing paths (fewer          */
+                                   /* registers); 0: some may (ABI 12)              */
 } dgen_tables;
 
 /* Agent batch, structure of arrays (device pointers, length n).  Column

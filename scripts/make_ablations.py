@@ -319,6 +319,13 @@ VARIANTS["ks_occ4"] = [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(
 # the demand-charge instantiations at 3 waves per SIMD (168 VGPRs: spills)
 VARIANTS["ks_dc3"] = [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(3)")]
 
+# yl_build_bins: slot sums loaded 12 / 24 per row and batch (2 / 1 batches per
+# day type instead of 3): C3 k_size 9.3 -> 9.7 / 14.5 ms (profiles/r05/s18)
+VARIANTS["bins_b12"] = [("        constexpr int BB = 8;\n        const double* lm = lslots + m * 48;",
+                         "        constexpr int BB = 12;\n        const double* lm = lslots + m * 48;")]
+VARIANTS["bins_b24"] = [("        constexpr int BB = 8;\n        const double* lm = lslots + m * 48;",
+                         "        constexpr int BB = 24;\n        const double* lm = lslots + m * 48;")]
+
 # yl_bill_nb: staged entries read per group ahead of the billed group
 VARIANTS["nbu2"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 2")]
 VARIANTS["nbu8"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 8")]

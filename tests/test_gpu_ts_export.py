@@ -85,6 +85,28 @@ def test_ts_agent_independent_of_batch(engine):
         assert np.array_equal(full[k][j], one[k][0], equal_nan=True), k
 
 
+def test_ts_agent_outputs_with_and_without_planes(engine):
+    """The one dependence on the hourly flag: a TS sell-rate
+    agent's battery-case split is built by its own scan when planes are
+    requested and by k_batt_finance's plane pass otherwise, so the four
+    battery-case money outputs of those agents differ between the two calls by
+    the re-association of the split's sums (pinned here at 1e-9 relative);
+    the search, the sizing and every discrete decision are bit-identical, and
+    every other agent's outputs are the same bits."""
+    pop = _pop(800, seed=20260421)
+    ts = path_class(pop.cols) == 2
+    assert ts.sum() >= 40
+    on, _, _ = _size(engine, pop, hourly=True)
+    off, _, _ = _size(engine, pop, hourly=False)
+    for k in ("system_kw", "npv", "nfev", "tariff_final", "switched", "batt_kwh", "batt_kw", "payback_period",
+              "first_with", "first_without", "cash_flow", "status"):
+        assert np.array_equal(on[k], off[k], equal_nan=True), k
+    for k in BATT:
+        a, b = np.asarray(on[k], np.float64), np.asarray(off[k], np.float64)
+        assert np.array_equal(a[~ts], b[~ts], equal_nan=True), k
+        assert np.allclose(a[ts], b[ts], rtol=1e-9, atol=1e-9, equal_nan=True), k
+
+
 def test_combined_export_plane_bit_identical(engine):
     """dgen_export_plane's combined plane summed by dgen_state_hourly
     (planes_f32 = 3) gives the three-plane form's per-state rows bit for bit."""

@@ -1,0 +1,46 @@
+"""Engine._no_net_of (dgen_tables.no_net, ABI 12): a batch may run the
+demand-charge kernels without their net-billing paths only when no agent can
+reach a net-billing tariff -- initial tariff or any solar / storage rate-switch
+candidate.  Host logic only (no GPU)."""
+import numpy as np
+
+from dgen_amd.engine import Engine
+from dgen_amd.synth import make_population
+
+
+class _Host(Engine):
+    def __init__(self):          # no device: the batch logic only
+        pass
+
+
+def _eng(pop):
+    e = _Host()
+    e._tariff_mo = pop.tariffs["mo"].copy()
+    e._switch_tariff = pop.switches["tariff"].copy()
+    return e
+
+
+def test_demand_charge_population_has_no_net_agent():
+    pop = make_population("com_dc_batt", 3000)
+    assert np.isin(pop.tariffs["mo"], (2, 3)).any()       # the table holds CA net-billing variants
+    assert _eng(pop)._no_net_of(pop.cols, 3000)
+
+
+def test_net_billing_agents_are_seen():
+    pop = make_population("ca_res_storage", 3000)
+    assert not _eng(pop)._no_net_of(pop.cols, 3000)
+
+
+def test_switch_candidate_to_a_net_tariff_counts():
+    pop = make_population("com_dc_batt", 2000)
+    e = _eng(pop)
+    cols = {k: np.asarray(v).copy() for k, v in pop.cols.items()}
+    net_t = int(np.flatnonzero(np.isin(pop.tariffs["mo"], (2, 3)))[0])
+    # one agent gets a storage-switch candidate that lands on a net tariff
+    e._switch_tariff = np.concatenate([e._switch_tariff, [net_t]])
+    cols["sw_storage_off"][7] = e._switch_tariff.size - 1
+    cols["sw_storage_cnt"][7] = 1
+    assert not e._no_net_of(cols, 2000)
+    # an unknown switch table is conservative
+    e._switch_tariff = None
+    assert not e._no_net_of(pop.cols, 2000)
