@@ -4814,8 +4814,23 @@ k_state_hourly(const V* __restrict__ base, const V* __restrict__ pvo,
 // x cl6, the float32 roundings of ld and max(ld - pl, 0) -- so every term, and
 // the sums (k_state_hourly's tiled order), are the three-plane form's, bit for
 // bit, from 4 B of plane per agent-hour instead of 12 (or a re-run scan).
+// Per agent once per call: the two scalars every hour tile of the agent
+// needs (ls, cl6), so the tiles read one 16-B record instead of the
+// load_row -> shape_sum chain, status, x_last and three divisions each.
+__global__ void k_state_rows_prep(dgen_tables T, dgen_agents A, dgen_outputs O, int64_t n,
+                                  double2* __restrict__ scal) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const int lr = A.load_row[c];
+    const double ls = A.load_kwh[c] / T.shape_sum[lr];
+    const bool unsized = (O.status[c] & DGEN_ST_UNIT) != 0;
+    const double x_last = unsized ? 0.0 : O.x_last[c];
+    const double cl6 = (((x_last * 1000.0) * 0.96) / 1000.0) / 1e6;
+    scal[c] = make_double2(ls, cl6);
+}
+
 __global__ void __launch_bounds__(256)
-k_state_hourly_rows(dgen_tables T, dgen_agents A, dgen_outputs O, const float* __restrict__ wbt,
+k_state_hourly_rows(dgen_tables T, dgen_agents A, const double2* __restrict__ scal, const float* __restrict__ wbt,
                     const double* __restrict__ w_pvo, const double* __restrict__ w_batt,
                     const double* __restrict__ w_non, const int64_t* __restrict__ idx, int64_t n,
                     const int64_t* __restrict__ seg_off, int64_t n_seg, double* __restrict__ out) {
@@ -4832,10 +4847,8 @@ k_state_hourly_rows(dgen_tables T, dgen_agents A, dgen_outputs O, const float* _
         const int64_t c = idx ? idx[i] : i;
         const double a = w_pvo[c], b = w_batt[c], d = w_non[c];
         const int lr = A.load_row[c], cr = A.cf_row[c];
-        const double ls = A.load_kwh[c] / T.shape_sum[lr];
-        const bool unsized = (O.status[c] & DGEN_ST_UNIT) != 0;
-        const double x_last = unsized ? 0.0 : O.x_last[c];
-        const double cl6 = (((x_last * 1000.0) * 0.96) / 1000.0) / 1e6;
+        const double2 sc = scal[c];
+        const double ls = sc.x, cl6 = sc.y;                          // k_state_rows_prep
         const float* shp = T.shapes + (int64_t)lr * NH + h0;
         const int32_t* cfp = T.cfs + (int64_t)cr * NH + h0;
 #pragma unroll
@@ -5045,6 +5058,8 @@ struct dgen_ctx {
     int64_t count;
     void* dc_buf = nullptr;   // demand-charge envelopes, DCW_BYTES per agent (grown on demand)
     size_t dc_cap = 0;
+    void* rows_buf = nullptr; // dgen_state_hourly_rows' per-agent scalars, 16 B per agent (grown on demand)
+    size_t rows_cap = 0;
     void* dcr_buf = nullptr;  // battery-case demand records, DCR_BYTES per scratch slot (grown on demand)
     size_t dcr_cap = 0;
     int dcr_enable = DCR_CAP; // kept hours per record, 0 = off (dgen_set_dc_records)
@@ -5190,6 +5205,7 @@ int32_t dgen_close(dgen_ctx* c) {
     }
     if (c->dc_buf) (void)hipFree(c->dc_buf);
     if (c->dcr_buf) (void)hipFree(c->dcr_buf);
+    if (c->rows_buf) (void)hipFree(c->rows_buf);
     delete c;
     return DGEN_OK;
 }
@@ -5370,7 +5386,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // 21.38 -> 20.22 ms per step, k_batt_finance 3.54 -> 1.11 ms); without them
     // (the model-year loop's sizing call) the one-wave form's latency shows
     // (C5 2.5M: k_hourly_batt 56 -> 98 ms against k_batt_finance 47 -> 15 ms),
-    // and the plane pass stays
+    // and the plane pass stays; in the with-battery-plane call (WO) as well
+    // (round 5: 63 -> 102 ms against 46.5 -> 14.7 ms, profiles/r05/loop_ts_wo)
     const size_t lds_ts = lds + (size_t)(BLOCK / 64) * HB_DAY_BYTES;
     // (not in batches with the demand machinery at all: whether their agents
     // take this form must not depend on the demand records being on)
@@ -6010,8 +6027,22 @@ int32_t dgen_state_hourly_rows(dgen_ctx* c, const dgen_tables* T, const dgen_age
     }
     if (n_seg == 0) return DGEN_OK;
     HIP_TRY(hipSetDevice(c->device));
+    if ((size_t)n * sizeof(double2) > c->rows_cap) {        // per-agent scalars (grown on demand)
+        if (c->rows_buf) {
+            HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+            HIP_TRY(hipFree(c->rows_buf));
+        }
+        c->rows_buf = nullptr;
+        c->rows_cap = 0;
+        HIP_TRY(hipMalloc(&c->rows_buf, (size_t)(n > 0 ? n : 1) * sizeof(double2)));
+        c->rows_cap = (size_t)(n > 0 ? n : 1) * sizeof(double2);
+    }
+    double2* const scal = reinterpret_cast<double2*>(c->rows_buf);
+    if (n > 0)
+        hipLaunchKernelGGL(k_state_rows_prep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           *T, *A, *O, n, scal);
     const dim3 grid((unsigned)n_seg, (unsigned)((NH + SH_TILE - 1) / SH_TILE));
-    hipLaunchKernelGGL(k_state_hourly_rows, grid, dim3(256), 0, (hipStream_t)stream, *T, *A, *O, with_batt,
+    hipLaunchKernelGGL(k_state_hourly_rows, grid, dim3(256), 0, (hipStream_t)stream, *T, *A, scal, with_batt,
                        w_pvo, w_batt, w_non, idx, n, seg_off, n_seg, out);
     HIP_TRY(hipGetLastError());
     return DGEN_OK;
