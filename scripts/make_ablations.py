@@ -326,6 +326,10 @@ VARIANTS["bins_b12"] = [("        constexpr int BB = 8;\n        const double* l
 VARIANTS["bins_b24"] = [("        constexpr int BB = 8;\n        const double* lm = lslots + m * 48;",
                          "        constexpr int BB = 24;\n        const double* lm = lslots + m * 48;")]
 
+# k_dc_env at 2 waves per SIMD (no spills) instead of 3
+VARIANTS["dce_w2"] = [("__global__ void __launch_bounds__(WAVE * DCE_WPB) __attribute__((amdgpu_waves_per_eu(NQ <= 4 ? 3 : 2)))",
+                       "__global__ void __launch_bounds__(WAVE * DCE_WPB) __attribute__((amdgpu_waves_per_eu(2)))")]
+
 # yl_bill_nb: staged entries read per group ahead of the billed group
 VARIANTS["nbu2"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 2")]
 VARIANTS["nbu8"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 8")]
