@@ -1566,13 +1566,20 @@ constexpr int PK_SLOTS = 12;
 static_assert(sizeof(dgen_tariff) % sizeof(double) == 0, "tariff staging copies qwords");
 constexpr int TRF_QW = (int)(sizeof(dgen_tariff) / sizeof(double));
 
-__host__ __device__ inline size_t ylds_bytes(int half, int lpa, bool pk) {
+// LDS slots per lane: 4 half (the net-billing bill stages entries and month
+// sums after its 2 half accumulators); the bins-only (NEM) kernels use 2 half
+// (yl_bill_mo0's credits and billed kWh; the cash flow's two rows), and the
+// smaller layout lets k_batt_finance run a fourth wave per SIMD
+__host__ __device__ inline int ylds_slots(int half, bool slim) { return slim ? 2 * half : 4 * half; }
+
+__host__ __device__ inline size_t ylds_bytes(int half, int lpa, bool pk, bool slim = false) {
     const size_t trf = lpa < WAVE ? (size_t)(WAVE / lpa) * sizeof(dgen_tariff) : 0;
-    return trf + sizeof(double) * ((size_t)24 * half * (WAVE / lpa) + (size_t)(4 * half + (pk ? PK_SLOTS : 0)) * WAVE);
+    return trf + sizeof(double) * ((size_t)24 * half * (WAVE / lpa) +
+                                   (size_t)(ylds_slots(half, slim) + (pk ? PK_SLOTS : 0)) * WAVE);
 }
 
 template <int LPA>
-__device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>& g, bool pk) {
+__device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>& g, bool pk, bool slim = false) {
     YLds y;
     y.trf = nullptr;
     if (LPA < WAVE) {
@@ -1582,7 +1589,7 @@ __device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>
     y.L = base + (LPA == WAVE ? 0 : (g.lane / LPA) * 24 * half);
     y.G = y.L + 12 * half;
     y.lane = base + (WAVE / LPA) * 24 * half + g.lane;
-    y.pk = pk ? y.lane + 4 * half * WAVE : nullptr;
+    y.pk = pk ? y.lane + ylds_slots(half, slim) * WAVE : nullptr;
     y.half = half;
     return y;
 }
@@ -3793,7 +3800,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     YCtx<LPA> c(lane);
     const int sl = c.g.sl;
     c.y = sl + 1;
-    c.S = ylds_make(dyn_lds, half, c.g, PK && T.peak_units != 0);
+    c.S = ylds_make(dyn_lds, half, c.g, PK && T.peak_units != 0, !DC && !NET);
     c.tariffs = T.tariffs;
     c.dem_table = T.demand;
     c.n_dem = T.n_demand;
@@ -4265,7 +4272,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     const Seg<LPA> g(lane);
     const int y = g.sl + 1;
     const int half = lds_half(T.max_periods);
-    YLds S = ylds_make(dyn_lds, half, g, PK && T.peak_units != 0);
+    YLds S = ylds_make(dyn_lds, half, g, PK && T.peak_units != 0, !DC && !NET);
     WsLayout W = ws_layout(ws, n);
     const bool is_res = (A.flags[i] & 1) != 0;
     const bool is_ca = (A.flags[i] & 2) != 0;
@@ -5405,6 +5412,9 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     const bool pk = dc && T->peak_units != 0;       // kWh/kW tiers: the PK instantiations
     const int lpa_s = (fits32 && !(pk ? DGEN_NO2_SIZE_PK : dc ? DGEN_NO2_SIZE_DC : DGEN_NO2_SIZE)) ? 32 : WAVE;
     const int lpa_f = (fits32 && !(pk ? DGEN_NO2_FIN_PK : dc ? DGEN_NO2_FIN_DC : DGEN_NO2_FIN)) ? 32 : WAVE;
+    // the NEM-only (!dc, !net) instantiations' slimmer layout
+    const size_t ylds_s_nem = ylds_bytes(lds_half(T->max_periods), lpa_s, false, true);
+    const size_t ylds_f_nem = ylds_bytes(lds_half(T->max_periods), lpa_f, false, true);
     const size_t ylds_s = ylds_bytes(lds_half(T->max_periods), lpa_s, pk) +
                           (dc ? (size_t)(WAVE / lpa_s) * DCS_BYTES : 0);   // k_size's envelope stage
     // k_batt_finance's demand-charge instantiations stage hours per segment
@@ -5454,7 +5464,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_size_w<32, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
                                    n, i0, i1, nullptr, nbws, pre);
             else
-                hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_s, dim3(WAVE), ylds_s_nem, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws, pre);
 #endif
         } else if (lpa_s == 32 && !pk) {
@@ -5476,7 +5486,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_size_w<WAVE, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws, pre);
             else
-                hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_s, dim3(WAVE), ylds_s_nem, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws, pre);
         } else if (!pk) {
             if (dc_net)
@@ -5612,7 +5622,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_batt_finance_w<32, false, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
             else
-                hipLaunchKernelGGL((k_batt_finance_w<32, false, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                hipLaunchKernelGGL((k_batt_finance_w<32, false, false, false>), ygrid_f, dim3(WAVE), ylds_f_nem, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
 #endif
         } else if (lpa_f == 32 && !pk) {
@@ -5634,7 +5644,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
             else
-                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
+                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false, false>), ygrid_f, dim3(WAVE), ylds_f_nem, s2, *T,
                                    *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
         } else if (!pk) {
             if (dc_net)

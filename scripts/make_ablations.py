@@ -330,6 +330,10 @@ VARIANTS["bins_b24"] = [("        constexpr int BB = 8;\n        const double* l
 VARIANTS["dce_w2"] = [("__global__ void __launch_bounds__(WAVE * DCE_WPB) __attribute__((amdgpu_waves_per_eu(NQ <= 4 ? 3 : 2)))",
                        "__global__ void __launch_bounds__(WAVE * DCE_WPB) __attribute__((amdgpu_waves_per_eu(2)))")]
 
+# the NEM-only k_size at 4 waves per SIMD (128 VGPRs: spills) now that its
+# slimmer LDS layout would admit a fourth
+VARIANTS["ks_nem_w4"] = [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? 2 : (NET ? 3 : 4))")]
+
 # yl_bill_nb: staged entries read per group ahead of the billed group
 VARIANTS["nbu2"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 2")]
 VARIANTS["nbu8"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 8")]
