@@ -334,6 +334,17 @@ VARIANTS["dce_w2"] = [("__global__ void __launch_bounds__(WAVE * DCE_WPB) __attr
 # slimmer LDS layout would admit a fourth
 VARIANTS["ks_nem_w4"] = [("amdgpu_waves_per_eu(DC ? 2 : 3)", "amdgpu_waves_per_eu(DC ? 2 : (NET ? 3 : 4))")]
 
+# timing only (C3: mo 0, P <= PREG, so the NEM bills use no slot but the
+# cash flow's two): NEM-only kernels with 2 slots per lane, k_batt_finance's
+# NEM-only instantiation at 5 waves per SIMD -- C3 k_batt_finance 3.14 -> 3.14 /
+# 3.35 ms (profiles/r05/s29), not kept
+VARIANTS["kf_w5"] = [("__host__ __device__ inline int ylds_slots(int half, bool slim) { return slim ? 2 * half : 4 * half; }",
+                      "__host__ __device__ inline int ylds_slots(int half, bool slim) { return slim ? 2 : 4 * half; }"),
+                     ("template <int LPA, bool DC, bool NET, bool PK>\n__global__ void __launch_bounds__(WAVE)\nk_batt_finance_w(",
+                      "template <int LPA, bool DC, bool NET, bool PK>\n__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu((DC || NET) ? 1 : 5)))\nk_batt_finance_w(")]
+VARIANTS["kf_s2"] = [("__host__ __device__ inline int ylds_slots(int half, bool slim) { return slim ? 2 * half : 4 * half; }",
+                      "__host__ __device__ inline int ylds_slots(int half, bool slim) { return slim ? 2 : 4 * half; }")]
+
 # yl_bill_nb: staged entries read per group ahead of the billed group
 VARIANTS["nbu2"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 2")]
 VARIANTS["nbu8"] = [("#define DGEN_NB_U 4", "#define DGEN_NB_U 8")]
