@@ -191,3 +191,29 @@ def test_prebuilt_envelopes_kwh_per_kw_bit_identical(engine):
     for k in on:
         if on[k] is not None:
             assert np.array_equal(on[k], off[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("long_life", [False, True])
+def test_no_net_kernels_bit_identical(engine_dc, long_life):
+    """A demand-charge batch none of whose agents can bill net runs the
+    NET = false instantiations of k_size / k_batt_finance (dgen_tables.no_net,
+    set per batch); forcing the NET = true ones gives every output bit for bit
+    (the net-billing paths are unreachable for these agents)."""
+    pop = _pop(160, False, seed=17, long_life=long_life)
+    eng = engine_dc
+    eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    eng.set_tariffs(pop.tariffs, pop.demand)
+    eng.set_switches(pop.switches)
+    res = []
+    for no_net in (True, False):
+        batch = eng.upload_agents(pop.cols, pop.n_scratch)
+        assert batch.no_net                 # C4's table holds net variants no agent reaches
+        batch.no_net = no_net
+        out = eng.alloc_outputs(batch.n, hourly=True)
+        eng.size(batch, out)
+        torch.cuda.synchronize()
+        res.append(outputs_to_host(out))
+    a, b = res
+    for k in a:
+        if a[k] is not None:
+            assert np.array_equal(a[k], b[k], equal_nan=True), k
