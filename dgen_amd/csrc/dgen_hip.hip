@@ -1566,20 +1566,27 @@ constexpr int PK_SLOTS = 12;
 static_assert(sizeof(dgen_tariff) % sizeof(double) == 0, "tariff staging copies qwords");
 constexpr int TRF_QW = (int)(sizeof(dgen_tariff) / sizeof(double));
 
-// LDS slots per lane: 4 half (the net-billing bill stages entries and month
-// sums after its 2 half accumulators); the bins-only (NEM) kernels use 2 half
-// (yl_bill_mo0's credits and billed kWh; the cash flow's two rows), and the
-// smaller layout lets k_batt_finance run a fourth wave per SIMD
-__host__ __device__ inline int ylds_slots(int half, bool slim) { return slim ? 2 * half : 4 * half; }
+// LDS slots per lane (layout modes): YL_FULL 4 half (the net-billing bill
+// stages entries and month sums after its 2 half accumulators); YL_NEM 2 half
+// for the bins-only kernels (yl_bill_mo0's credits and billed kWh; the cash
+// flow's two rows); YL_DC max(2 half, DCP) for the demand-charge kernels
+// without net billing (the demand passes' per-period peaks).  The smaller
+// layouts let k_batt_finance run one more wave per SIMD.
+constexpr int YL_FULL = 0, YL_NEM = 1, YL_DC = 2;
+__host__ __device__ inline int ylds_slots(int half, int mode) {
+    return mode == YL_NEM ? 2 * half : mode == YL_DC ? (2 * half > DCP ? 2 * half : DCP) : 4 * half;
+}
+template <bool DC, bool NET>
+constexpr int yl_mode() { return NET ? YL_FULL : (DC ? YL_DC : YL_NEM); }
 
-__host__ __device__ inline size_t ylds_bytes(int half, int lpa, bool pk, bool slim = false) {
+__host__ __device__ inline size_t ylds_bytes(int half, int lpa, bool pk, int mode = YL_FULL) {
     const size_t trf = lpa < WAVE ? (size_t)(WAVE / lpa) * sizeof(dgen_tariff) : 0;
     return trf + sizeof(double) * ((size_t)24 * half * (WAVE / lpa) +
-                                   (size_t)(ylds_slots(half, slim) + (pk ? PK_SLOTS : 0)) * WAVE);
+                                   (size_t)(ylds_slots(half, mode) + (pk ? PK_SLOTS : 0)) * WAVE);
 }
 
 template <int LPA>
-__device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>& g, bool pk, bool slim = false) {
+__device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>& g, bool pk, int mode = YL_FULL) {
     YLds y;
     y.trf = nullptr;
     if (LPA < WAVE) {
@@ -1589,7 +1596,7 @@ __device__ __forceinline__ YLds ylds_make(double* base, int half, const Seg<LPA>
     y.L = base + (LPA == WAVE ? 0 : (g.lane / LPA) * 24 * half);
     y.G = y.L + 12 * half;
     y.lane = base + (WAVE / LPA) * 24 * half + g.lane;
-    y.pk = pk ? y.lane + ylds_slots(half, slim) * WAVE : nullptr;
+    y.pk = pk ? y.lane + ylds_slots(half, mode) * WAVE : nullptr;
     y.half = half;
     return y;
 }
@@ -3800,7 +3807,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     YCtx<LPA> c(lane);
     const int sl = c.g.sl;
     c.y = sl + 1;
-    c.S = ylds_make(dyn_lds, half, c.g, PK && T.peak_units != 0, !DC && !NET);
+    c.S = ylds_make(dyn_lds, half, c.g, PK && T.peak_units != 0, yl_mode<DC, NET>());
     c.tariffs = T.tariffs;
     c.dem_table = T.demand;
     c.n_dem = T.n_demand;
@@ -3822,7 +3829,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         }
         // the segment's envelope stage sits after the year-lane layout
         c.stg = reinterpret_cast<DcStage*>(reinterpret_cast<char*>(dyn_lds) +
-                                           ylds_bytes(half, LPA, PK && T.peak_units != 0)) + lane / LPA;
+                                           ylds_bytes(half, LPA, PK && T.peak_units != 0, yl_mode<DC, NET>())) + lane / LPA;
     }
     {
         const int slot = A.scratch_slot[i];
@@ -4272,7 +4279,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     const Seg<LPA> g(lane);
     const int y = g.sl + 1;
     const int half = lds_half(T.max_periods);
-    YLds S = ylds_make(dyn_lds, half, g, PK && T.peak_units != 0, !DC && !NET);
+    YLds S = ylds_make(dyn_lds, half, g, PK && T.peak_units != 0, yl_mode<DC, NET>());
     WsLayout W = ws_layout(ws, n);
     const bool is_res = (A.flags[i] & 1) != 0;
     const bool is_ca = (A.flags[i] & 2) != 0;
@@ -4299,7 +4306,7 @@ k_batt_finance_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int
     const dgen_demand* dem = pk13 ? tariff_peaks(T.demand, T.n_demand, t) : bill_dem;
     // the segment's LDS stage of the staged demand pass sits after the year-lane layout
     DemStage* const stage = reinterpret_cast<DemStage*>(reinterpret_cast<char*>(dyn_lds) +
-                                                        ylds_bytes(half, LPA, S.pk != nullptr)) + (lane / LPA);
+                                                        ylds_bytes(half, LPA, S.pk != nullptr, yl_mode<DC, NET>())) + (lane / LPA);
     YSrc src;
     {
         const int lr = A.load_row[i];
@@ -5413,8 +5420,13 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     const int lpa_s = (fits32 && !(pk ? DGEN_NO2_SIZE_PK : dc ? DGEN_NO2_SIZE_DC : DGEN_NO2_SIZE)) ? 32 : WAVE;
     const int lpa_f = (fits32 && !(pk ? DGEN_NO2_FIN_PK : dc ? DGEN_NO2_FIN_DC : DGEN_NO2_FIN)) ? 32 : WAVE;
     // the NEM-only (!dc, !net) instantiations' slimmer layout
-    const size_t ylds_s_nem = ylds_bytes(lds_half(T->max_periods), lpa_s, false, true);
-    const size_t ylds_f_nem = ylds_bytes(lds_half(T->max_periods), lpa_f, false, true);
+    const size_t ylds_s_nem = ylds_bytes(lds_half(T->max_periods), lpa_s, false, YL_NEM);
+    const size_t ylds_f_nem = ylds_bytes(lds_half(T->max_periods), lpa_f, false, YL_NEM);
+    // the demand-charge instantiations without net billing (no PK: those bill net)
+    const size_t ylds_s_dc = ylds_bytes(lds_half(T->max_periods), lpa_s, false, YL_DC) +
+                             (size_t)(WAVE / lpa_s) * DCS_BYTES;
+    const size_t ylds_f_dc = ylds_bytes(lds_half(T->max_periods), lpa_f, false, YL_DC) +
+                             (size_t)(WAVE / lpa_f) * DEM_STAGE_BYTES;
     const size_t ylds_s = ylds_bytes(lds_half(T->max_periods), lpa_s, pk) +
                           (dc ? (size_t)(WAVE / lpa_s) * DCS_BYTES : 0);   // k_size's envelope stage
     // k_batt_finance's demand-charge instantiations stage hours per segment
@@ -5473,7 +5485,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_size_w<32, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
             else
-                hipLaunchKernelGGL((k_size_w<32, true, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                hipLaunchKernelGGL((k_size_w<32, true, false, false>), ygrid_s, dim3(WAVE), ylds_s_dc, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
 #endif
         } else if (lpa_s == 32) {
@@ -5493,7 +5505,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_size_w<WAVE, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
             else
-                hipLaunchKernelGGL((k_size_w<WAVE, true, false, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                hipLaunchKernelGGL((k_size_w<WAVE, true, false, false>), ygrid_s, dim3(WAVE), ylds_s_dc, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
         } else {
             hipLaunchKernelGGL((k_size_w<WAVE, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
@@ -5631,7 +5643,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_batt_finance_w<32, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
             else
-                hipLaunchKernelGGL((k_batt_finance_w<32, true, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
+                hipLaunchKernelGGL((k_batt_finance_w<32, true, false, false>), ygrid_f, dim3(WAVE), ylds_f_dc, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
 #endif
         } else if (lpa_f == 32) {
@@ -5651,7 +5663,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                 hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
                                    *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
             else
-                hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, false, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
+                hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, false, false>), ygrid_f, dim3(WAVE), ylds_f_dc, s2, *T,
                                    *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
         } else {
             hipLaunchKernelGGL((k_batt_finance_w<WAVE, true, true, true>), ygrid_f, dim3(WAVE), ylds_f, s2, *T,
