@@ -5060,6 +5060,7 @@ struct dgen_ctx {
     int ts_scan;       // 1: the TS sell-rate agents' split built in their own scan (DGEN_TS_SCAN=0: off, A/B)
     int dc_pre;        // 1: the first-evaluation tariff's demand envelopes prebuilt by k_dc_env (DGEN_DC_PREBUILD=0: off)
     int nb_pre;        // 1: its net-billing split prebuilt by k_nb_env (DGEN_NB_PREBUILD=0: off, k_size builds it)
+    int64_t nem_hi;    // rows [0, nem_hi) of a batch hold no scratch-slot agent (dgen_set_nem_rows)
     int64_t ts_lo, ts_hi;   // the batch rows holding every TS-capable agent (dgen_set_ts_rows)
     int chunks;        // pipeline depth (dgen_set_pipeline)
     int hb_months;     // months per k_hourly_batt launch (dgen_set_hourly_segment)
@@ -5172,6 +5173,7 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     }
     c->ts_lo = 0;
     c->ts_hi = INT64_MAX;
+    c->nem_hi = 0;
     hipError_t e = hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking);
     for (int k = 0; k < dgen_ctx::MAXSPLIT - 1 && e == hipSuccess; k++) {
         e = hipStreamCreateWithFlags(&c->sx[k], hipStreamNonBlocking);
@@ -5447,10 +5449,13 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         HIP_TRY(hipEventRecord(e[0], s));
         // net-billing splits and demand envelopes of the initial tariffs
         // (counted in k_size's time)
-        if (nb_pre)
-            hipLaunchKernelGGL((k_nb_env<32>), dim3((unsigned)((m + 1) / 2)), dim3(WAVE),
-                               4 * WAVE * sizeof(double) + 2 * NBS_BYTES, s,
-                               *T, *A, i0, i1, nbws);
+        if (nb_pre) {
+            // its agents all hold a scratch slot: the bins-only prefix is skipped
+            const int64_t ja = (!dc && c->nem_hi > i0) ? (c->nem_hi < i1 ? c->nem_hi : i1) : i0;
+            if (i1 > ja)
+                hipLaunchKernelGGL((k_nb_env<32>), dim3((unsigned)((i1 - ja + 1) / 2)), dim3(WAVE),
+                                   4 * WAVE * sizeof(double) + 2 * NBS_BYTES, s, *T, *A, ja, i1, nbws);
+        }
         if (dc_pre) {
             const dim3 eg((unsigned)((m + DCE_WPB - 1) / DCE_WPB));
             if (dc_nq <= 2)
@@ -5470,12 +5475,22 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         // of the table bills net (dgen_tables.no_net; registers: C4 k_size
         // spills 412 -> 200 B per lane without them)
         const bool dc_net = T->no_net == 0;
+        // a net batch's leading rows without a scratch slot (dgen_set_nem_rows:
+        // bins-only agents, profile_order puts them first) run the bins-only
+        // instantiations: fewer registers and the slimmer LDS layout
+        const int64_t nm = (net && !dc && c->nem_hi > i0) ? (c->nem_hi < i1 ? c->nem_hi : i1) : i0;
+        const dim3 ygrid_sa((unsigned)((nm - i0 + WAVE / lpa_s - 1) / (WAVE / lpa_s)));
+        const dim3 ygrid_sb((unsigned)((i1 - nm + WAVE / lpa_s - 1) / (WAVE / lpa_s)));
         if (lpa_s == 32 && !dc) {
 #if !DGEN_NO2_SIZE
-            if (net)
-                hipLaunchKernelGGL((k_size_w<32, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O, c->cfg,
-                                   n, i0, i1, nullptr, nbws, pre);
-            else
+            if (net) {
+                if (nm > i0)
+                    hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_sa, dim3(WAVE), ylds_s_nem, s, *T, *A,
+                                       *O, c->cfg, n, i0, nm, nullptr, nbws, pre);
+                if (i1 > nm)
+                    hipLaunchKernelGGL((k_size_w<32, false, true, false>), ygrid_sb, dim3(WAVE), ylds_s, s, *T, *A, *O,
+                                       c->cfg, n, nm, i1, nullptr, nbws, pre);
+            } else
                 hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_s, dim3(WAVE), ylds_s_nem, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws, pre);
 #endif
@@ -5494,10 +5509,14 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                                c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
 #endif
         } else if (!dc) {
-            if (net)
-                hipLaunchKernelGGL((k_size_w<WAVE, false, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws, pre);
-            else
+            if (net) {
+                if (nm > i0)
+                    hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_sa, dim3(WAVE), ylds_s_nem, s, *T,
+                                       *A, *O, c->cfg, n, i0, nm, nullptr, nbws, pre);
+                if (i1 > nm)
+                    hipLaunchKernelGGL((k_size_w<WAVE, false, true, false>), ygrid_sb, dim3(WAVE), ylds_s, s, *T, *A,
+                                       *O, c->cfg, n, nm, i1, nullptr, nbws, pre);
+            } else
                 hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_s, dim3(WAVE), ylds_s_nem, s, *T, *A, *O,
                                    c->cfg, n, i0, i1, nullptr, nbws, pre);
         } else if (!pk) {
@@ -5626,14 +5645,20 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
 #undef DGEN_HB_LAUNCH_LOSS
         }
         HIP_TRY(hipEventRecord(e[3], s2));
+        const dim3 ygrid_fa((unsigned)((nm - i0 + WAVE / lpa_f - 1) / (WAVE / lpa_f)));
+        const dim3 ygrid_fb((unsigned)((i1 - nm + WAVE / lpa_f - 1) / (WAVE / lpa_f)));
         if (!c->battery) {
             // PV-only variant: no battery-case bill / cash flow
         } else if (lpa_f == 32 && !dc) {
 #if !DGEN_NO2_FIN
-            if (net)
-                hipLaunchKernelGGL((k_batt_finance_w<32, false, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
-            else
+            if (net) {
+                if (nm > i0)
+                    hipLaunchKernelGGL((k_batt_finance_w<32, false, false, false>), ygrid_fa, dim3(WAVE), ylds_f_nem, s2,
+                                       *T, *A, *O, c->cfg, n, ws, n_scratch, i0, nm, nbws, (int)nb_scan, dcr, dc_nq);
+                if (i1 > nm)
+                    hipLaunchKernelGGL((k_batt_finance_w<32, false, true, false>), ygrid_fb, dim3(WAVE), ylds_f, s2, *T,
+                                       *A, *O, c->cfg, n, ws, n_scratch, nm, i1, nbws, (int)nb_scan, dcr, dc_nq);
+            } else
                 hipLaunchKernelGGL((k_batt_finance_w<32, false, false, false>), ygrid_f, dim3(WAVE), ylds_f_nem, s2, *T, *A,
                                    *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
 #endif
@@ -5652,10 +5677,14 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
                                *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
 #endif
         } else if (!dc) {
-            if (net)
-                hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, true, false>), ygrid_f, dim3(WAVE), ylds_f, s2, *T, *A,
-                                   *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
-            else
+            if (net) {
+                if (nm > i0)
+                    hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false, false>), ygrid_fa, dim3(WAVE), ylds_f_nem,
+                                       s2, *T, *A, *O, c->cfg, n, ws, n_scratch, i0, nm, nbws, (int)nb_scan, dcr, dc_nq);
+                if (i1 > nm)
+                    hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, true, false>), ygrid_fb, dim3(WAVE), ylds_f, s2,
+                                       *T, *A, *O, c->cfg, n, ws, n_scratch, nm, i1, nbws, (int)nb_scan, dcr, dc_nq);
+            } else
                 hipLaunchKernelGGL((k_batt_finance_w<WAVE, false, false, false>), ygrid_f, dim3(WAVE), ylds_f_nem, s2, *T,
                                    *A, *O, c->cfg, n, ws, n_scratch, i0, i1, nbws, (int)nb_scan, dcr, dc_nq);
         } else if (!pk) {
@@ -5826,6 +5855,15 @@ int32_t dgen_set_ts_rows(dgen_ctx* c, int64_t lo, int64_t hi) {
     }
     c->ts_lo = lo;
     c->ts_hi = hi;
+    return DGEN_OK;
+}
+
+int32_t dgen_set_nem_rows(dgen_ctx* c, int64_t hi) {
+    if (!c || hi < 0) {
+        set_err("dgen_set_nem_rows: need hi >= 0");
+        return DGEN_E_ARG;
+    }
+    c->nem_hi = hi;
     return DGEN_OK;
 }
 

@@ -43,6 +43,8 @@ class AgentBatch:
     ts_rows: tuple = (0, 2 ** 62)
     # no agent can bill net hourly (dgen_tables.no_net, Engine._no_net_of)
     no_net: bool = False
+    # leading device rows without a scratch slot (dgen_set_nem_rows)
+    nem_rows: int = 0
 
 
 def path_class(cols: Dict[str, np.ndarray]) -> np.ndarray:
@@ -251,7 +253,24 @@ class Engine:
         ca.max_years = int(dev["econ_life"].max().item()) if n else 0
         return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order,
                           nb_scan=self._nb_scan_pays(cols, n, n_scratch), ts_rows=self._ts_rows_of(cols, n),
-                          no_net=self._no_net_of(cols, n))
+                          no_net=self._no_net_of(cols, n), nem_rows=self._nem_rows_of(cols, n))
+
+    def _nem_rows_of(self, cols, n: int) -> int:
+        """dgen_set_nem_rows: the length of the batch's leading run of device
+        rows without a scratch slot (bins-only agents; profile_order puts them
+        first), which a batch with scratch slots sizes with the bins-only
+        kernels.  0 when the columns are not host arrays or DGEN_NEM_SPLIT=0."""
+        import os
+        if os.environ.get("DGEN_NEM_SPLIT", "1") == "0":
+            return 0
+        try:
+            sl = np.asarray(cols["scratch_slot"])
+        except Exception:
+            return 0
+        if sl.ndim != 1 or sl.size != n:
+            return 0
+        has = np.flatnonzero(sl >= 0)
+        return int(has[0]) if has.size else n
 
     def _ts_rows_of(self, cols, n: int):
         """dgen_set_ts_rows: the device rows [lo, hi) holding every agent that
@@ -386,6 +405,9 @@ class Engine:
             _lib.check(self.lib.dgen_set_nb_scan(self.ctx, _lib.NB_CAPM if batch.nb_scan else 0),
                        "dgen_set_nb_scan")
             self._nb_scan = batch.nb_scan
+        if int(batch.nem_rows) != getattr(self, "_nem_rows", 0):
+            _lib.check(self.lib.dgen_set_nem_rows(self.ctx, int(batch.nem_rows)), "dgen_set_nem_rows")
+            self._nem_rows = int(batch.nem_rows)
         if tuple(batch.ts_rows) != getattr(self, "_ts_rows", (0, 2 ** 62)):
             _lib.check(self.lib.dgen_set_ts_rows(self.ctx, int(batch.ts_rows[0]), int(batch.ts_rows[1])),
                        "dgen_set_ts_rows")

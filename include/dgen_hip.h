@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 12
+#define DGEN_ABI_VERSION 13
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_DEFAULT_HOURLY_SPLIT 2   /* parts of a chunk's hourly scan, each on its own stream */
@@ -561,6 +561,18 @@ int32_t dgen_last_paths(dgen_ctx* ctx, int32_t* out, int32_t n_out);
  * kept lines are the same set either way and an evaluation takes their max,
  * so results are bit-identical (ABI 11).  Replaces nothing in the reference. */
 int32_t dgen_set_dc_prebuild(dgen_ctx* ctx, int32_t on);
+
+/* Rows [0, hi) of the next dgen_size_agents batches hold only agents without a
+ * scratch slot (scratch_slot < 0: bins-only billing, no net-billing or demand
+ * path; engine.profile_order puts them first).  A batch that has scratch slots
+ * then sizes those rows with the bins-only instantiations of k_size /
+ * k_batt_finance (fewer registers, slimmer LDS) and skips them in the split
+ * prebuild; results are bit-identical (the same bills on the same path).  0
+ * (default): the whole batch takes the batch's form.  A row in [0, hi) that
+ * does hold a scratch slot would be flagged DGEN_ST_SCRATCH, so the caller
+ * must only cover true bins-only rows (ABI 13).  Replaces nothing in the
+ * reference. */
+int32_t dgen_set_nem_rows(dgen_ctx* ctx, int64_t hi);
 
 /* Pipeline depth of dgen_size_agents: the batch is cut into `chunks` pieces;
  * k_size of piece j+1 runs on the caller's stream while k_hourly_batt and

@@ -145,6 +145,37 @@ def test_nb_prebuild_is_invisible(engine, cfg, n, monkeypatch):
         assert np.array_equal(a[k], b[k], equal_nan=True), k
 
 
+@pytest.mark.parametrize("cfg,n,long_life", [("national_mixed", 3000, False), ("national_mixed", 2000, True),
+                                             ("metering_mix", 2000, False)])
+def test_nem_rows_split_is_invisible(engine, cfg, n, long_life, monkeypatch):
+    """A batch with scratch slots sizes its leading bins-only rows (profile
+    order) with the bins-only kernels (dgen_set_nem_rows); every output equals
+    the whole batch on the net-billing kernels (DGEN_NEM_SPLIT=0), bit for bit."""
+    from dgen_amd.engine import profile_order
+    pop = _small_pop(cfg, n)
+    if long_life:
+        life = pop.cols["econ_life"].copy()
+        life[::4] = 33 + (np.arange(life[::4].size) % 18)
+        pop.cols["econ_life"] = life
+    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    engine.set_tariffs(pop.tariffs)
+    engine.set_switches(pop.switches)
+    res = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("DGEN_NEM_SPLIT", split)
+        batch = engine.upload_agents(pop.cols, pop.n_scratch, order=profile_order(pop.cols))
+        assert (batch.nem_rows > 0) == (split == "1")
+        out = engine.alloc_outputs(batch.n, hourly=True)
+        engine.size(batch, out)
+        torch.cuda.synchronize()
+        res.append(outputs_to_host(out, batch.perm))
+    a, b = res
+    for k in a:
+        if a[k] is None:
+            continue
+        assert np.array_equal(a[k], b[k], equal_nan=True), k
+
+
 @pytest.mark.parametrize("cfg,nb_scan", [("national_mixed", None), ("national_mixed", True),
                                          ("ca_res_storage", None)])
 def test_pipeline_depth_is_invisible(engine, cfg, nb_scan):

@@ -44,3 +44,16 @@ def test_switch_candidate_to_a_net_tariff_counts():
     # an unknown switch table is conservative
     e._switch_tariff = None
     assert not e._no_net_of(pop.cols, 2000)
+
+
+def test_nem_rows_are_the_leading_bins_only_run(monkeypatch):
+    from dgen_amd.engine import profile_order
+    pop = make_population("national_mixed", 3000)
+    order = profile_order(pop.cols)
+    cols = {k: np.asarray(v)[order] for k, v in pop.cols.items()}
+    e = _eng(pop)
+    k = e._nem_rows_of(cols, 3000)
+    sl = cols["scratch_slot"]
+    assert k > 0 and (sl[:k] < 0).all() and sl[k] >= 0
+    monkeypatch.setenv("DGEN_NEM_SPLIT", "0")
+    assert e._nem_rows_of(cols, 3000) == 0
