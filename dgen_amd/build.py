@@ -47,23 +47,56 @@ def needs_build() -> bool:
 GUARD = os.path.join(OUT_DIR, "build_guard.json")
 
 
+# The year-lane search kernels (k_size_w, k_dc_env, k_nb_env) build in a
+# translation unit of their own under the code generator's iterative
+# max-occupancy scheduler: k_size -4 % on C2 and C4 against the default
+# scheduler, which the hourly scan keeps (it is 1 % slower under the other;
+# DESIGN.md section 6, round 5).
+TUS = (("main", []), ("search", ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"]))
+
+
 def _compile(defines, verbose):
-    """One hipcc run in a scratch directory with -save-temps: the library and
-    the gfx950 assembly it was assembled from."""
+    """hipcc -c of each translation unit in a scratch directory with
+    -save-temps, then the link: the library and the gfx950 assembly of both
+    units (concatenated) it was assembled from."""
     work = tempfile.mkdtemp(prefix="dgen_build_")
     tmp = os.path.join(work, "libdgen_hip.so")
-    cmd = [hipcc(), *FLAGS, *[f"-D{d}=1" for d in defines], "-save-temps", "-o", tmp, SRC]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    res = subprocess.run(cmd, capture_output=True, text=True, cwd=work)
-    if res.returncode != 0:
+    cflags = [f for f in FLAGS if f != "-shared"]
+    objs, asms = [], []
+    try:
+        procs = []
+        for tu, extra in TUS:                          # the units compile side by side
+            d = os.path.join(work, tu)
+            os.makedirs(d)
+            obj = os.path.join(d, f"{tu}.o")
+            cmd = [hipcc(), *cflags, *extra, f"-DDGEN_TU_{tu.upper()}=1", *[f"-D{x}=1" for x in defines],
+                   "-save-temps", "-c", "-o", obj, SRC]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            procs.append((tu, d, obj, subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                                       text=True, cwd=d)))
+        for tu, d, obj, p in procs:
+            _, err = p.communicate()
+            if p.returncode != 0:
+                raise RuntimeError(f"hipcc failed on the {tu} unit ({p.returncode}):\n{err[-4000:]}")
+            asm = [f for f in os.listdir(d) if f.endswith(f"-hip-amdgcn-amd-amdhsa-{ARCH}.s")]
+            if not asm:
+                raise RuntimeError(f"hipcc -save-temps left no device assembly of the {tu} unit to check")
+            objs.append(obj)
+            asms.append(os.path.join(d, asm[0]))
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+        res = subprocess.run(cmd, capture_output=True, text=True, cwd=work)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed ({res.returncode}):\n{res.stderr[-4000:]}")
+        both = os.path.join(work, "device.s")
+        with open(both, "w") as out:
+            for a in asms:
+                with open(a) as f:
+                    shutil.copyfileobj(f, out)
+    except Exception:
         shutil.rmtree(work, ignore_errors=True)
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
-    asm = [f for f in os.listdir(work) if f.endswith(f"-hip-amdgcn-amd-amdhsa-{ARCH}.s")]
-    if not asm:
-        shutil.rmtree(work, ignore_errors=True)
-        raise RuntimeError("hipcc -save-temps left no device assembly to check")
-    return work, tmp, os.path.join(work, asm[0])
+        raise
+    return work, tmp, both
 
 
 def build(force: bool = False, verbose: bool = False) -> str:

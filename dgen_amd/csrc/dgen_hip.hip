@@ -3795,10 +3795,16 @@ __device__ __forceinline__ double yl_objective(YCtx<LPA>& c, double kw) {
 // the lanes keep the month peaks, which the demand pass computes ahead of the
 // energy bill; a separate instantiation so the other builds' registers are
 // untouched.
+}  // namespace
+namespace dgen_srch {
 template <int LPA, bool DC, bool NET, bool PK>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
-         void* dcws, char* nbws, int pre) {
+         void* dcws, char* nbws, int pre)
+#ifdef DGEN_TU_MAIN
+;
+#else
+{
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -3960,6 +3966,10 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
     PH_ADD(0, t_all, sl == 0);
     PH_CNT(9, nfev, sl == 0);
 }
+#endif
+}  // namespace dgen_srch
+namespace {
+using dgen_srch::k_size_w;
 
 // The tariff an agent bills its first Brent evaluation with: scipy's first
 // point a + golden_mean (b - a) (brent_bounded) through the solar rate switch
@@ -4014,9 +4024,15 @@ __device__ __forceinline__ void dce_first_max(double& v, int& h) {
     }
 }
 
+}  // namespace
+namespace dgen_srch {
 template <int NQ>
 __global__ void __launch_bounds__(WAVE * DCE_WPB) __attribute__((amdgpu_waves_per_eu(NQ <= 4 ? 3 : 2)))
-k_dc_env(dgen_tables T, dgen_agents A, dgen_cfg cfg, int64_t i0, int64_t i1, void* dcws) {
+k_dc_env(dgen_tables T, dgen_agents A, dgen_cfg cfg, int64_t i0, int64_t i1, void* dcws)
+#ifdef DGEN_TU_MAIN
+;
+#else
+{
     const int lane = threadIdx.x & (WAVE - 1);
     // the wave's agent: wave-uniform (readfirstlane), so its scalars and
     // addresses live in SGPRs
@@ -4210,15 +4226,25 @@ k_dc_env(dgen_tables T, dgen_agents A, dgen_cfg cfg, int64_t i0, int64_t i1, voi
     const bool bad = __ballot(!ok) != 0ull;
     if (lane == 0) *E.tag = bad ? -(t0 + 1) : t0 + 1;
 }
+#endif
+}  // namespace dgen_srch
+namespace {
+using dgen_srch::k_dc_env;
 
 // The PV-only search's net-billing split of every agent's first-evaluation
 // tariff (first_eval_tariff), built ahead of k_size on the same stream (yl_nb_build<false> over the same
 // range [tlo, thi]; k_size builds only for a tariff the rate switch moves to).
 // The build ran at k_size's occupancy with its registers; here it runs alone.
 // tag = 1 + the tariff (0: not built -- no slot, not billed net, or invalid).
+}  // namespace
+namespace dgen_srch {
 template <int LPA>
 __global__ void __launch_bounds__(WAVE)
-k_nb_env(dgen_tables T, dgen_agents A, int64_t i0, int64_t i1, char* nbws) {
+k_nb_env(dgen_tables T, dgen_agents A, int64_t i0, int64_t i1, char* nbws)
+#ifdef DGEN_TU_MAIN
+;
+#else
+{
     const int lane = threadIdx.x;
     const int64_t i = i0 + (int64_t)blockIdx.x * (WAVE / LPA) + (LPA == WAVE ? 0 : lane / LPA);
     if (i >= i1) return;
@@ -4264,6 +4290,10 @@ k_nb_env(dgen_tables T, dgen_agents A, int64_t i0, int64_t i1, char* nbws) {
     }
     if (g.sl == 0) nbr_tag(nbp) = tag;
 }
+#endif
+}  // namespace dgen_srch
+namespace {
+using dgen_srch::k_nb_env;
 
 // Battery-case Utilityrate5 + Cashloan (ff:178-288), lanes = years.
 template <int LPA, bool DC, bool NET, bool PK>
@@ -5034,6 +5064,41 @@ __global__ void k_finance_series(Series6 src, const int32_t* __restrict__ len, i
     out[t] = isfinite(v) ? v : 0.0;
 }
 }  // namespace
+
+// The year-lane search kernels (k_size_w, k_dc_env, k_nb_env) have external
+// linkage so that dgen_amd/build.py can compile them in a translation unit of
+// their own (DGEN_TU_SEARCH) with the code generator's scheduling options for
+// them, while this file's other kernels and the host API build as
+// DGEN_TU_MAIN, where the three are declarations only.  Without either macro
+// the file is one translation unit, as before (the ablation builds).
+#ifdef DGEN_TU_SEARCH
+namespace dgen_srch {
+#define DGEN_INST_SIZE(L, D, N, P)                                                                       \
+    template __global__ void k_size_w<L, D, N, P>(dgen_tables, dgen_agents, dgen_outputs, dgen_cfg,   \
+                                                  int64_t, int64_t, int64_t, void*, char*, int);
+#if !DGEN_NO2_SIZE
+DGEN_INST_SIZE(32, false, false, false)
+DGEN_INST_SIZE(32, false, true, false)
+#endif
+#if !DGEN_NO2_SIZE_DC
+DGEN_INST_SIZE(32, true, true, false)
+DGEN_INST_SIZE(32, true, false, false)
+#endif
+#if !DGEN_NO2_SIZE_PK
+DGEN_INST_SIZE(32, true, true, true)
+#endif
+DGEN_INST_SIZE(64, false, false, false)
+DGEN_INST_SIZE(64, false, true, false)
+DGEN_INST_SIZE(64, true, true, false)
+DGEN_INST_SIZE(64, true, false, false)
+DGEN_INST_SIZE(64, true, true, true)
+#undef DGEN_INST_SIZE
+template __global__ void k_dc_env<2>(dgen_tables, dgen_agents, dgen_cfg, int64_t, int64_t, void*);
+template __global__ void k_dc_env<4>(dgen_tables, dgen_agents, dgen_cfg, int64_t, int64_t, void*);
+template __global__ void k_dc_env<DGEN_DCP>(dgen_tables, dgen_agents, dgen_cfg, int64_t, int64_t, void*);
+template __global__ void k_nb_env<32>(dgen_tables, dgen_agents, int64_t, int64_t, char*);
+}  // namespace dgen_srch
+#else
 
 // ===========================================================================
 // C-ABI
@@ -6175,3 +6240,4 @@ int32_t dgen_finance_series(dgen_ctx* c, const dgen_outputs* O, const int32_t* l
 }
 
 }  // extern "C"
+#endif  // DGEN_TU_SEARCH

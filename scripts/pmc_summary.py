@@ -30,7 +30,7 @@ for d in glob.glob(pattern):
 disp = collections.defaultdict(set)       # (file, kernel) -> dispatch ids
 for f in files:
     for r in csv.DictReader(open(f)):
-        kn = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("<")[0]
+        kn = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("dgen_srch::", "").replace("void ", "").split("(")[0].split("<")[0]
         agg[(kn, r["Counter_Name"])].append(float(r["Counter_Value"]))
         disp[(f, kn)].add(r["Dispatch_Id"])
 # dispatches per sizing call, measured: a kernel's dispatches over k_size_w's
