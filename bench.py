@@ -289,6 +289,12 @@ def timed_region(step, steps: int, sync, dist_mod=None, device=None) -> float:
 
 def main():
     args = parse()
+    # --gpus N without torch.distributed.run: start N rank children before any
+    # GPU call (dgen_amd.launch); under torchrun, WORLD_SIZE must equal --gpus
+    from dgen_amd.launch import maybe_launch
+    st = maybe_launch(args.gpus, __file__, sys.argv[1:])
+    if st is not None:
+        sys.exit(st)
     ws, rank, local = dist_env()
     import torch
     import torch.distributed as dist
@@ -358,6 +364,9 @@ def main():
 
     st = out["status"].cpu().numpy()
     n_bad = int(((st & 0x3B) != 0).sum())
+    # agents the last timed call re-ran in the oracle's arithmetic (certified
+    # Brent paths, dgen_set_exact; their cost is inside k_size's time)
+    n_exact = eng.exact_count()
     total_agents = args.agents * ws * args.steps
     value = total_agents / el
 
@@ -449,7 +458,9 @@ def main():
                        "device_order": "caller" if args.caller_order else
                        ("profile (cf_row, load_row)" if args.order_major == "cf" else "profile (load_row, cf_row)"),
                        "parallelism": f"dp{ws} (agent shards, no collective in the step)",
-                       "agents_with_status_errors": n_bad},
+                       "agents_with_status_errors": n_bad,
+                       "certified_brent_paths": {"mode": int(eng.cfg.exact_brent),
+                                                 "exact_reruns_per_step": n_exact}},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -54,6 +54,12 @@ def main():
                     help="plan_partition tol: a rank cut snaps to a state boundary within this share of "
                          "the per-rank cost (0: cut inside states wherever balance puts the cut)")
     args = ap.parse_args()
+    # --gpus N without torch.distributed.run: start N rank children before any
+    # GPU call (dgen_amd.launch); under torchrun, WORLD_SIZE must equal --gpus
+    from dgen_amd.launch import maybe_launch
+    st = maybe_launch(args.gpus, __file__, sys.argv[1:])
+    if st is not None:
+        sys.exit(st)
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -57,7 +57,8 @@ class Tables(ctypes.Structure):
         ("n_shapes", _i64), ("n_cfs", _i64), ("n_wholesale", _i64), ("n_switches", _i64),
         ("n_tariffs", _i32), ("max_periods", _i32),
         ("demand", _vp), ("n_demand", _i32), ("peak_units", _i32),
-        ("max_dc_periods", _i32), ("no_net", _i32),
+        ("max_dc_periods", _i32), ("no_net", _i32), ("pad_t", _i32),
+        ("bt_tariff", _vp), ("bt_shape_max", _vp), ("bt_cf_max", _vp), ("bt_ts_max", _vp),
     ]
 
 
@@ -105,7 +106,7 @@ class DgenError(RuntimeError):
 
 _LIB: Optional[ctypes.CDLL] = None
 
-ABI_VERSION = 13   # include/dgen_hip.h DGEN_ABI_VERSION
+ABI_VERSION = 14   # include/dgen_hip.h DGEN_ABI_VERSION
 DEFAULT_CHUNKS = 1   # include/dgen_hip.h DGEN_DEFAULT_CHUNKS
 DEFAULT_HOURLY_MONTHS = 1   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_MONTHS
 DEFAULT_HOURLY_SPLIT = 2   # include/dgen_hip.h DGEN_DEFAULT_HOURLY_SPLIT
@@ -114,7 +115,7 @@ EXPORTED = [
     "dgen_abi_version", "dgen_last_error", "dgen_open", "dgen_close", "dgen_prep_shapes",
     "dgen_prep_cfs", "dgen_workspace_bytes", "dgen_size_agents", "dgen_brent_selftest",
     "dgen_kernel_times", "dgen_last_paths", "dgen_set_dc_prebuild", "dgen_segment_sums", "dgen_max_market_share", "dgen_diffusion",
-    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_set_ts_rows", "dgen_set_nem_rows", "dgen_set_dc_records", "dgen_hourly_planes", "dgen_export_plane", "dgen_state_hourly_rows", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
+    "dgen_set_pipeline", "dgen_set_hourly_segment", "dgen_set_battery", "dgen_set_nb_scan", "dgen_set_ts_rows", "dgen_set_nem_rows", "dgen_set_dc_records", "dgen_set_exact", "dgen_exact_count", "dgen_hourly_planes", "dgen_export_plane", "dgen_state_hourly_rows", "dgen_batt_attach", "dgen_export_weights", "dgen_state_hourly",
     "dgen_finance_series", "dgen_year_inputs", "dgen_initial_market_shares", "dgen_rows_seq_sum",
 ]
 
@@ -177,6 +178,10 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     L.dgen_set_nem_rows.argtypes = [_vp, _i64]
     L.dgen_set_dc_records.restype = _i32
     L.dgen_set_dc_records.argtypes = [_vp, _i32]
+    L.dgen_set_exact.restype = _i32
+    L.dgen_set_exact.argtypes = [_vp, _i32]
+    L.dgen_exact_count.restype = _i32
+    L.dgen_exact_count.argtypes = [_vp, ctypes.POINTER(ctypes.c_int64)]
     L.dgen_hourly_planes.restype = _i32
     L.dgen_hourly_planes.argtypes = L.dgen_size_agents.argtypes
     L.dgen_export_plane.restype = _i32

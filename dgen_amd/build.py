@@ -55,6 +55,52 @@ GUARD = os.path.join(OUT_DIR, "build_guard.json")
 TUS = (("main", []), ("search", ["-mllvm", "-amdgpu-sched-strategy=iterative-maxocc"]))
 
 
+# Developer cache of compiled units (outside the tree): a unit whose
+# preprocessed source (no line markers) and flags are unchanged reuses its
+# object and assembly -- an edit to the main unit's kernels does not recompile
+# the search unit.  DGEN_BUILD_CACHE=0 turns it off.
+CACHE_DIR = os.environ.get("DGEN_BUILD_CACHE_DIR", "/tmp/dgen_build_cache")
+
+
+def _unit_key(tu_flags):
+    import hashlib
+    if os.environ.get("DGEN_BUILD_CACHE", "1") == "0":
+        return None
+    try:
+        pp = subprocess.run([hipcc(), *tu_flags, "-E", "-P", SRC], capture_output=True, timeout=300)
+    except Exception:
+        return None
+    if pp.returncode != 0:
+        return None
+    h = hashlib.sha256(pp.stdout)
+    h.update(" ".join(tu_flags).encode())
+    return h.hexdigest()
+
+
+def _cache_get(key, d, obj):
+    if not key:
+        return False
+    src = os.path.join(CACHE_DIR, key)
+    o, a = os.path.join(src, "unit.o"), os.path.join(src, "unit.s")
+    if not (os.path.exists(o) and os.path.exists(a)):
+        return False
+    shutil.copyfile(o, obj)
+    shutil.copyfile(a, os.path.join(d, f"unit-hip-amdgcn-amd-amdhsa-{ARCH}.s"))
+    return True
+
+
+def _cache_put(key, obj, asm):
+    if not key:
+        return
+    try:
+        dst = os.path.join(CACHE_DIR, key)
+        os.makedirs(dst, exist_ok=True)
+        shutil.copyfile(obj, os.path.join(dst, "unit.o"))
+        shutil.copyfile(asm, os.path.join(dst, "unit.s"))
+    except OSError:
+        pass
+
+
 def _compile(defines, verbose):
     """hipcc -c of each translation unit in a scratch directory with
     -save-temps, then the link: the library and the gfx950 assembly of both
@@ -69,19 +115,29 @@ def _compile(defines, verbose):
             d = os.path.join(work, tu)
             os.makedirs(d)
             obj = os.path.join(d, f"{tu}.o")
-            cmd = [hipcc(), *cflags, *extra, f"-DDGEN_TU_{tu.upper()}=1", *[f"-D{x}=1" for x in defines],
-                   "-save-temps", "-c", "-o", obj, SRC]
+            tu_flags = [*cflags, *extra, f"-DDGEN_TU_{tu.upper()}=1", *[f"-D{x}=1" for x in defines]]
+            key = _unit_key(tu_flags)
+            hit = _cache_get(key, d, obj)
+            if hit:
+                if verbose:
+                    print(f"{tu} unit: unchanged (cached object)", flush=True)
+                procs.append((tu, d, obj, None, key))
+                continue
+            cmd = [hipcc(), *tu_flags, "-save-temps", "-c", "-o", obj, SRC]
             if verbose:
                 print(" ".join(cmd), flush=True)
             procs.append((tu, d, obj, subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                                                       text=True, cwd=d)))
-        for tu, d, obj, p in procs:
-            _, err = p.communicate()
-            if p.returncode != 0:
-                raise RuntimeError(f"hipcc failed on the {tu} unit ({p.returncode}):\n{err[-4000:]}")
+                                                       text=True, cwd=d), key))
+        for tu, d, obj, p, key in procs:
+            if p is not None:
+                _, err = p.communicate()
+                if p.returncode != 0:
+                    raise RuntimeError(f"hipcc failed on the {tu} unit ({p.returncode}):\n{err[-4000:]}")
             asm = [f for f in os.listdir(d) if f.endswith(f"-hip-amdgcn-amd-amdhsa-{ARCH}.s")]
             if not asm:
                 raise RuntimeError(f"hipcc -save-temps left no device assembly of the {tu} unit to check")
+            if p is not None:
+                _cache_put(key, obj, os.path.join(d, asm[0]))
             objs.append(obj)
             asms.append(os.path.join(d, asm[0]))
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]

@@ -48,13 +48,21 @@ class EngineConfig:
     # targets (SSC's BTM dispatcher keeps a monthly target, as we read its
     # source; parity unpinned); 0: every plan stands alone (default)
     batt_month_floor: int = 0
+    # certified Brent paths (dgen_set_exact, not a PySAM input): 1 re-runs in
+    # the reference's hour-order arithmetic every agent whose search a bound on
+    # the device / reference objective difference does not settle, so each
+    # agent takes the reference's Brent path; 2 re-runs every agent (tests); 0
+    # keeps the fast search alone
+    exact_brent: int = 1
 
     def to_c(self) -> _lib.Cfg:
         d = asdict(self)
+        d.pop("exact_brent")
         return _lib.Cfg(pad0=0, pad1=0, **d)
 
     def oracle_kwargs(self) -> dict:
         d = asdict(self)
         d.pop("skip_demand_charges")
         d.pop("force_net_billing")
+        d.pop("exact_brent")
         return d

@@ -330,9 +330,13 @@ __device__ __forceinline__ double np_sign(double v) {
 // objective is called from one site (the loop head), so the kernel carries one
 // inlined copy of it: scipy's first evaluation and its loop evaluations run
 // through the same call, the first one only seeding the state.
+// trace (optional, one lane per agent): the objective value of evaluation k
+// goes to trace[k] for k < BT_MAX -- the certified-path replay's input
+// (k_brent_certify), whose x's are this loop's, recomputed from these values
+constexpr int BT_MAX = 32;
 template <class Obj>
 __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, double xatol, int* nfev,
-                                double* x_last) {
+                                double* x_last, double* trace = nullptr) {
     const double sqrt_eps = 1.4832396974191326e-08;     // sqrt(2.2e-16)
     const double golden_mean = 0.3819660112501051;      // 0.5 * (3 - sqrt(5))
     double a = x1, b = x2;
@@ -345,6 +349,7 @@ __device__ __forceinline__ double brent_bounded(Obj&& f, double x1, double x2, d
     for (;;) {
         const double fu = f(x);
         *x_last = x;
+        if (trace && num < BT_MAX) trace[num] = fu;
         num += 1;
         if (num == 1) {
             fx = fu;
@@ -3800,7 +3805,7 @@ namespace dgen_srch {
 template <int LPA, bool DC, bool NET, bool PK>
 __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(DC ? 2 : 3)))
 k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, int64_t i0, int64_t i1,
-         void* dcws, char* nbws, int pre)
+         void* dcws, char* nbws, int pre, double* btrace)
 #ifdef DGEN_TU_MAIN
 ;
 #else
@@ -3931,7 +3936,7 @@ k_size_w(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t n, 
         [&](double x) __attribute__((always_inline)) {
             return yl_objective<LPA, DC, NET, PK>(c, x);
         },
-        low, high, xatol, &nfev, &x_last);
+        low, high, xatol, &nfev, &x_last, (btrace && sl == 0) ? btrace + i * BT_MAX : nullptr);
     const YLast& l = c.last;
     const YFlow& f = l.flow;
     const double w1 = c.g.bcast(l.w, 0);
@@ -5063,6 +5068,770 @@ __global__ void k_finance_series(Series6 src, const int32_t* __restrict__ len, i
     if (k < len[i]) v = src.p[c][i * stride + k];
     out[t] = isfinite(v) ? v : 0.0;
 }
+
+#ifndef DGEN_TU_SEARCH
+// ===========================================================================
+// Certified Brent paths (round 6).  k_size bills from re-associated sums (the
+// rows' slot sums, the net-billing split), so its objective differs from the
+// oracle's -- SSC's hour order -- by a few ulps, and scipy's parabolic step can
+// amplify such a difference into another Brent path.
+// Each search traces its objective values (brent_bounded's trace);
+// k_brent_certify replays the search from them with a bound on |device -
+// oracle| carried through every state variable, and lists the agents where a
+// decision is not certain under that bound; k_size_exact re-runs those
+// agents' searches in the oracle's own arithmetic (oracle/orc.c
+// perf_no_batt / orc_ur5 / orc_cashloan, op for op, hours in time order), so
+// every agent's Brent path, bills and NPV are the reference driver's.
+// ===========================================================================
+constexpr double BT_EPS = 2.220446049250313e-16;
+// error bound of one evaluation, in units of eps x the magnitude of the sums
+// it re-associates: a recursive sum of n terms errs by at most (n - 1) eps
+// times the sum of their magnitudes; the longest (month, period) bin holds 744
+// hours, and the slot / split forms add < 100 terms of their own
+constexpr double BT_GAMMA = 2048.0;
+
+struct BtModel {
+    double c0, c1, ce;   // |f_device - f_oracle| <= c0 + c1 x + ce |f| at the same x
+    double lip;          // |f(x) - f(x')| <= lip |x - x'| between rate switches
+};
+
+// bound of an operation's result: exact inputs give bit-identical results on
+// both sides; inexact ones add one rounding of the result
+__device__ __forceinline__ double bt_rnd(double d, double v) { return d > 0.0 ? d + BT_EPS * fabs(v) : 0.0; }
+
+// is the comparison of u and v (bounds du, dv) decided the same way on both sides?
+__device__ __forceinline__ bool bt_sure(double u, double du, double v, double dv) {
+    const double s = du + dv;
+    return s == 0.0 || fabs(u - v) > s;
+}
+// equality of two Brent points: the same evaluation's x is equal on both sides
+__device__ __forceinline__ bool bt_sure_eq(double u, double du, int pu, double v, double dv, int pv) {
+    return pu == pv || bt_sure(u, du, v, dv);
+}
+
+// brent_bounded replayed from its traced objective values with bounds: true
+// when every decision (comparisons, branch tests, the rate switch's
+// thresholds, the final x's to 1e-10) is the oracle's under the model M.
+// The values follow brent_bounded's operations exactly (same x's).
+__device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, double x2, double xatol,
+                          const BtModel& M, const dgen_switch* sw, int sw_cnt) {
+    const double sqrt_eps = 1.4832396974191326e-08;
+    const double golden_mean = 0.3819660112501051;
+    double a = x1, b = x2, da = 0.0, db = 0.0;
+    double fulc = a + golden_mean * (b - a);
+    double nfc = fulc, xf = fulc;
+    double dfulc = 0.0, dnfc = 0.0, dxf = 0.0;
+    int pfulc = 0, pnfc = 0, pxf = 0;             // evaluation each point came from
+    double rat = 0.0, e = 0.0, drat = 0.0, de = 0.0;
+    double x = xf, dx = 0.0, dx_last = 0.0;
+    double fx = 0.0, ffulc = 0.0, fnfc = 0.0, dfx = 0.0, dffulc = 0.0, dfnfc = 0.0;
+    int num = 0;
+    for (;;) {
+        if (num >= nfev || num >= BT_MAX) return false;
+        // the evaluation at x: the sticky solar switch's row test must agree
+        if (!bt_sure(x, dx, 0.0, 0.0)) return false;
+        for (int r = 0; r < sw_cnt; r++)
+            if (!bt_sure(x, dx, sw[r].min_kw, 0.0) || !bt_sure(x, dx, sw[r].max_kw, 0.0)) return false;
+        const double fu = f[num];
+        const double dfu = M.c0 + M.c1 * fabs(x) + M.ce * fabs(fu) + M.lip * dx;
+        const int px = num;
+        dx_last = dx;
+        num += 1;
+        if (num == 1) {
+            fx = fu; ffulc = fu; fnfc = fu;
+            dfx = dfu; dffulc = dfu; dfnfc = dfu;
+        } else {
+            if (!bt_sure(fu, dfu, fx, dfx)) return false;
+            if (!bt_sure(x, dx, xf, dxf)) return false;
+            if (fu <= fx) {
+                if (x >= xf) { a = xf; da = dxf; } else { b = xf; db = dxf; }
+                fulc = nfc; dfulc = dnfc; pfulc = pnfc; ffulc = fnfc; dffulc = dfnfc;
+                nfc = xf; dnfc = dxf; pnfc = pxf; fnfc = fx; dfnfc = dfx;
+                xf = x; dxf = dx; pxf = px; fx = fu; dfx = dfu;
+            } else {
+                if (x < xf) { a = x; da = dx; } else { b = x; db = dx; }
+                // (fu <= fnfc) || (nfc == xf): decided when both tests are, or
+                // when a decided test settles the ||
+                const bool ca = bt_sure(fu, dfu, fnfc, dfnfc), ra = fu <= fnfc;
+                const bool cb = bt_sure_eq(nfc, dnfc, pnfc, xf, dxf, pxf), rb = nfc == xf;
+                if (!((ca && cb) || (ca && ra) || (cb && rb))) return false;
+                if (ra || rb) {
+                    fulc = nfc; dfulc = dnfc; pfulc = pnfc; ffulc = fnfc; dffulc = dfnfc;
+                    nfc = x; dnfc = dx; pnfc = px; fnfc = fu; dfnfc = dfu;
+                } else {
+                    const bool cc = bt_sure(fu, dfu, ffulc, dffulc), rc = fu <= ffulc;
+                    const bool cd = bt_sure_eq(fulc, dfulc, pfulc, xf, dxf, pxf), rd = fulc == xf;
+                    const bool ce = bt_sure_eq(fulc, dfulc, pfulc, nfc, dnfc, pnfc), re = fulc == nfc;
+                    const bool any_true = (cc && rc) || (cd && rd) || (ce && re);
+                    if (!any_true && !(cc && cd && ce)) return false;
+                    if (rc || rd || re) { fulc = x; dfulc = dx; pfulc = px; ffulc = fu; dffulc = dfu; }
+                }
+            }
+        }
+        const double xm = 0.5 * (a + b);
+        const double dxm = bt_rnd(0.5 * (da + db), xm);
+        const double tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+        const double dtol1 = bt_rnd(sqrt_eps * dxf, tol1);
+        const double tol2 = 2.0 * tol1, dtol2 = 2.0 * dtol1;
+        if (num >= 500) break;
+        {
+            const double lhs = fabs(xf - xm), rhs = tol2 - 0.5 * (b - a);
+            const double dl = bt_rnd(dxf + dxm, lhs), dr = bt_rnd(dtol2 + 0.5 * (da + db), rhs);
+            if (!bt_sure(lhs, dl, rhs, dr)) return false;
+            if (!(lhs > rhs)) break;
+        }
+        bool golden = true, rat_tol = false;
+        if (!bt_sure(fabs(e), de, tol1, dtol1)) return false;
+        if (fabs(e) > tol1) {
+            golden = false;
+            const bool s1 = pxf == pnfc, s2 = pxf == pfulc;     // exact zero differences
+            const double u1 = xf - nfc, du1 = s1 ? 0.0 : bt_rnd(dxf + dnfc, u1);
+            const double u2 = xf - fulc, du2 = s2 ? 0.0 : bt_rnd(dxf + dfulc, u2);
+            const double v1 = fx - ffulc, dv1 = s2 ? 0.0 : bt_rnd(dfx + dffulc, v1);
+            const double v2 = fx - fnfc, dv2 = s1 ? 0.0 : bt_rnd(dfx + dfnfc, v2);
+            double r = u1 * v1;
+            const double dr = bt_rnd(fabs(u1) * dv1 + fabs(v1) * du1 + du1 * dv1, r);
+            double q = u2 * v2;
+            double dq = bt_rnd(fabs(u2) * dv2 + fabs(v2) * du2 + du2 * dv2, q);
+            const double t1 = u2 * q, t2 = u1 * r;
+            const double dt1 = bt_rnd(fabs(u2) * dq + fabs(q) * du2 + du2 * dq, t1);
+            const double dt2 = bt_rnd(fabs(u1) * dr + fabs(r) * du1 + du1 * dr, t2);
+            double p = t1 - t2;
+            double dp = bt_rnd(dt1 + dt2, p);
+            q = 2.0 * (q - r);
+            dq = bt_rnd(2.0 * (dq + dr), q);
+            if (pnfc == pfulc) { dp = 0.0; dq = 0.0; }       // the same point twice: r == q, p == 0
+            const double r2 = e, dr2 = de;
+            e = rat; de = drat;
+            // (fabs(p) < fabs(0.5 q r)) && (p > q (a - xf)) && (p < q (b - xf)),
+            // after p = -p when q > 0 and q = |q|
+            const double aq = fabs(q);
+            const double c1l = fabs(p), c1r = fabs(0.5 * aq * r2);
+            const double dc1r = bt_rnd(0.5 * (aq * dr2 + fabs(r2) * dq + dq * dr2), c1r);
+            if (!bt_sure(c1l, dp, c1r, dc1r)) return false;
+            bool para = false;
+            if (c1l < c1r) {
+                if (!bt_sure(q, dq, 0.0, 0.0)) return false;
+                p = q > 0.0 ? -p : p;
+                const double ta = aq * (a - xf), dta = bt_rnd(aq * (da + dxf) + fabs(a - xf) * dq + dq * (da + dxf), ta);
+                if (!bt_sure(p, dp, ta, dta)) return false;
+                if (p > ta) {
+                    const double tb = aq * (b - xf), dtb = bt_rnd(aq * (db + dxf) + fabs(b - xf) * dq + dq * (db + dxf), tb);
+                    if (!bt_sure(p, dp, tb, dtb)) return false;
+                    para = p < tb;
+                }
+            } else if (q > 0.0) {
+                p = -p;
+            }
+            q = aq;
+            if (para) {
+                rat = (p + 0.0) / q;
+                // |p'/q' - p/q| <= (dp + |p/q| dq) / (|q| - dq), |q| > dq above
+                drat = bt_rnd((dp + fabs(rat) * dq) / (q - dq), rat);
+                x = xf + rat;
+                dx = bt_rnd(dxf + drat, x);
+                // ((x - a) < tol2) || ((b - x) < tol2)
+                const double xa = x - a, dxa = bt_rnd(dx + da, xa);
+                const double bx = b - x, dbx = bt_rnd(db + dx, bx);
+                const bool c1 = bt_sure(xa, dxa, tol2, dtol2), r1 = xa < tol2;
+                const bool c2 = bt_sure(bx, dbx, tol2, dtol2), r2b = bx < tol2;
+                if (!((c1 && c2) || (c1 && r1) || (c2 && r2b))) return false;
+                if (r1 || r2b) {
+                    const double dm = xm - xf, ddm = bt_rnd(dxm + dxf, dm);
+                    if (!bt_sure(dm, ddm, 0.0, 0.0)) return false;
+                    const double si = np_sign(dm) + ((dm == 0.0) ? 1.0 : 0.0);
+                    rat = tol1 * si;
+                    drat = dtol1;
+                    rat_tol = true;                   // |rat| == tol1 on both sides
+                }
+            } else {
+                golden = true;
+            }
+        }
+        if (golden) {
+            if (!bt_sure(xf, dxf, xm, dxm)) return false;
+            if (xf >= xm) { e = a - xf; de = bt_rnd(da + dxf, e); }
+            else { e = b - xf; de = bt_rnd(db + dxf, e); }
+            rat = golden_mean * e;
+            drat = bt_rnd(golden_mean * de, rat);
+        }
+        if (!bt_sure(rat, drat, 0.0, 0.0)) return false;
+        const double si = np_sign(rat) + ((rat == 0.0) ? 1.0 : 0.0);
+        const double ar = fabs(rat);
+        if (!rat_tol && !bt_sure(ar, drat, tol1, dtol1)) return false;
+        const bool big = ar > tol1;
+        x = xf + si * (big ? ar : tol1);
+        dx = bt_rnd(dxf + (big ? drat : dtol1), x);
+    }
+    if (num != nfev) return false;
+    // the reported x's (system_kw = xf, x_last) within 1e-10 of the oracle's
+    if (dxf > 1e-10 * fmax(1.0, fabs(xf)) || dx_last > 1e-10 * fmax(1.0, fabs(x))) return false;
+    return true;
+}
+
+// Price bounds of the tariffs an agent's search can bill with (its initial
+// tariff and every solar switch row): energy ($/kWh: buy, sell, the true-up
+// rate, the TS sell rate), demand ($/kW a month) and the kWh/kW tier caps'
+// sensitivity to the month peak.  From dgen_tables.bt_tariff (3 per tariff,
+// Engine.set_tariffs) when present, else from the records.
+__device__ void bt_prices(const dgen_tables& T, const dgen_cfg& cfg, int tix, double& pm, double& pmdc, double& pku,
+                          bool& mo2) {
+    const dgen_tariff& t = T.tariffs[tix];
+    mo2 = mo2 || t.mo == 2;
+    if (T.bt_tariff) {
+        pm = fmax(pm, T.bt_tariff[3 * tix]);
+        pmdc = fmax(pmdc, cfg.skip_demand_charges == 0 ? T.bt_tariff[3 * tix + 1] : 0.0);
+        pku = fmax(pku, T.bt_tariff[3 * tix + 2]);
+        return;
+    }
+    double e = 0.0, cap = 0.0;
+    for (int p = 0; p < t.P && p < MAXP; p++)
+        for (int k = 0; k < t.T && k < MAXT; k++) e = fmax(e, fmax(fabs(t.buy[p][k]), fabs(t.sell[p][k])));
+    for (int k = 0; k < t.T && k < MAXT; k++) cap += fabs(t.cap[k]);
+    pm = fmax(pm, e);
+    if (t.unit == 1 || t.unit == 3) pku = fmax(pku, 2.0 * e * cap * (t.unit == 3 ? 31.0 : 1.0));
+    if (cfg.skip_demand_charges == 0 && t.dc > 0) pmdc = INFINITY;   // no bound without the table
+}
+
+// One thread per agent: replay its traced search, list it when not certain.
+// list[0] counts the chunk's listed agents, list[1 ..] their rows.
+__global__ void __launch_bounds__(256)
+k_brent_certify(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int64_t i0, int64_t i1,
+                const double* __restrict__ trace, int32_t* list, int mode) {
+    const int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool flag = false;
+    if (i < i1) {
+        const int nfev = O.nfev[i];
+        const int st = O.status[i];
+        if (nfev > 0 && !(st & (DGEN_ST_BOUNDS | DGEN_ST_TARIFF | DGEN_ST_UNIT | DGEN_ST_YEARS))) {
+            flag = true;
+            if (mode == 1 && nfev <= BT_MAX) {
+                const int N = A.econ_life[i];
+                const double kwh = A.load_kwh[i];
+                const int lr = A.load_row[i], cr = A.cf_row[i];
+                const double naep0 = T.cf_naep[cr];
+                const double max_load = kwh / naep0;               // k_size's bracket
+                const double low = max_load * 0.8, high = max_load * 1.25;
+                const double span = high - low;
+                const double tl = (span > 1.0 ? span : 1.0) * 1e-3;
+                const double fl_tl = floor(tl);
+                const double xatol = fl_tl < 2.0 ? 2.0 : fl_tl;
+                // prices of every tariff the search can bill with
+                double pm = fabs(cfg.nm_yearend_sell_rate), pmdc = 0.0, pku = 0.0, otc = 0.0;
+                bool mo2 = false;
+                const int t0 = A.tariff0[i];
+                bt_prices(T, cfg, t0, pm, pmdc, pku, mo2);
+                const dgen_switch* sw = T.switches + A.sw_solar_off[i];
+                const int sw_cnt = A.sw_solar_cnt[i];
+                bool ok = true;
+                for (int r = 0; r < sw_cnt; r++) {
+                    const int tt = sw[r].tariff;
+                    if (tt < 0 || tt >= T.n_tariffs) { ok = false; break; }
+                    bt_prices(T, cfg, tt, pm, pmdc, pku, mo2);
+                    otc = fmax(otc, fabs(sw[r].one_time_charge));
+                }
+                const bool is_ca = (A.flags[i] & 2) != 0;
+                const int wr = A.wholesale_row[i];
+                if (mo2 && !is_ca && wr >= 0 && T.wholesale) {
+                    if (!T.bt_ts_max) ok = false;
+                    else pm = fmax(pm, T.bt_ts_max[wr] * fabs(A.price_mult[i]) * (1.0 + 1e-6));
+                }
+                // discounted escalation over the analysis period, D = sum_y rr^y
+                // (1 + infl + esc)^(y - 1), and the largest degradation factor
+                const double infl = A.inflation[i], real = A.real_discount[i];
+                const double rr = 1.0 / ((1.0 + real) * (1.0 + infl));
+                const double rb = fabs(1.0 + infl + A.escalator[i]);
+                const double sb = fabs(1.0 - A.pv_deg[i]);
+                double D = 0.0, dr = 1.0, er = 1.0, smax = 1.0, sy = 1.0;
+                for (int y = 1; y <= N && y <= MAXY; y++) {
+                    dr *= rr;
+                    D += dr * er;
+                    er *= rb;
+                    smax = fmax(smax, sy);
+                    sy *= sb;
+                }
+                D *= 1.01;
+                // peak load (kW) and per-kW generation of the agent's rows
+                const double S = T.shape_sum[lr];
+                const double lmax = T.bt_shape_max ? T.bt_shape_max[lr] * fabs(kwh / S) : INFINITY;
+                const double gmax = T.bt_cf_max ? T.bt_cf_max[cr] * 1e-6 : INFINITY;
+                const double capc = fabs(A.capex[i] * A.ccm[i]);
+                const double dem = pmdc + pku;                    // $/kW a month of peak
+                const double g = BT_GAMMA * BT_EPS;
+                BtModel M;
+                // bills: 4 x price x (load + generation) per year, demand: 12
+                // months x price x (peak load + generation at the peak hour)
+                M.c0 = g * (4.0 * D * (pm * 2.0 * fabs(kwh) + (dem > 0.0 ? dem * 24.0 * lmax : 0.0)) + otc);
+                M.c1 = g * (4.0 * D * smax * 0.96 * (pm * fabs(naep0) + (dem > 0.0 ? dem * 12.0 * gmax : 0.0)) + 4.0 * capc);
+                M.ce = g;
+                M.lip = 4.0 * capc + 4.0 * D * smax * 0.96 * (pm * fabs(naep0) + (dem > 0.0 ? dem * 12.0 * gmax : 0.0));
+                if (ok && isfinite(M.c0) && isfinite(M.c1) && isfinite(M.lip) && isfinite(xatol))
+                    flag = !bt_replay(trace + i * BT_MAX, nfev, low, high, xatol, M, sw, sw_cnt);
+            }
+        }
+    }
+    // compact the wave's listed agents (one counter add per wave)
+    const unsigned long long m = __ballot(flag);
+    const int lane = threadIdx.x & (WAVE - 1);
+    int base = 0;
+    if (m) {
+        const int lead = __ffsll((long long)m) - 1;
+        if (lane == lead) base = atomicAdd(list, __popcll(m));
+        base = __shfl(base, lead, WAVE);
+        if (flag) list[1 + base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_size_exact: the listed agents' searches in the oracle's arithmetic.  One
+// block per agent at a time (the blocks stride over the list): threads =
+// (month, year) cells of a block of YB analysis years (month-major, so a
+// wave's lanes read two months' hours), each summing its month's hours in
+// time order (oracle bin_year); then one thread per year bills its months in
+// order (year_bill, year_demand) and thread 0 runs the cash flow
+// (orc_cashloan).  Hour data live in the block's global scratch (load, this
+// evaluation's generation, TS sell rate), handed between lanes with a
+// vmcnt(0) wait, a barrier and an agent-scope acquire (L1 dropped).
+// ---------------------------------------------------------------------------
+constexpr int EX_THREADS = 384;                 // 12 months x 32 years
+constexpr int EX_BLOCKS = 1024;
+constexpr size_t EX_WS_DOUBLES = (size_t)3 * NH;
+
+__device__ __forceinline__ void ex_handoff() {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__device__ __forceinline__ double ex_month_charge(const dgen_tariff& t, int m, const double* u, double peak) {
+    double U = 0.0;
+    for (int p = 0; p < t.P; p++) U += u[p];
+    if (!(U > 0.0)) return 0.0;
+    if (t.T == 1) {
+        double charge = 0.0;
+        for (int p = 0; p < t.P; p++) charge += u[p] * t.buy[p][0];
+        return charge;
+    }
+    const double days = (double)c_days_in_month[m];
+    const double scale = (t.unit == 2) ? days : (t.unit == 1) ? peak : (t.unit == 3) ? peak * days : 1.0;
+    double charge = 0.0, prev = 0.0;
+    for (int k = 0; k < t.T; k++) {
+        const double hi = (k == t.T - 1) ? INFINITY : t.cap[k] * scale;
+        const double top = U < hi ? U : hi;
+        double amt = top - prev;
+        if (amt < 0.0) amt = 0.0;
+        if (hi > prev) prev = hi;
+        for (int p = 0; p < t.P; p++) charge += (u[p] / U) * amt * t.buy[p][k];
+    }
+    return charge;
+}
+
+__device__ __forceinline__ double ex_dc_tier(double peak, const double* cap, const double* price, int nt) {
+    double charge = 0.0, prev = 0.0;
+    for (int k = 0; k < nt; k++) {
+        const double hi = (k == nt - 1) ? INFINITY : cap[k];
+        const double top = peak < hi ? peak : hi;
+        double amt = top - prev;
+        if (amt < 0.0) amt = 0.0;
+        if (hi > prev) prev = hi;
+        charge += amt * price[k];
+    }
+    return charge;
+}
+
+struct ExLds {         // dynamic LDS of k_size_exact
+    double* bins;      // [cells][2 P]: mo 0/1 net | mo 4 load, gen | mo 2/3 import, export ($ with TS)
+    double* peak;      // [cells] the month's largest import (units 1 / 3)
+    double* dcv;       // [cells][1 + DCP] flat and TOU demand peaks (billed demand only)
+    double* yr;        // [YB][2 MAXP] per-year-thread credit / billed kWh
+    double* res;       // [6][MAXY + 1] aev, bill_w, bill_wo, cf_payback, cf_energy_value, atcf; + 8 scalars
+};
+
+__host__ __device__ inline size_t ex_lds_bytes(int P, int yb, bool dcb) {
+    const size_t cells = (size_t)12 * yb;
+    return sizeof(double) * (cells * (2 * (size_t)P + 1 + (dcb ? 1 + DCP : 0)) + (size_t)yb * 2 * MAXP +
+                             6 * (size_t)(MAXY + 1) + 8);
+}
+
+struct ExAgent {
+    const dgen_tariff* tariffs;
+    const dgen_demand* demand;
+    int n_demand;
+    bool dc_on;
+    const double* Lh;
+    double* Gh;
+    const double* TSh;
+    bool has_ts;
+    int N, P, yb;
+    double rate_base, sys_base, yearend;
+};
+
+// the (month, year) cells of years [y0, y0 + yb): oracle bin_year for month m
+// of year y (generation x s_y; gen == false: the no-system bins)
+__device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int y0, bool gen,
+                         const ExLds& L) {
+    const int P = t.P;
+    const int cells = 12 * a.yb;
+    for (int c = threadIdx.x; c < cells; c += blockDim.x) {
+        const int m = c / a.yb, y = y0 + c % a.yb;
+        if (y >= (gen ? a.N : 1)) continue;
+        const double s = pow_seq(a.sys_base, y);
+        double* bn = L.bins + (size_t)c * 2 * P;
+        for (int k = 0; k < 2 * P; k++) bn[k] = 0.0;
+        double peak = 0.0, flat = 0.0;
+        double* dv = dem ? L.dcv + (size_t)c * (1 + DCP) : nullptr;
+        if (dv)
+            for (int k = 0; k < DCP; k++) dv[1 + k] = 0.0;
+        const bool ts = a.has_ts && t.mo == 2;
+        int i = c_month_start_day[m] * 24;
+        for (int d = 0; d < c_days_in_month[m]; d++) {
+            for (int hh = 0; hh < 24; hh++, i++) {
+                const bool weekend = (i % 168) >= 120;
+                const int p = weekend ? t.wkend[m][hh] : t.wkday[m][hh];
+                const double ld = a.Lh[i];
+                const double g = gen ? a.Gh[i] * s : 0.0;
+                const double dd = ld - g;
+                if (dd > peak) peak = dd;
+                if (t.mo == 0 || t.mo == 1) {
+                    bn[p] += dd;
+                } else if (t.mo == 4) {
+                    bn[p] += ld;
+                    bn[P + p] += g;
+                } else if (dd > 0.0) {
+                    bn[p] += dd;
+                } else {
+                    const double ex = -dd;
+                    bn[P + p] += ts ? ex * a.TSh[i] : ex;
+                }
+                if (dv) {
+                    const int q = weekend ? dem->wkend[m][hh] : dem->wkday[m][hh];
+                    if (dd > flat) flat = dd;
+                    if (dd > dv[1 + q]) dv[1 + q] = dd;
+                }
+            }
+        }
+        L.peak[c] = peak;
+        if (dv) dv[0] = flat;
+    }
+}
+
+// oracle year_bill (+ year_demand) of year y from its 12 cells
+__device__ double ex_year_bill(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int yl,
+                               const ExLds& L) {
+    const int P = t.P;
+    double* credit = L.yr + (size_t)yl * 2 * MAXP;
+    double* u = credit + MAXP;
+    for (int p = 0; p < MAXP; p++) credit[p] = 0.0;
+    const bool ts = a.has_ts && t.mo == 2;
+    double total = 0.0, carry = 0.0;
+    for (int m = 0; m < 12; m++) {
+        const int c = m * a.yb + yl;
+        const double* bn = L.bins + (size_t)c * 2 * P;
+        const double pk = L.peak[c];
+        double bill = t.fixed;
+        if (t.mo == 0) {
+            for (int p = 0; p < P; p++) {
+                const double n = bn[p];
+                if (n >= 0.0) {
+                    const double use = n < credit[p] ? n : credit[p];
+                    u[p] = n - use;
+                    credit[p] -= use;
+                } else {
+                    u[p] = 0.0;
+                    credit[p] += -n;
+                }
+            }
+            bill += ex_month_charge(t, m, u, pk);
+            if (m == 11) {
+                double cc = 0.0;
+                for (int p = 0; p < P; p++) cc += credit[p];
+                bill -= cc * a.yearend;
+            }
+        } else if (t.mo == 1) {
+            double cr = 0.0;
+            for (int p = 0; p < P; p++) {
+                const double n = bn[p];
+                u[p] = n > 0.0 ? n : 0.0;
+                cr += (n < 0.0 ? -n : 0.0) * t.sell[p][0];
+            }
+            const double e = ex_month_charge(t, m, u, pk) - cr - carry;
+            carry = e < 0.0 ? -e : 0.0;
+            bill += e < 0.0 ? 0.0 : e;
+        } else if (t.mo == 4) {
+            double cr = 0.0;
+            for (int p = 0; p < P; p++) {
+                u[p] = bn[p];
+                cr += bn[P + p] * t.sell[p][0];
+            }
+            bill += ex_month_charge(t, m, u, pk) - cr;
+        } else {
+            double cr = 0.0;
+            for (int p = 0; p < P; p++) u[p] = bn[p];
+            const double charge = ex_month_charge(t, m, u, pk);
+            if (ts) {
+                for (int p = 0; p < P; p++) cr += bn[P + p];
+            } else {
+                for (int p = 0; p < P; p++) cr += bn[P + p] * t.sell[p][0];
+            }
+            if (t.mo == 3) {
+                const double e = charge - cr - carry;
+                carry = e < 0.0 ? -e : 0.0;
+                bill += e < 0.0 ? 0.0 : e;
+            } else {
+                bill += charge;
+                bill -= cr;
+            }
+        }
+        total += bill;
+    }
+    if (dem) {
+        double dtot = 0.0;
+        for (int m = 0; m < 12; m++) {
+            const double* dv = L.dcv + (size_t)(m * a.yb + yl) * (1 + DCP);
+            double c = ex_dc_tier(dv[0], dem->flat_cap[m], dem->flat_price[m], dem->flat_nt[m]);
+            for (int p = 0; p < DCP; p++) c += ex_dc_tier(dv[1 + p], dem->tou_cap[p], dem->tou_price[p], dem->tou_nt[p]);
+            dtot += c;
+        }
+        total += dtot;
+    }
+    return total;
+}
+
+// the tariff's no-system bill wo1 (year 1 bins without generation)
+__device__ double ex_wo1(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, const ExLds& L) {
+    __syncthreads();
+    ex_cells(a, t, dem, 0, false, L);
+    __syncthreads();
+    if (threadIdx.x == 0) L.res[6 * (MAXY + 1)] = ex_year_bill(a, t, dem, 0, L);
+    __syncthreads();
+    return L.res[6 * (MAXY + 1)];
+}
+
+// oracle orc_cashloan over aev[0 .. N] (thread 0); returns npv, payback
+__device__ void ex_cashloan(const dgen_agents& A, const dgen_cfg& cfg, int64_t i, int N, double C, const double* aev,
+                            double* cf_payback, double* cf_ev, double* atcf, double* npv_out, double* pb_out) {
+    const bool is_res = (A.flags[i] & 1) != 0;
+    const int market = is_res ? 0 : 1;
+    const int depr_type = is_res ? 0 : 2;
+    const double infl = (A.inflation[i] * 100.0) * 0.01;
+    const double real = (A.real_discount[i] * 100.0) * 0.01;
+    const double nom = (1.0 + real) * (1.0 + infl) - 1.0;
+    const double fed = ((A.tax_rate[i] * 100.0) * 0.7) * 0.01, sta = ((A.tax_rate[i] * 100.0) * 0.3) * 0.01;
+    const double debt = (100.0 - (A.down_payment[i] * 100.0)) * 0.01 * C;
+    const double r = cfg.loan_rate_pct * 0.01;
+    const int term = A.loan_term[i];
+    double pmt = 0.0;
+    if (term > 0 && debt != 0.0) {
+        if (r != 0.0) {
+            const double f = pow_seq(1.0 + r, term);
+            pmt = debt * r / (1.0 - 1.0 / f);
+        } else {
+            pmt = debt / (double)term;
+        }
+    }
+    double itc = A.itc_frac[i] * 0.01 * C;
+    if (itc > cfg.itc_fed_max) itc = cfg.itc_fed_max;
+    const double basis = C - 0.5 * itc;
+    const double ins = cfg.insurance_rate_pct * 0.01 * C;
+    double balance = debt;
+    atcf[0] = -(C - debt);
+    cf_payback[0] = -C;
+    cf_ev[0] = 0.0;
+    for (int y = 1; y <= N; y++) {
+        const double ev = aev[y];
+        const double oe = ins * pow_seq(1.0 + infl, y - 1);
+        double interest = 0.0, payment = 0.0;
+        if (y <= term && pmt != 0.0) {
+            interest = balance * r;
+            payment = pmt;
+            balance = balance - (pmt - interest);
+        }
+        const double itc_y = (y == 1) ? itc : 0.0;
+        double sta_tax = 0.0, fed_tax = 0.0;
+        if (market != 0) {
+            const double dep = depr_frac(depr_type, y, cfg.depr_sl_years) * basis;
+            sta_tax = sta * (ev - oe - interest - dep);
+            fed_tax = fed * (ev - oe - interest - dep - sta_tax);
+        }
+        const double taxsav = itc_y - sta_tax - fed_tax;
+        atcf[y] = ev - oe - payment + taxsav;
+        cf_payback[y] = ev - oe + taxsav;
+        cf_ev[y] = ev;
+    }
+    const double rr = 1.0 / (1.0 + nom);
+    double acc = 0.0;
+    for (int y = N; y > 0; y--) acc = rr * acc + atcf[y];
+    *npv_out = atcf[0] + acc * rr;
+    double cum = cf_payback[0];
+    double pb = 1e99;
+    for (int y = 1; y <= N; y++) {
+        cum += cf_payback[y];
+        if (cum > 0.0) {
+            pb = (cf_payback[y] != 0.0) ? (double)y - cum / cf_payback[y] : (double)y - 0.5;
+            break;
+        }
+    }
+    *pb_out = pb;
+}
+
+__global__ void __launch_bounds__(EX_THREADS)
+k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const int32_t* __restrict__ list,
+             double* exws, int yb) {
+    const int cnt = list[0];
+    ExLds L;
+    {
+        double* base = dyn_lds;
+        const int P = T.max_periods > 0 && T.max_periods <= MAXP ? T.max_periods : MAXP;
+        const size_t cells = (size_t)12 * yb;
+        L.bins = base; base += cells * 2 * P;
+        L.peak = base; base += cells;
+        const bool dcb = cfg.skip_demand_charges == 0 && T.n_demand > 0;
+        L.dcv = dcb ? base : nullptr; base += dcb ? cells * (1 + DCP) : 0;
+        L.yr = base; base += (size_t)yb * 2 * MAXP;
+        L.res = base;
+    }
+    double* const aev = L.res;
+    double* const bw = L.res + (MAXY + 1);
+    double* const bwo = L.res + 2 * (MAXY + 1);
+    double* const cfpb = L.res + 3 * (MAXY + 1);
+    double* const cfev = L.res + 4 * (MAXY + 1);
+    double* const atcf = L.res + 5 * (MAXY + 1);
+    double* const sc = L.res + 6 * (MAXY + 1);          // [0] wo1, [1] npv, [2] payback
+    ExAgent a;
+    a.tariffs = T.tariffs;
+    a.demand = T.demand;
+    a.n_demand = T.n_demand;
+    a.dc_on = cfg.skip_demand_charges == 0;
+    double* const Lw = exws + (size_t)blockIdx.x * EX_WS_DOUBLES;
+    a.Lh = Lw;
+    a.Gh = Lw + NH;
+    a.TSh = Lw + 2 * NH;
+    a.yb = yb;
+    a.yearend = cfg.nm_yearend_sell_rate;
+    for (int w = blockIdx.x; w < cnt; w += gridDim.x) {
+        const int64_t i = list[1 + w];
+        const int lr = A.load_row[i], cr = A.cf_row[i];
+        const double kwh = A.load_kwh[i];
+        const uint8_t fl = A.flags[i];
+        const bool is_ca = (fl & 2) != 0;
+        const int wr = A.wholesale_row[i];
+        a.N = A.econ_life[i];
+        a.has_ts = !is_ca && wr >= 0 && T.wholesale != nullptr;
+        a.rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
+        a.sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
+        // hourly load (elec.py:571-577 scale_array_sum) and TS sell rate
+        // (ff:182,246,372 x multiplier, float32-rounded), once per agent
+        {
+            const double S = T.shape_sum[lr];
+            const float* sh = T.shapes + (int64_t)lr * NH;
+            double* Lh = Lw;
+            double* TSh = Lw + 2 * NH;
+            const double* wrow = a.has_ts ? T.wholesale + (int64_t)wr * NH : nullptr;
+            const double pmul = A.price_mult[i];
+            for (int h = threadIdx.x; h < NH; h += blockDim.x) {
+                Lh[h] = ((double)sh[h] / S) * kwh;
+                if (wrow) TSh[h] = (double)(float)(wrow[h] * pmul);
+            }
+        }
+        const int32_t* cfr = T.cfs + (int64_t)cr * NH;
+        const double naep0 = T.cf_naep[cr];
+        const double max_load = kwh / naep0;
+        const double low = max_load * 0.8, high = max_load * 1.25;
+        const double span = high - low;
+        const double tl = (span > 1.0 ? span : 1.0) * 1e-3;
+        const double fl_tl = floor(tl);
+        const double xatol = fl_tl < 2.0 ? 2.0 : fl_tl;
+        const dgen_switch* sw = T.switches + A.sw_solar_off[i];
+        const int sw_cnt = A.sw_solar_cnt[i];
+        int tariff = A.tariff0[i], switched = 0;
+        int status = O.status[i] | T.tariffs[tariff].flags;
+        int wo_tag = -1;
+        double wo1 = 0.0, total = 0.0, npv = 0.0, pb = 0.0;
+        auto perf = [&](double kw) __attribute__((always_inline)) -> double {
+            // ff:117-120 generation per hour, oracle perf_no_batt's order
+            for (int h = threadIdx.x; h < NH; h += blockDim.x)
+                a.Gh[h] = (((cf_per_kw(cfr[h]) * kw) * 1000.0) * 0.96) / 1000.0;
+            double otc = 0.0;
+            if (kw > 0.0) {
+                int nt;
+                otc = rate_switch(sw, sw_cnt, kw, &nt);
+                if (nt >= 0) {
+                    tariff = nt;
+                    switched = 1;
+                    status |= T.tariffs[nt].flags;
+                }
+            }
+            const dgen_tariff& t = T.tariffs[tariff];
+            const dgen_demand* dem = (a.dc_on && t.dc > 0 && t.dc <= a.n_demand) ? a.demand + (t.dc - 1) : nullptr;
+            ex_handoff();
+            if (wo_tag != tariff) {
+                wo1 = ex_wo1(a, t, dem, L);
+                wo_tag = tariff;
+            }
+            for (int y0 = 0; y0 < a.N; y0 += a.yb) {
+                __syncthreads();
+                ex_cells(a, t, dem, y0, true, L);
+                __syncthreads();
+                const int yl = (int)threadIdx.x;
+                if (yl < a.yb && y0 + yl < a.N) {
+                    const int y = y0 + yl;
+                    const double r = pow_seq(a.rate_base, y);
+                    const double wb = ex_year_bill(a, t, dem, yl, L);
+                    const double w = wb * r;
+                    const double wo = wo1 * r;
+                    bw[y + 1] = w;
+                    bwo[y + 1] = wo;
+                    aev[y + 1] = wo - w;
+                }
+            }
+            __syncthreads();
+            total = ((A.capex[i] * kw + 0.0) * A.ccm[i]) + 0.0 + otc;
+            if (threadIdx.x == 0) {
+                aev[0] = 0.0;
+                bw[0] = 0.0;
+                bwo[0] = 0.0;
+                double v, q;
+                ex_cashloan(A, cfg, i, a.N, total, aev, cfpb, cfev, atcf, &v, &q);
+                sc[1] = v;
+                sc[2] = q;
+            }
+            __syncthreads();
+            npv = sc[1];
+            pb = sc[2];
+            return -npv;
+        };
+        int nfev = 0;
+        double x_last = 0.0;
+        const double kw_star = brent_bounded(perf, low, high, xatol, &nfev, &x_last);
+        __syncthreads();
+        // the driver's last-evaluation capture (ff:449-474), as k_size writes it
+        const int64_t row = i * (MAXY + 1);
+        for (int k = threadIdx.x; k <= a.N; k += blockDim.x) {
+            O.cash_flow[row + k] = k == 0 ? -total : cfpb[k];
+            O.cfev_pv[row + k] = k == 0 ? 0.0 : cfev[k];
+            O.bill_w_pv[row + k] = bw[k];
+            O.bill_wo_pv[row + k] = bwo[k];
+        }
+        if (threadIdx.x == 0) {
+            O.npv[i] = npv;
+            O.payback_raw[i] = pb;
+            const double pbr = isfinite(pb) ? pb : 30.1;
+            O.payback_period[i] = rint(pbr * 10.0) / 10.0;
+            O.first_with[i] = bw[1];
+            O.first_without[i] = wo1;
+            O.price_per_kwh[i] = wo1 / kwh;
+            O.system_kw[i] = kw_star;
+            O.x_last[i] = x_last;
+            O.nfev[i] = nfev;
+            O.tariff_final[i] = tariff;
+            O.switched[i] = switched;
+            O.status[i] = status;
+        }
+        __syncthreads();
+    }
+}
+#endif  // !DGEN_TU_SEARCH
+
 }  // namespace
 
 // The year-lane search kernels (k_size_w, k_dc_env, k_nb_env) have external
@@ -5075,7 +5844,7 @@ __global__ void k_finance_series(Series6 src, const int32_t* __restrict__ len, i
 namespace dgen_srch {
 #define DGEN_INST_SIZE(L, D, N, P)                                                                       \
     template __global__ void k_size_w<L, D, N, P>(dgen_tables, dgen_agents, dgen_outputs, dgen_cfg,   \
-                                                  int64_t, int64_t, int64_t, void*, char*, int);
+                                                  int64_t, int64_t, int64_t, void*, char*, int, double*);
 #if !DGEN_NO2_SIZE
 DGEN_INST_SIZE(32, false, false, false)
 DGEN_INST_SIZE(32, false, true, false)
@@ -5143,6 +5912,16 @@ struct dgen_ctx {
     void* dcr_buf = nullptr;  // battery-case demand records, DCR_BYTES per scratch slot (grown on demand)
     size_t dcr_cap = 0;
     int dcr_enable = DCR_CAP; // kept hours per record, 0 = off (dgen_set_dc_records)
+    // certified Brent paths (dgen_set_exact): the search traces, the listed
+    // agents per chunk, the exact re-run's per-block hour scratch
+    int exact = 1;
+    double* bt_buf = nullptr;      // [n][BT_MAX] objective values
+    size_t bt_cap = 0;
+    int32_t* ex_list = nullptr;    // chunk j: [i0 + j] count, then its rows
+    size_t ex_list_cap = 0;
+    double* ex_ws = nullptr;       // [EX_BLOCKS][3][8760]
+    int ex_last_nch = 0;
+    int64_t ex_last_off[MAXCH] = {0};
 };
 
 static int fold_one(dgen_ctx* c, int slot) {
@@ -5287,6 +6066,9 @@ int32_t dgen_close(dgen_ctx* c) {
     if (c->dc_buf) (void)hipFree(c->dc_buf);
     if (c->dcr_buf) (void)hipFree(c->dcr_buf);
     if (c->rows_buf) (void)hipFree(c->rows_buf);
+    if (c->bt_buf) (void)hipFree(c->bt_buf);
+    if (c->ex_list) (void)hipFree(c->ex_list);
+    if (c->ex_ws) (void)hipFree(c->ex_ws);
     delete c;
     return DGEN_OK;
 }
@@ -5407,6 +6189,33 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         }
     }
     hipStream_t s = (hipStream_t)stream;
+    // certified Brent paths: trace buffer, per-chunk lists, exact scratch
+    const bool exact_on = c->exact != 0;
+    if (exact_on) {
+        if ((size_t)n * BT_MAX * sizeof(double) > c->bt_cap) {
+            if (c->bt_buf) HIP_TRY(hipFree(c->bt_buf));
+            c->bt_buf = nullptr;
+            c->bt_cap = 0;
+            HIP_TRY(hipMalloc(&c->bt_buf, (size_t)n * BT_MAX * sizeof(double)));
+            c->bt_cap = (size_t)n * BT_MAX * sizeof(double);
+        }
+        if ((size_t)(n + dgen_ctx::MAXCH) * sizeof(int32_t) > c->ex_list_cap) {
+            if (c->ex_list) HIP_TRY(hipFree(c->ex_list));
+            c->ex_list = nullptr;
+            c->ex_list_cap = 0;
+            HIP_TRY(hipMalloc(&c->ex_list, (size_t)(n + dgen_ctx::MAXCH) * sizeof(int32_t)));
+            c->ex_list_cap = (size_t)(n + dgen_ctx::MAXCH) * sizeof(int32_t);
+        }
+        if (!c->ex_ws) HIP_TRY(hipMalloc(&c->ex_ws, (size_t)EX_BLOCKS * EX_WS_DOUBLES * sizeof(double)));
+    }
+    // the exact re-run's block: 12 months x yb years of cells within 64 KB of LDS
+    const bool ex_dcb = c->cfg.skip_demand_charges == 0 && T->n_demand > 0;
+    const int ex_P = (T->max_periods > 0 && T->max_periods <= MAXP) ? T->max_periods : MAXP;
+    int ex_yb = 32;
+    while (ex_yb > 1 && ex_lds_bytes(ex_P, ex_yb, ex_dcb) > 65536) ex_yb--;
+    const int ex_threads = (12 * ex_yb + WAVE - 1) / WAVE * WAVE;
+    const size_t ex_lds = ex_lds_bytes(ex_P, ex_yb, ex_dcb);
+    double* const bt = exact_on ? c->bt_buf : nullptr;
     if (c->pending == dgen_ctx::RING) {   // fold the oldest record before reuse
         int r = fold_one(c, c->head);
         if (r) return r;
@@ -5506,6 +6315,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     c->last_paths[6] = dc_pre;
     const int nb_pre = (n_scratch > 0 && c->nb_pre) ? 1 : 0;
     const int pre = dc_pre | (nb_pre << 1);     // k_size's view of the two prebuilds
+    c->ex_last_nch = exact_on ? nch : 0;
     HIP_TRY(hipEventRecord(c->fork, s));
     HIP_TRY(hipStreamWaitEvent(s2, c->fork, 0));
     for (int j = 0; j < nch; j++) {
@@ -5551,49 +6361,61 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             if (net) {
                 if (nm > i0)
                     hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_sa, dim3(WAVE), ylds_s_nem, s, *T, *A,
-                                       *O, c->cfg, n, i0, nm, nullptr, nbws, pre);
+                                       *O, c->cfg, n, i0, nm, nullptr, nbws, pre, bt);
                 if (i1 > nm)
                     hipLaunchKernelGGL((k_size_w<32, false, true, false>), ygrid_sb, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                       c->cfg, n, nm, i1, nullptr, nbws, pre);
+                                       c->cfg, n, nm, i1, nullptr, nbws, pre, bt);
             } else
                 hipLaunchKernelGGL((k_size_w<32, false, false, false>), ygrid_s, dim3(WAVE), ylds_s_nem, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws, pre);
+                                   c->cfg, n, i0, i1, nullptr, nbws, pre, bt);
 #endif
         } else if (lpa_s == 32 && !pk) {
 #if !DGEN_NO2_SIZE_DC
             if (dc_net)
                 hipLaunchKernelGGL((k_size_w<32, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre, bt);
             else
                 hipLaunchKernelGGL((k_size_w<32, true, false, false>), ygrid_s, dim3(WAVE), ylds_s_dc, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre, bt);
 #endif
         } else if (lpa_s == 32) {
 #if !DGEN_NO2_SIZE_PK
             hipLaunchKernelGGL((k_size_w<32, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre, bt);
 #endif
         } else if (!dc) {
             if (net) {
                 if (nm > i0)
                     hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_sa, dim3(WAVE), ylds_s_nem, s, *T,
-                                       *A, *O, c->cfg, n, i0, nm, nullptr, nbws, pre);
+                                       *A, *O, c->cfg, n, i0, nm, nullptr, nbws, pre, bt);
                 if (i1 > nm)
                     hipLaunchKernelGGL((k_size_w<WAVE, false, true, false>), ygrid_sb, dim3(WAVE), ylds_s, s, *T, *A,
-                                       *O, c->cfg, n, nm, i1, nullptr, nbws, pre);
+                                       *O, c->cfg, n, nm, i1, nullptr, nbws, pre, bt);
             } else
                 hipLaunchKernelGGL((k_size_w<WAVE, false, false, false>), ygrid_s, dim3(WAVE), ylds_s_nem, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, nullptr, nbws, pre);
+                                   c->cfg, n, i0, i1, nullptr, nbws, pre, bt);
         } else if (!pk) {
             if (dc_net)
                 hipLaunchKernelGGL((k_size_w<WAVE, true, true, false>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre, bt);
             else
                 hipLaunchKernelGGL((k_size_w<WAVE, true, false, false>), ygrid_s, dim3(WAVE), ylds_s_dc, s, *T, *A, *O,
-                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+                                   c->cfg, n, i0, i1, c->dc_buf, nbws, pre, bt);
         } else {
             hipLaunchKernelGGL((k_size_w<WAVE, true, true, true>), ygrid_s, dim3(WAVE), ylds_s, s, *T, *A, *O,
-                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre);
+                               c->cfg, n, i0, i1, c->dc_buf, nbws, pre, bt);
+        }
+        if (exact_on) {
+            // the chunk's searches replayed against the oracle-difference
+            // bound; the listed agents re-run in the oracle's arithmetic
+            // (counted in k_size's time)
+            int32_t* const lst = c->ex_list + i0 + j;
+            c->ex_last_off[j] = i0 + j;
+            HIP_TRY(hipMemsetAsync(lst, 0, sizeof(int32_t), s));
+            hipLaunchKernelGGL(k_brent_certify, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, *T, *A, *O,
+                               c->cfg, i0, i1, bt, lst, c->exact);
+            hipLaunchKernelGGL(k_size_exact, dim3((unsigned)(m < EX_BLOCKS ? m : EX_BLOCKS)), dim3(ex_threads),
+                               ex_lds, s, *T, *A, *O, c->cfg, lst, c->ex_ws, ex_yb);
         }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
@@ -5895,6 +6717,26 @@ int32_t dgen_set_dc_records(dgen_ctx* c, int32_t cap) {
     return DGEN_OK;
 }
 
+int32_t dgen_set_exact(dgen_ctx* c, int32_t mode) {
+    if (!c || mode < 0 || mode > 2) { set_err("dgen_set_exact: mode must be 0, 1 or 2"); return DGEN_E_ARG; }
+    c->exact = mode;
+    return DGEN_OK;
+}
+
+int32_t dgen_exact_count(dgen_ctx* c, int64_t* out) {
+    if (!c || !out) { set_err("dgen_exact_count: null argument"); return DGEN_E_ARG; }
+    *out = 0;
+    if (c->ex_last_nch == 0 || !c->ex_list) return DGEN_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    for (int j = 0; j < c->ex_last_nch; j++) {
+        int32_t k = 0;
+        HIP_TRY(hipMemcpy(&k, c->ex_list + c->ex_last_off[j], sizeof(int32_t), hipMemcpyDeviceToHost));
+        *out += k;
+    }
+    return DGEN_OK;
+}
+
 int32_t dgen_set_battery(dgen_ctx* c, int32_t on) {
     if (!c || (on != 0 && on != 1)) {
         set_err("dgen_set_battery: on must be 0 or 1");
@@ -6153,8 +6995,8 @@ int32_t dgen_state_hourly_rows(dgen_ctx* c, const dgen_tables* T, const dgen_age
     if (n_seg == 0) return DGEN_OK;
     HIP_TRY(hipSetDevice(c->device));
     if ((size_t)n * sizeof(double2) > c->rows_cap) {        // per-agent scalars (grown on demand)
-        if (c->rows_buf) {
-            HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+        if (c->rows_buf) {       // an earlier call may still read it on another stream
+            HIP_TRY(hipDeviceSynchronize());
             HIP_TRY(hipFree(c->rows_buf));
         }
         c->rows_buf = nullptr;

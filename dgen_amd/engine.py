@@ -45,6 +45,9 @@ class AgentBatch:
     no_net: bool = False
     # leading device rows without a scratch slot (dgen_set_nem_rows)
     nem_rows: int = 0
+    # Engine._tables_gen when no_net / nb_scan were decided: a later
+    # set_tariffs / set_switches makes size() fall back to the general forms
+    tables_gen: int = 0
 
 
 def path_class(cols: Dict[str, np.ndarray]) -> np.ndarray:
@@ -88,6 +91,33 @@ def profile_order(cols: Dict[str, np.ndarray], major: str = "load",
     return np.lexsort(keys).astype(np.int64)
 
 
+def tariff_price_bounds(recs: np.ndarray, dem: Optional[np.ndarray]) -> np.ndarray:
+    """dgen_tables.bt_tariff: per tariff [max |buy|, |sell| over its periods
+    and tiers ($/kWh); the largest month's flat demand price + every TOU
+    period's ($/kW, 0 without a demand record); the kWh/kW tier caps'
+    sensitivity to the month peak (2 x energy price x sum of caps, x 31 for
+    daily caps; 0 for other units)] -- the certified Brent paths' bounds
+    (k_brent_certify)."""
+    n = recs.size
+    out = np.zeros((n, 3), np.float64)
+    for j in range(n):
+        r = recs[j]
+        P, T = int(r["P"]), int(r["T"])
+        e = max(float(np.abs(r["buy"][:P, :T]).max(initial=0.0)), float(np.abs(r["sell"][:P, :T]).max(initial=0.0)))
+        out[j, 0] = e
+        dc = int(r["dc"])
+        if dem is not None and 0 < dc <= len(dem):
+            d = dem[dc - 1]
+            tou = sum(float(np.abs(d["tou_price"][p, :int(d["tou_nt"][p])]).max(initial=0.0))
+                      for p in range(d["tou_price"].shape[0]))
+            flat = max(float(np.abs(d["flat_price"][m, :int(d["flat_nt"][m])]).max(initial=0.0)) for m in range(12))
+            out[j, 1] = flat + tou
+        u = int(r["unit"])
+        if u in (1, 3):
+            out[j, 2] = 2.0 * e * float(np.abs(r["cap"][:T]).sum()) * (31.0 if u == 3 else 1.0)
+    return out
+
+
 class Engine:
     def __init__(self, device: int = 0, cfg: Optional[EngineConfig] = None):
         torch = _torch()
@@ -102,11 +132,13 @@ class Engine:
         c = self.cfg.to_c()
         _lib.check(self.lib.dgen_open(self.device, ctypes.byref(c), ctypes.byref(h)), "dgen_open")
         self.ctx = h
+        _lib.check(self.lib.dgen_set_exact(self.ctx, int(self.cfg.exact_brent)), "dgen_set_exact")
         self.tables = _lib.Tables()
         self.chunks = _lib.DEFAULT_CHUNKS
         self.hb_months = _lib.DEFAULT_HOURLY_MONTHS
         self.battery = True
         self._keep: Dict[str, object] = {}
+        self._tables_gen = 0            # bumped by set_tariffs / set_switches
 
     # ------------------------------------------------------------------ utils
     def stream_handle(self) -> int:
@@ -154,12 +186,19 @@ class Engine:
             ws = self._to_dev(wholesale, torch.float64)
             if ws.dim() != 2 or ws.shape[1] != _lib.NH:
                 raise ValueError("wholesale table must be [rows, 8760]")
+        # row maxima for the certified Brent paths' error bounds (dgen_set_exact)
+        sh_max = sh.abs().amax(dim=1).to(torch.float64).contiguous()
+        cf_max = cf.abs().amax(dim=1).to(torch.float64).contiguous()
+        ws_max = (torch.nan_to_num(ws.abs(), nan=0.0, posinf=0.0).amax(dim=1).contiguous()
+                  if ws is not None else None)
         self._keep.update(shapes=sh, shape_sum=s_sum, shape_slots=s_slots, cfs=cf,
-                          cf_naep=c_naep, cf_slots=c_slots, wholesale=ws)
+                          cf_naep=c_naep, cf_slots=c_slots, wholesale=ws,
+                          bt_shape_max=sh_max, bt_cf_max=cf_max, bt_ts_max=ws_max)
         T = self.tables
         T.shapes, T.shape_sum, T.shape_slots = _ptr(sh), _ptr(s_sum), _ptr(s_slots)
         T.cfs, T.cf_naep, T.cf_slots = _ptr(cf), _ptr(c_naep), _ptr(c_slots)
         T.wholesale = _ptr(ws)
+        T.bt_shape_max, T.bt_cf_max, T.bt_ts_max = _ptr(sh_max), _ptr(cf_max), _ptr(ws_max)
         T.n_shapes, T.n_cfs = R, C
         T.n_wholesale = 0 if ws is None else ws.shape[0]
 
@@ -192,9 +231,13 @@ class Engine:
         self._keep["tariffs"] = t
         self.tariff_records = recs
         self.tables.tariffs = _ptr(t)
+        bt = self._to_dev(tariff_price_bounds(recs, dem), _torch().float64)
+        self._keep["bt_tariff"] = bt
+        self.tables.bt_tariff = _ptr(bt)
         self.tables.n_tariffs = int(recs.size)
         self.tables.max_periods = int(recs["P"].max())
         self.tables.no_net = 0                # set per batch by size() (AgentBatch.no_net)
+        self._tables_gen += 1
 
     def set_switches(self, sw: np.ndarray):
         sw = np.ascontiguousarray(sw, dtype=SWITCH_DTYPE)
@@ -206,6 +249,7 @@ class Engine:
         self.tables.switches = _ptr(t)
         self.tables.n_switches = int(sw.size)
         self._switch_tariff = sw["tariff"].copy()
+        self._tables_gen += 1
 
     def profile_sums(self):
         """(shape row sums, cf naep) as host arrays (for tests / host checks)."""
@@ -253,7 +297,8 @@ class Engine:
         ca.max_years = int(dev["econ_life"].max().item()) if n else 0
         return AgentBatch(n=n, n_scratch=n_scratch, cols=dev, workspace=ws, c_agents=ca, perm=order,
                           nb_scan=self._nb_scan_pays(cols, n, n_scratch), ts_rows=self._ts_rows_of(cols, n),
-                          no_net=self._no_net_of(cols, n), nem_rows=self._nem_rows_of(cols, n))
+                          no_net=self._no_net_of(cols, n), nem_rows=self._nem_rows_of(cols, n),
+                          tables_gen=self._tables_gen)
 
     def _nem_rows_of(self, cols, n: int) -> int:
         """dgen_set_nem_rows: the length of the batch's leading run of device
@@ -296,7 +341,12 @@ class Engine:
         net = np.isin(mo, (2, 3))
         if not net.any():
             return True
-        t0 = np.asarray(cols["tariff0"], np.int64)
+        try:                   # device-tensor columns: keep the net-billing forms
+            t0 = np.asarray(cols["tariff0"], np.int64)
+            offs = {k: (np.asarray(cols[f"sw_{k}_off"], np.int64), np.asarray(cols[f"sw_{k}_cnt"], np.int64))
+                    for k in ("solar", "storage")}
+        except Exception:
+            return False
         if ((t0 < 0) | (t0 >= net.size)).any() or net[t0].any():
             return False
         swt = getattr(self, "_switch_tariff", None)
@@ -306,9 +356,7 @@ class Engine:
         okr = (swt >= 0) & (swt < net.size)
         sw_net[okr] = net[swt[okr]]
         csum = np.concatenate([[0], np.cumsum(sw_net.astype(np.int64))])
-        for k in ("solar", "storage"):
-            off = np.asarray(cols[f"sw_{k}_off"], np.int64)
-            cnt = np.asarray(cols[f"sw_{k}_cnt"], np.int64)
+        for off, cnt in offs.values():
             lo = np.clip(off, 0, swt.size)
             hi = np.clip(off + cnt, 0, swt.size)
             if ((csum[hi] - csum[lo]) > 0).any():
@@ -400,11 +448,16 @@ class Engine:
     def size(self, batch: AgentBatch, out: Dict[str, object], c_out: Optional[_lib.Outputs] = None):
         """Launch the sizing kernels for `batch` on the current stream (async)."""
         co = c_out if c_out is not None else self.c_outputs(out)
-        self.tables.no_net = int(batch.no_net)
-        if batch.nb_scan != getattr(self, "_nb_scan", True):
-            _lib.check(self.lib.dgen_set_nb_scan(self.ctx, _lib.NB_CAPM if batch.nb_scan else 0),
+        # no_net / nb_scan were decided against the tables of upload time; after
+        # a set_tariffs / set_switches take the forms that are right for any
+        # table (the net-billing instantiations, the scan-built split on)
+        fresh = batch.tables_gen == self._tables_gen
+        self.tables.no_net = int(batch.no_net and fresh)
+        nb_scan = batch.nb_scan or (not fresh and batch.n_scratch > 0)
+        if nb_scan != getattr(self, "_nb_scan", True):
+            _lib.check(self.lib.dgen_set_nb_scan(self.ctx, _lib.NB_CAPM if nb_scan else 0),
                        "dgen_set_nb_scan")
-            self._nb_scan = batch.nb_scan
+            self._nb_scan = nb_scan
         if int(batch.nem_rows) != getattr(self, "_nem_rows", 0):
             _lib.check(self.lib.dgen_set_nem_rows(self.ctx, int(batch.nem_rows)), "dgen_set_nem_rows")
             self._nem_rows = int(batch.nem_rows)
@@ -485,6 +538,20 @@ class Engine:
         _lib.check(self.lib.dgen_last_paths(self.ctx, a, 7), "dgen_last_paths")
         keys = ("nb_scan", "dcr_on", "ts_split", "dc", "max_periods", "dc_periods", "dc_prebuild")
         return dict(zip(keys, (int(v) for v in a)))
+
+    def set_exact(self, mode: int):
+        """Certified Brent paths (dgen_set_exact): 1 (default) re-runs the
+        agents whose search a device/oracle difference bound does not settle
+        in the reference's arithmetic, 2 every agent, 0 none."""
+        _lib.check(self.lib.dgen_set_exact(self.ctx, int(mode)), "dgen_set_exact")
+        self.cfg.exact_brent = int(mode)
+
+    def exact_count(self) -> int:
+        """Agents the last size() call re-ran in the reference's arithmetic
+        (synchronises the device)."""
+        v = ctypes.c_int64(0)
+        _lib.check(self.lib.dgen_exact_count(self.ctx, ctypes.byref(v)), "dgen_exact_count")
+        return int(v.value)
 
     def kernel_times(self):
         """Average per-launch device time (ms) of the three sizing kernels over

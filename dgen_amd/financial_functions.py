@@ -208,14 +208,18 @@ def device_rows_budget(eng, frac: float = 0.3) -> int:
     unused blocks) / agent_device_bytes.  frac 0.3: two sub-batches are
     resident at once (one sizing while the previous one's planes download),
     and other workers sharing the GPU (a spawn pool larger than the node's GPU
-    count) see the rest.  At least 1024."""
+    count) see the rest.  Workers that share a device may read the free
+    memory at the same moment, so frac is divided by ``DGEN_WORKERS_PER_DEVICE``
+    (pool size / GPUs; default 1); _run_device also halves its sub-batch and
+    retries when a device allocation fails.  At least 1024."""
     env = os.environ.get("DGEN_MAX_ROWS", "").strip()
     if env:
         return max(1, int(env))
     import torch
+    share = max(1, int(os.environ.get("DGEN_WORKERS_PER_DEVICE", "1").strip() or 1))
     free, _total = torch.cuda.mem_get_info(eng.dev)
     spare = torch.cuda.memory_reserved(eng.dev) - torch.cuda.memory_allocated(eng.dev)
-    return max(1024, int(frac * (free + max(spare, 0)) / agent_device_bytes(eng)))
+    return max(1024, int(frac / share * (free + max(spare, 0)) / agent_device_bytes(eng)))
 
 
 def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[dict] = None,
@@ -237,6 +241,21 @@ def _run_device(b: PopulationBuilder, cols, src: ProfileStore, timing: Optional[
     if max_rows is None:
         max_rows = device_rows_budget(get_engine())
     max_rows = max(1, int(max_rows))
+    import torch
+    try:
+        return _run_device_rows(b, cols, src, timing, net_weights, hourly_async, hourly_device, max_rows)
+    except torch.cuda.OutOfMemoryError:
+        # another worker on this device took the memory the budget counted on:
+        # free this process's cached blocks and size in halves (down to 1024)
+        smaller = min(n, max_rows) // 2
+        if smaller < 1024:
+            raise
+        torch.cuda.empty_cache()
+        return _run_device(b, cols, src, timing, net_weights, hourly_async, hourly_device, max_rows=smaller)
+
+
+def _run_device_rows(b, cols, src, timing, net_weights, hourly_async, hourly_device, max_rows: int):
+    n = len(cols["load_kwh"])
     if n <= max_rows:
         return _run_device_once(b, cols, src, timing, net_weights, hourly_async, hourly_device)
     from .hourly_column import _Segments

@@ -684,7 +684,7 @@ class YearLoop:
             ca = _lib.Agents(**{name: cols[name].data_ptr() for name, _ in _lib.AGENT_COLUMNS})
             ca.max_years = B.c_agents.max_years
             sub = AgentBatch(n=m, n_scratch=B.n_scratch, cols=cols, workspace=B.workspace,
-                             c_agents=ca, nb_scan=B.nb_scan)
+                             c_agents=ca, nb_scan=B.nb_scan, tables_gen=B.tables_gen)
             out = {k: v[a:b] for k, v in self.out.items() if v is not None}
             wc = tuple(x[a:b] for x in w)
             if self._comb:

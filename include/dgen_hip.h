@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define DGEN_ABI_VERSION 13
+#define DGEN_ABI_VERSION 14
 #define DGEN_DEFAULT_CHUNKS 1  /* dgen_size_agents pipeline depth (dgen_set_pipeline) */
 #define DGEN_DEFAULT_HOURLY_MONTHS 1  /* months per k_hourly_batt launch (dgen_set_hourly_segment) */
 #define DGEN_DEFAULT_HOURLY_SPLIT 2   /* parts of a chunk's hourly scan, each on its own stream */
@@ -190,6 +190,16 @@ typedef struct {
                                    /* charge kernels run their instantiations       */
                                    /* without the net-billing paths (fewer          */
                                    /* registers); 0: some may (ABI 12)              */
+    int32_t pad_t;
+    /* Bounds of the certified Brent paths (ABI 14, dgen_set_exact; each may be   */
+    /* NULL: the agents that would need it take the exact re-run instead):        */
+    const double*  bt_tariff;      /* [n_tariffs][3]: max |buy|, |sell| ($/kWh);   */
+                                   /* demand prices, max over months of the flat   */
+                                   /* tier price + the TOU periods' ($/kW); the     */
+                                   /* kWh/kW tier caps' peak sensitivity ($/kW)     */
+    const double*  bt_shape_max;   /* [n_shapes] max |shape| of the row             */
+    const double*  bt_cf_max;      /* [n_cfs]    max |cf| of the row (x 1e6)        */
+    const double*  bt_ts_max;      /* [n_wholesale] max |wholesale| of the row      */
 } dgen_tables;
 
 /* Agent batch, structure of arrays (device pointers, length n).  Column
@@ -607,6 +617,11 @@ int32_t dgen_hourly_planes(dgen_ctx* ctx, const dgen_tables* tables, const dgen_
  * instead of 12.  Daily plan without the loss model only (DGEN_E_ARG
  * otherwise: use dgen_hourly_planes).  n < 2^27.  Replaces nothing in the
  * reference (attachment_rate_functions.py:151-206 sums the frame's lists).   */
+int32_t dgen_export_plane(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
+                          const dgen_outputs* outputs, const double* w_pvo, const double* w_batt,
+                          const double* w_non, double* plane, int64_t n, void* workspace,
+                          size_t workspace_bytes, int64_t n_scratch, void* stream);
+
 /* The per-state export from the with-battery plane alone (ABI 11): a batch
  * sized by dgen_size_agents with only outputs.net_with_batt set (float32
  * hour-quad tiles; daily plan, no loss model, no demand charges / kWh/kW
@@ -616,16 +631,13 @@ int32_t dgen_hourly_planes(dgen_ctx* ctx, const dgen_tables* tables, const dgen_
  * MW) equals dgen_state_hourly over the three float32 planes bit for bit,
  * from 4 B of plane per agent-hour.  idx / seg_off as dgen_state_hourly.
  * Replaces nothing in the reference (attachment_rate_functions.py:151-206
- * sums the frame's hourly lists).                                           */
+ * sums the frame's hourly lists).  The per-agent scalars live in a buffer
+ * the ctx owns and grows on demand (after a device-wide sync): calls on one
+ * ctx must be serialised, as for every other entry point.                 */
 int32_t dgen_state_hourly_rows(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
                                const dgen_outputs* outputs, const float* with_batt, const double* w_pvo,
                                const double* w_batt, const double* w_non, const int64_t* idx, int64_t n,
                                const int64_t* seg_off, int64_t n_seg, double* out, void* stream);
-
-int32_t dgen_export_plane(dgen_ctx* ctx, const dgen_tables* tables, const dgen_agents* agents,
-                          const dgen_outputs* outputs, const double* w_pvo, const double* w_batt,
-                          const double* w_non, double* plane, int64_t n, void* workspace,
-                          size_t workspace_bytes, int64_t n_scratch, void* stream);
 
 /* Months of the year per k_hourly_batt launch (the sequential 8760-h scan of
  * dgen_size_agents): the year is swept in ceil(12 / months) launches, SOC and
@@ -679,6 +691,23 @@ int32_t dgen_set_ts_rows(dgen_ctx* ctx, int64_t lo, int64_t hi);
  * same values).  An agent whose kept hours overflow the record falls back to
  * the plane.  Replaces nothing in the reference.                            */
 int32_t dgen_set_dc_records(dgen_ctx* ctx, int32_t cap);
+
+/* Certified Brent paths (ABI 14).  The search bills from re-associated sums
+ * (slot sums, net-billing split), a few ulps from the reference's hour order,
+ * and scipy's bounded Brent can turn such a difference into another search
+ * path (ff:440-447).  mode 1 (default): every search traces its objective
+ * values; a replay with a bound on |device - reference| carried through every
+ * Brent state variable lists the agents with a decision that bound does not
+ * settle, and those agents' searches re-run in the reference's arithmetic
+ * (hours in time order: Utilityrate5 bins, bill, Cashloan, op for op), so every
+ * agent takes the reference's path.  mode 2: every searched agent re-runs
+ * (test mode).  mode 0: off (k_size's search alone).  Replaces nothing in the
+ * reference (its one path is the hour-order one).                            */
+int32_t dgen_set_exact(dgen_ctx* ctx, int32_t mode);
+
+/* Agents the last dgen_size_agents call re-ran in the reference's arithmetic
+ * (synchronises the ctx's stream work of that call).                         */
+int32_t dgen_exact_count(dgen_ctx* ctx, int64_t* out);
 
 #ifdef __cplusplus
 }

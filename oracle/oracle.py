@@ -328,6 +328,18 @@ class Population:
             raise ValueError(f"orc_eval_at failed: {rc}")
         return result_to_dict(r, int(self.agents[i].econ_life), bufs)
 
+    def run_parallel(self, cfg: Cfg, threads: int = 0, idx=None):
+        """As run() without hourly outputs, the agents sized by the OpenMP batch
+        entry (orc_size_batch) over `threads` (0: OMP_NUM_THREADS or all CPUs)."""
+        import os
+        idxs = list(range(self.n)) if idx is None else [int(i) for i in idx]
+        if threads <= 0:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        sub = (Agent * len(idxs))(*[self.agents[i] for i in idxs])
+        res = (Result * len(idxs))()
+        lib().orc_size_batch(sub, len(idxs), self.tariffs, self.n_tariffs, ctypes.byref(cfg), res, int(threads))
+        return [result_to_dict(res[k], int(sub[k].econ_life)) for k in range(len(idxs))]
+
     def run_batch_timed(self, cfg: Cfg, threads: int, idx: Sequence[int]):
         """Batch entry used for the CPU baseline (OpenMP over `threads`)."""
         sub = (Agent * len(idx))(*[self.agents[i] for i in idx])

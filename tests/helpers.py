@@ -230,13 +230,15 @@ def golden_market():
 
 
 # ---------------------------------------------------------------------------
-# Knife-edge agents: scipy's bounded Brent divides
-# differences of nearly equal objective values in its parabolic step, so on a
-# few agents per thousand an ulp of difference between the device's and the
-# oracle's objective (their bills re-associate sums) leads to a different,
-# equally valid Brent path.  Such an agent is checked at the device's own
-# point: its kW within scipy's xatol of the oracle's, and every output equal to
-# the oracle's driver evaluated where the device's search ended (orc_eval_at).
+# Brent paths: the device's fast search bills from
+# re-associated sums, a few ulps from the oracle's hour order; scipy's bounded
+# Brent divides differences of nearly equal objective values in its parabolic
+# step, so such a difference can move the search path.  The certified paths
+# (dgen_set_exact, on by default) re-run every agent whose path a bound on that
+# difference does not settle in the oracle's arithmetic, so every agent is on
+# the oracle's path (same_path); with them off (exact_brent = 0), a divergent
+# agent ends within scipy's xatol and equals the oracle's driver evaluated at
+# the device's own search end (at_device_point).
 # ---------------------------------------------------------------------------
 def xatol_of(load_kwh: float, naep: float) -> float:
     """ff:440-444: bracket (0.8, 1.25) x load / naep, xatol = max(2, int(1e-3 x span))."""
@@ -251,19 +253,14 @@ def same_path(o, i: int, r) -> bool:
             and abs(o["x_last"][i] - r["x_last"]) <= 1e-9 * max(1.0, abs(r["x_last"])))
 
 
-def at_device_point(o, i: int, opop, j: int, cfg, r, tariff0: int, xatol: float, hourly: bool = False):
-    """Oracle outputs of agent j of opop at device agent i's search end (kW,
-    last x, sticky tariff state): the device's chosen kW must be within xatol
-    of the oracle's; of the tariff states the device may have ended its search
-    in (its final tariff, the oracle's, the initial one) the one whose NPV is
-    nearest is returned for the caller's full comparison."""
+def at_device_point(o, i: int, opop, j: int, cfg, r, xatol: float, hourly: bool = False):
+    """Oracle outputs of agent j of opop evaluated once at device agent i's
+    search end -- its kW, last x and sticky tariff state (tariff_final and
+    switched as the device reports them: size with the battery run off, so no
+    storage switch follows the search).  The device's kW must be within
+    scipy's xatol of the oracle's search result."""
     kw, xl = float(o["system_kw"][i]), float(o["x_last"][i])
     assert abs(kw - r["system_kw"]) <= xatol, ("kW beyond xatol", i, kw, r["system_kw"], xatol)
-    best = None
-    for t in dict.fromkeys((int(o["tariff_final"][i]), int(r["tariff_final"]), int(tariff0))):
-        e = opop.eval_at(cfg, j, kw, xl, t, int(o["switched"][i]), hourly=hourly)
-        d = abs(e["npv"] - o["npv"][i]) / max(1.0, abs(e["npv"]))
-        if best is None or d < best[0]:
-            best = (d, e)
-    best[1]["nfev"] = int(o["nfev"][i])
-    return best[1]
+    e = opop.eval_at(cfg, j, kw, xl, int(o["tariff_final"][i]), int(o["switched"][i]), hourly=hourly)
+    e["nfev"] = int(o["nfev"][i])
+    return e

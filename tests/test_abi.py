@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(L, name), name
     assert set(names) == set(_lib.EXPORTED)
-    assert L.dgen_abi_version() == _lib.ABI_VERSION == 13
+    assert L.dgen_abi_version() == _lib.ABI_VERSION == 14
     m = re.search(r"#define DGEN_DEFAULT_CHUNKS\s+(\d+)", open(HEADER).read())
     assert m and int(m.group(1)) == _lib.DEFAULT_CHUNKS
     m = re.search(r"#define DGEN_DEFAULT_HOURLY_MONTHS\s+(\d+)", open(HEADER).read())

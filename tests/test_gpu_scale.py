@@ -1,15 +1,19 @@
-"""Oracle spot checks at the configurations' per-GPU sizes:
-C2 (CA-like net billing + storage, 200k agents), C4 (commercial, demand
-charges + battery, 1M agents = 8M / 8 GPUs) and a C5 model-year loop
-(national, 2.5M agents = 20M / 8 GPUs, three years, chunked hourly export).
+"""Oracle checks at the configurations' per-GPU sizes (VERDICT r02 item 3,
+r05 item 1): C2 (CA-like net billing + storage, 200k agents), national mix
+(200k), C3 (1M residential NEM TOU), C4 (commercial, demand charges + battery,
+1M agents = 8M / 8 GPUs) and a C5 model-year loop (national, 2.5M agents =
+20M / 8 GPUs, three years, chunked hourly export).
 
 At these sizes the batch exercises what small parity populations do not:
 net-billing split records near their capacity, envelope overflow fallbacks,
 the two-agent demand-charge build, chunked re-sizing for the state export.
-Each test sizes the whole batch on the GPU and checks a random sample of 150
-agents against the oracle (hourly planes included for C2 / C4); the C5 loop
-checks each year's sizing and Bass step of a sample against the oracle with
-that year's gathered inputs."""
+Each test sizes the whole batch on the GPU in the bench's device order, then
+
+* checks the Brent path of a 20 000-agent sample against the oracle (its
+  OpenMP batch driver): every agent's nfev, system kW and last x (to 1e-9),
+  sticky tariff state and NPV -- no allowance: the certified paths
+  (dgen_set_exact) put every agent on the oracle's path;
+* checks 150 of them in full (bills, payback, battery case, hourly planes)."""
 import numpy as np
 import pytest
 import torch
@@ -22,14 +26,8 @@ from tests import helpers
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 SAMPLE = 150
-
-
-def KNIFE_EDGE_MAX(n):
-    """Agents whose Brent path may leave the oracle's (every one is still
-    compared, at the device's point: helpers.at_device_point): 0.5 % of a
-    sample, at least 1.  The oracle's own path moves on ~0.1-0.3 % of C4 /
-    long-life agents under +-1 ulp of objective noise."""
-    return max(1, n // 200)
+PATH_SAMPLE = 20_000
+PATH_KEYS = ("system_kw", "x_last", "nfev", "npv", "tariff_final", "switched", "status", "payback_period")
 
 
 def _check_sample(pop, out, idx, cfg, demand=None, hourly=True, tag=""):
@@ -39,20 +37,14 @@ def _check_sample(pop, out, idx, cfg, demand=None, hourly=True, tag=""):
     o = {k: out[k].cpu().numpy()[idx] for k in ("system_kw", "npv", "nfev", "payback_period", "batt_kwh",
                                                  "annual_kwh", "npv_pv_batt", "status", "x_last",
                                                  "tariff_final", "switched")}
-    naep = pop.cfs.astype(np.float64).sum(axis=1) / 1e6
     hp = {}
     if hourly:
         ti = torch.as_tensor(idx, device=out["baseline"].device)
         hp = {k: out[k].index_select(1, ti).permute(1, 0, 2).reshape(len(idx), -1).double().cpu().numpy()
               for k in ("baseline", "net_pvonly", "net_with_batt")}
-    flips = []
     for n_j, (j, r) in enumerate(zip(idx, ref)):
         assert o["status"][n_j] == 0 and r["status"] == 0, (tag, j)
-        if not helpers.same_path(o, n_j, r):
-            # a knife-edge agent: checked at the device's own point (helpers)
-            flips.append(j)
-            xa = helpers.xatol_of(pop.cols["load_kwh"][j], naep[pop.cols["cf_row"][j]])
-            r = helpers.at_device_point(o, n_j, opop, n_j, cfg, r, pop.cols["tariff0"][j], xa, hourly=hourly)
+        assert helpers.same_path(o, n_j, r), (tag, j, o["nfev"][n_j], r["nfev"])
         assert np.isclose(o["npv"][n_j], r["npv"], rtol=1e-6, atol=1e-6), (tag, j)
         assert o["payback_period"][n_j] == r["payback_period"], (tag, j)
         assert np.isclose(o["annual_kwh"][n_j], r["annual_kwh"], rtol=1e-9), (tag, j)
@@ -64,16 +56,68 @@ def _check_sample(pop, out, idx, cfg, demand=None, hourly=True, tag=""):
                 ref_h = np.asarray(r[k_r], dtype=np.float64)
                 assert np.allclose(hp[k_o][n_j], ref_h, rtol=2e-6,
                                    atol=2e-6 * max(1.0, np.abs(ref_h).max())), (tag, j, k_o)
-    return flips
 
 
-def _device_sample(out, dev_idx):
+def _path_sample(pop, o, idx, cfg, demand=None, tag=""):
+    """The Brent path of every sampled agent against the oracle's OpenMP
+    batch driver (o: the sample's device outputs, host arrays).  Returns the
+    divergent agents (the callers require none)."""
+    opop = helpers.oracle_population({k: v[idx] for k, v in pop.cols.items()}, pop.tariffs, pop.switches,
+                                     pop.shapes, pop.cfs, pop.wholesale, demand=demand)
+    ref = opop.run_parallel(cfg)
+    div = []
+    for n_j, r in enumerate(ref):
+        assert o["status"][n_j] == 0 and r["status"] == 0, (tag, idx[n_j])
+        if not (helpers.same_path(o, n_j, r) and o["tariff_final"][n_j] == r["tariff_final"]
+                and o["switched"][n_j] == r["switched"]
+                and np.isclose(o["npv"][n_j], r["npv"], rtol=1e-6, atol=1e-6)
+                and o["payback_period"][n_j] == r["payback_period"]):
+            div.append(int(idx[n_j]))
+    print(f"\n{tag}: {len(ref)} sampled agents, Brent-path divergences {len(div)}: {div[:20]}", flush=True)
+    return div
+
+
+def _device_sample(out, dev_idx, hourly=True):
     ti = torch.as_tensor(np.asarray(dev_idx, np.int64), device=out["npv"].device)
     sub = {k: out[k].index_select(0, ti) for k in ("system_kw", "npv", "nfev", "payback_period", "batt_kwh",
                                                    "annual_kwh", "npv_pv_batt", "status", "x_last",
                                                    "tariff_final", "switched")}
-    sub.update({k: out[k].index_select(1, ti) for k in ("baseline", "net_pvonly", "net_with_batt")})
+    if hourly:
+        sub.update({k: out[k].index_select(1, ti) for k in ("baseline", "net_pvonly", "net_with_batt")})
     return sub
+
+
+def _size_at_scale(eng, pop, hourly=True, demand=None):
+    """The whole population sized in the bench's device order; returns
+    (device-order outputs, caller -> device row map, agents listed for the
+    exact re-run)."""
+    eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
+    eng.set_tariffs(pop.tariffs, demand)
+    eng.set_switches(pop.switches)
+    batch = eng.upload_agents(pop.cols, pop.n_scratch, order=profile_order(pop.cols))
+    out = eng.alloc_outputs(batch.n, hourly=hourly)
+    eng.size(batch, out)
+    torch.cuda.synchronize()
+    n_ex = eng.exact_count()
+    assert (out["status"].cpu().numpy() == 0).all()
+    inv = np.empty(batch.n, np.int64)
+    inv[batch.perm] = np.arange(batch.n)
+    print(f"\n{batch.n} agents: {n_ex} re-run in the oracle's arithmetic ({100.0 * n_ex / batch.n:.3f} %)",
+          flush=True)
+    return out, inv, batch
+
+
+def _path_check(pop, out, inv, seed, tag, demand=None, extra=None):
+    from dgen_amd.synth import subset
+    n = len(pop.cols["load_kwh"])
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(n, PATH_SAMPLE, replace=False)
+    if extra is not None:
+        idx = np.concatenate([idx, extra])
+    idx = np.unique(idx)
+    ti = torch.as_tensor(inv[idx], device=out["npv"].device)
+    o = {k: out[k].index_select(0, ti).cpu().numpy() for k in PATH_KEYS}
+    return _path_sample(subset(pop, idx), o, np.arange(idx.size), orc.make_cfg(), demand=demand, tag=tag), idx
 
 
 def test_c2_ca_like_200k_sample_vs_oracle(engine):
@@ -82,86 +126,68 @@ def test_c2_ca_like_200k_sample_vs_oracle(engine):
     from dgen_amd.synth import subset
     n = 200_000
     pop = make_population("ca_res_storage", n, seed=20260000 + 2 + 101)
-    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
-    engine.set_tariffs(pop.tariffs)
-    engine.set_switches(pop.switches)
-    batch = engine.upload_agents(pop.cols, pop.n_scratch, order=profile_order(pop.cols))
+    out, inv, batch = _size_at_scale(engine, pop)
     assert batch.nb_scan
-    out = engine.alloc_outputs(n, hourly=True)
-    engine.size(batch, out)
-    torch.cuda.synchronize()
-    assert (out["status"].cpu().numpy() == 0).all()
-    inv = np.empty(n, np.int64)
-    inv[batch.perm] = np.arange(n)
+    div, _ = _path_check(pop, out, inv, 22, "C2 200k")
+    assert not div, div
     idx = np.sort(np.random.default_rng(12).choice(n, SAMPLE, replace=False))
     sample = _device_sample(out, inv[idx])
     del out, batch
     torch.cuda.empty_cache()
-    flips = _check_sample(subset(pop, idx), sample, np.arange(SAMPLE), orc.make_cfg(), tag="C2")
-    assert len(flips) <= KNIFE_EDGE_MAX(SAMPLE), flips
+    _check_sample(subset(pop, idx), sample, np.arange(SAMPLE), orc.make_cfg(), tag="C2")
 
 
 def test_national_200k_sample_vs_oracle(engine):
     """The national mix at 200k with hourly planes, in the bench's device
     order: NEM bins, the scan-built net-billing split (CA and no-TS agents)
     and the TS sell-rate agents' own scan (k_hourly_batt<TS>) in one batch; a
-    random sample plus TS-path agents against the oracle."""
+    20 000-agent path sample and 150 agents in full (50 on the TS path)."""
     from dgen_amd.engine import path_class
     from dgen_amd.synth import subset
     n = 200_000
     pop = make_population("national_mixed", n, seed=20260000 + 5 + 211)
-    engine.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
-    engine.set_tariffs(pop.tariffs)
-    engine.set_switches(pop.switches)
-    batch = engine.upload_agents(pop.cols, pop.n_scratch, order=profile_order(pop.cols))
+    out, inv, batch = _size_at_scale(engine, pop)
     assert batch.nb_scan and batch.ts_rows[1] > batch.ts_rows[0]
-    out = engine.alloc_outputs(n, hourly=True)
-    engine.size(batch, out)
-    torch.cuda.synchronize()
-    assert (out["status"].cpu().numpy() == 0).all()
-    inv = np.empty(n, np.int64)
-    inv[batch.perm] = np.arange(n)
+    div, _ = _path_check(pop, out, inv, 25, "national 200k")
+    assert not div, div
     rng = np.random.default_rng(15)
     ts = np.flatnonzero(path_class(pop.cols) == 2)
     idx = np.unique(np.concatenate([rng.choice(n, SAMPLE - 50, replace=False), rng.choice(ts, 50, replace=False)]))
     sample = _device_sample(out, inv[idx])
     del out, batch
     torch.cuda.empty_cache()
-    flips = _check_sample(subset(pop, idx), sample, np.arange(idx.size), orc.make_cfg(), tag="national")
-    assert len(flips) <= KNIFE_EDGE_MAX(idx.size), flips
+    _check_sample(subset(pop, idx), sample, np.arange(idx.size), orc.make_cfg(), tag="national")
+
+
+def test_c3_1m_path_sample_vs_oracle(engine):
+    """C3 (the bench workload: 1M residential NEM TOU agents) in the bench's
+    device order: a 20 000-agent Brent-path sample against the oracle."""
+    n = 1_000_000
+    pop = make_population("res_1m_nem_tou", n, seed=20260000 + 3)
+    out, inv, batch = _size_at_scale(engine, pop, hourly=False)
+    div, _ = _path_check(pop, out, inv, 33, "C3 1M")
+    del out, batch
+    torch.cuda.empty_cache()
+    assert not div, div
 
 
 def test_c4_commercial_dc_1m_sample_vs_oracle(engine_dc):
     """C4 per GPU (8M commercial agents over 8 GPUs): demand charges billed
-    (extension mode), battery run, 1000 sampled agents against the oracle --
-    every agent on the oracle's Brent path (nfev, system kW to 1e-9), so NPV,
-    payback, bills and planes are compared for each.  A path diverges only if
-    the objective differs by a few ulps somewhere and scipy's parabolic step
-    amplifies it; the device computes NPV and the payback
-    sums in the oracle's (SSC's) order so that does not happen."""
+    (extension mode), battery run; a 20 000-agent Brent-path sample and 1000
+    agents in full against the oracle, every agent on the oracle's path."""
+    from dgen_amd.synth import subset
     eng = engine_dc
     n = 1_000_000
     pop = make_population("com_dc_batt", n, seed=20260000 + 4 + 101)
-    eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
-    eng.set_tariffs(pop.tariffs, pop.demand)
-    eng.set_switches(pop.switches)
-    batch = eng.upload_agents(pop.cols, pop.n_scratch)
-    out = eng.alloc_outputs(n, hourly=True)
-    eng.size(batch, out)
-    torch.cuda.synchronize()
-    st = out["status"].cpu().numpy()
-    assert (st == 0).all(), np.unique(st)
+    out, inv, batch = _size_at_scale(eng, pop, demand=pop.demand)
+    div, _ = _path_check(pop, out, inv, 44, "C4 1M", demand=pop.demand)
+    assert not div, div
     k = 1000
     idx = np.sort(np.random.default_rng(13).choice(n, k, replace=False))
-    from dgen_amd.synth import subset
-    sample = _device_sample(out, idx)
+    sample = _device_sample(out, inv[idx])
     del out, batch                       # the 1M-agent planes (105 GB) before the next test
     torch.cuda.empty_cache()
-    flips = _check_sample(subset(pop, idx), sample, np.arange(k), orc.make_cfg(),
-                          demand=pop.demand, tag="C4")
-    print(f"\nC4 1M sample: knife-edge agents (Brent path left the oracle's, checked at the device's "
-          f"point) {len(flips)} of {k}: {flips}", flush=True)
-    assert len(flips) <= KNIFE_EDGE_MAX(k), flips
+    _check_sample(subset(pop, idx), sample, np.arange(k), orc.make_cfg(), demand=pop.demand, tag="C4")
 
 
 def test_c5_loop_2p5m_sample_vs_oracle(engine):

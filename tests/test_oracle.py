@@ -437,3 +437,23 @@ def test_eval_at_reproduces_the_search_end():
             assert np.array_equal(e[k], r[k]), (i, k)
         tr, res = orc.brent_trace(opop, cfg, i)
         assert tr.shape[0] == r["nfev"] and tr[-1, 0] == r["x_last"] and res[0]["npv"] == r["npv"]
+
+
+def test_run_parallel_equals_run():
+    """The OpenMP batch driver (Population.run_parallel, the GPU tests' 20 000-
+    agent path samples) returns the sequential driver's results bit for bit."""
+    from dgen_amd.synth import make_population
+    from tests.helpers import oracle_population
+    pop = make_population("national_mixed", 120, n_res_shapes=16, n_com_shapes=8, n_cf=8, n_counties=8,
+                          n_tariffs=16)
+    opop = oracle_population(pop.cols, pop.tariffs, pop.switches, pop.shapes, pop.cfs, pop.wholesale)
+    cfg = orc.make_cfg()
+    a = opop.run(cfg)
+    b = opop.run_parallel(cfg, threads=4)
+    idx = [5, 17, 3]
+    c = opop.run_parallel(cfg, threads=2, idx=idx)
+    for x, y in zip(a, b):
+        for k in x:
+            assert np.array_equal(np.asarray(x[k]), np.asarray(y[k])), k
+    for j, i in enumerate(idx):
+        assert c[j]["system_kw"] == a[i]["system_kw"] and c[j]["nfev"] == a[i]["nfev"]
