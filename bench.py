@@ -171,6 +171,10 @@ def parse():
                          "over the next 24 h (DESIGN.md section 3)")
     ap.add_argument("--no-batt", action="store_true",
                     help="PV-only variant: no PV+battery forward run (SURVEY 8(d)); the reference always runs it")
+    ap.add_argument("--exact", type=int, default=-1, choices=[-1, 0, 1, 2],
+                    help="certified Brent paths (dgen_set_exact): 1 = re-run in the oracle's arithmetic the agents "
+                         "a device / oracle difference bound does not settle, 0 = off, 2 = every agent; -1 (default) "
+                         "= the engine's default (1 in the reference's mode, 0 with demand charges)")
     ap.add_argument("--pmc-dir", default=os.path.join(REPO, "profiles", "pmc"),
                     help="per-workload PMC summaries (traffic field); none -> traffic null")
     return ap.parse_args()
@@ -320,7 +324,8 @@ def main():
     # demand-charge configs run the extension mode; every other config the
     # reference's switch (SKIP_DEMAND_CHARGES = True, ff:35)
     eng = Engine(local if ws > 1 else 0, EngineConfig(skip_demand_charges=pop.skip_demand_charges,
-                                                      batt_update_hours=args.replan_hours))
+                                                      batt_update_hours=args.replan_hours,
+                                                      exact_brent=args.exact))
     if args.chunks is not None:
         eng.set_pipeline(args.chunks)
     if args.hb_months is not None:
@@ -459,7 +464,7 @@ def main():
                        ("profile (cf_row, load_row)" if args.order_major == "cf" else "profile (load_row, cf_row)"),
                        "parallelism": f"dp{ws} (agent shards, no collective in the step)",
                        "agents_with_status_errors": n_bad,
-                       "certified_brent_paths": {"mode": int(eng.cfg.exact_brent),
+                       "certified_brent_paths": {"mode": eng.cfg.exact_mode(),
                                                  "exact_reruns_per_step": n_exact}},
             "roofline": roof, "cpu_baseline": cpu,
         }

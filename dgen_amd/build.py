@@ -166,7 +166,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not needs_build():
         return OUT
     os.makedirs(OUT_DIR, exist_ok=True)
-    defines = []
+    # start from the previous build's withdrawals (a rebuild of unchanged
+    # units then hits the compile cache at once); the guard still scans every
+    # build, and DGEN_GUARD_FRESH=1 starts from none
+    defines, carried_flags = [], {}
+    if os.environ.get("DGEN_GUARD_FRESH", "0") != "1" and os.path.exists(GUARD):
+        try:
+            with open(GUARD) as f:
+                prev = json.load(f)
+            defines = sorted(set(prev.get("withdrawn", [])))
+            carried_flags = dict(prev.get("flagged_first_build") or {}) if defines else {}
+        except (OSError, ValueError):
+            defines, carried_flags = [], {}
     first = None
     for attempt in range(2):
         work, lib, asm = _compile(defines, verbose)
@@ -199,7 +210,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
         finally:
             shutil.rmtree(work, ignore_errors=True)
     with open(GUARD, "w") as f:
-        json.dump({"flagged_first_build": first, "withdrawn": defines,
+        # a withdrawal carried over from the previous build keeps that build's
+        # evidence (the kernel it flagged)
+        json.dump({"flagged_first_build": {**carried_flags, **(first or {})}, "withdrawn": defines,
                    "day_dma_wait_vmcnt": dma_k, "vmem_ops_after_day_dma": dma_issued}, f, indent=1)
     return OUT
 

@@ -52,8 +52,15 @@ class EngineConfig:
     # the reference's hour-order arithmetic every agent whose search a bound on
     # the device / reference objective difference does not settle, so each
     # agent takes the reference's Brent path; 2 re-runs every agent (tests); 0
-    # keeps the fast search alone
-    exact_brent: int = 1
+    # keeps the fast search alone.  -1 (default): 1 in the reference's mode, 0
+    # in the demand-charge extension mode (its piecewise-linear objectives
+    # leave most searches unsettled by the bound)
+    exact_brent: int = -1
+
+    def exact_mode(self) -> int:
+        if self.exact_brent >= 0:
+            return int(self.exact_brent)
+        return 1 if self.skip_demand_charges == 1 else 0
 
     def to_c(self) -> _lib.Cfg:
         d = asdict(self)

@@ -132,7 +132,7 @@ class Engine:
         c = self.cfg.to_c()
         _lib.check(self.lib.dgen_open(self.device, ctypes.byref(c), ctypes.byref(h)), "dgen_open")
         self.ctx = h
-        _lib.check(self.lib.dgen_set_exact(self.ctx, int(self.cfg.exact_brent)), "dgen_set_exact")
+        _lib.check(self.lib.dgen_set_exact(self.ctx, self.cfg.exact_mode()), "dgen_set_exact")
         self.tables = _lib.Tables()
         self.chunks = _lib.DEFAULT_CHUNKS
         self.hb_months = _lib.DEFAULT_HOURLY_MONTHS

@@ -24,10 +24,13 @@ def engine():
 
 @pytest.fixture(scope="session")
 def engine_dc():
-    """Engine in demand-charge extension mode (cfg.skip_demand_charges = 0)."""
+    """Engine in demand-charge extension mode (cfg.skip_demand_charges = 0),
+    certified Brent paths on (the extension mode's default is off: its
+    objectives leave most searches unsettled by the bound, DESIGN.md section 2;
+    the parity tests re-run them)."""
     from dgen_amd.config import EngineConfig
     from dgen_amd.engine import Engine
-    eng = Engine(0, EngineConfig(skip_demand_charges=0))
+    eng = Engine(0, EngineConfig(skip_demand_charges=0, exact_brent=1))
     yield eng
     eng.close()
 
