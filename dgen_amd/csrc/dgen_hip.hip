@@ -5120,6 +5120,14 @@ __device__ __forceinline__ bool bt_sure_eq(double u, double du, int pu, double v
 // when every decision (comparisons, branch tests, the rate switch's
 // thresholds, the final x's to 1e-10) is the oracle's under the model M.
 // The values follow brent_bounded's operations exactly (same x's).
+// bt_replay's undecided comparisons by kind (DGEN_PHASE_PROF builds: phase
+// slots 1 switch thresholds / x order / final x's, 2 fu vs fx, 3 the other
+// point updates, 7 the termination tests, 8 the parabolic step's tests)
+#if DGEN_PHASE_PROF
+#define BT_FAIL(k) do { atomicAdd(&g_phase[k], 1ull); return false; } while (0)
+#else
+#define BT_FAIL(k) return false
+#endif
 __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, double x2, double xatol,
                           const BtModel& M, const dgen_switch* sw, int sw_cnt) {
     const double sqrt_eps = 1.4832396974191326e-08;
@@ -5134,11 +5142,11 @@ __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, dou
     double fx = 0.0, ffulc = 0.0, fnfc = 0.0, dfx = 0.0, dffulc = 0.0, dfnfc = 0.0;
     int num = 0;
     for (;;) {
-        if (num >= nfev || num >= BT_MAX) return false;
+        if (num >= nfev || num >= BT_MAX) BT_FAIL(1);
         // the evaluation at x: the sticky solar switch's row test must agree
-        if (!bt_sure(x, dx, 0.0, 0.0)) return false;
+        if (!bt_sure(x, dx, 0.0, 0.0)) BT_FAIL(8);
         for (int r = 0; r < sw_cnt; r++)
-            if (!bt_sure(x, dx, sw[r].min_kw, 0.0) || !bt_sure(x, dx, sw[r].max_kw, 0.0)) return false;
+            if (!bt_sure(x, dx, sw[r].min_kw, 0.0) || !bt_sure(x, dx, sw[r].max_kw, 0.0)) BT_FAIL(1);
         const double fu = f[num];
         const double dfu = M.c0 + M.c1 * fabs(x) + M.ce * fabs(fu) + M.lip * dx;
         const int px = num;
@@ -5148,8 +5156,8 @@ __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, dou
             fx = fu; ffulc = fu; fnfc = fu;
             dfx = dfu; dffulc = dfu; dfnfc = dfu;
         } else {
-            if (!bt_sure(fu, dfu, fx, dfx)) return false;
-            if (!bt_sure(x, dx, xf, dxf)) return false;
+            if (!bt_sure(fu, dfu, fx, dfx)) BT_FAIL(2);
+            if (!bt_sure(x, dx, xf, dxf)) BT_FAIL(1);
             if (fu <= fx) {
                 if (x >= xf) { a = xf; da = dxf; } else { b = xf; db = dxf; }
                 fulc = nfc; dfulc = dnfc; pfulc = pnfc; ffulc = fnfc; dffulc = dfnfc;
@@ -5161,7 +5169,7 @@ __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, dou
                 // when a decided test settles the ||
                 const bool ca = bt_sure(fu, dfu, fnfc, dfnfc), ra = fu <= fnfc;
                 const bool cb = bt_sure_eq(nfc, dnfc, pnfc, xf, dxf, pxf), rb = nfc == xf;
-                if (!((ca && cb) || (ca && ra) || (cb && rb))) return false;
+                if (!((ca && cb) || (ca && ra) || (cb && rb))) BT_FAIL(3);
                 if (ra || rb) {
                     fulc = nfc; dfulc = dnfc; pfulc = pnfc; ffulc = fnfc; dffulc = dfnfc;
                     nfc = x; dnfc = dx; pnfc = px; fnfc = fu; dfnfc = dfu;
@@ -5170,7 +5178,7 @@ __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, dou
                     const bool cd = bt_sure_eq(fulc, dfulc, pfulc, xf, dxf, pxf), rd = fulc == xf;
                     const bool ce = bt_sure_eq(fulc, dfulc, pfulc, nfc, dnfc, pnfc), re = fulc == nfc;
                     const bool any_true = (cc && rc) || (cd && rd) || (ce && re);
-                    if (!any_true && !(cc && cd && ce)) return false;
+                    if (!any_true && !(cc && cd && ce)) BT_FAIL(3);
                     if (rc || rd || re) { fulc = x; dfulc = dx; pfulc = px; ffulc = fu; dffulc = dfu; }
                 }
             }
@@ -5184,11 +5192,11 @@ __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, dou
         {
             const double lhs = fabs(xf - xm), rhs = tol2 - 0.5 * (b - a);
             const double dl = bt_rnd(dxf + dxm, lhs), dr = bt_rnd(dtol2 + 0.5 * (da + db), rhs);
-            if (!bt_sure(lhs, dl, rhs, dr)) return false;
+            if (!bt_sure(lhs, dl, rhs, dr)) BT_FAIL(7);
             if (!(lhs > rhs)) break;
         }
         bool golden = true, rat_tol = false;
-        if (!bt_sure(fabs(e), de, tol1, dtol1)) return false;
+        if (!bt_sure(fabs(e), de, tol1, dtol1)) BT_FAIL(7);
         if (fabs(e) > tol1) {
             golden = false;
             const bool s1 = pxf == pnfc, s2 = pxf == pfulc;     // exact zero differences
@@ -5215,16 +5223,16 @@ __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, dou
             const double aq = fabs(q);
             const double c1l = fabs(p), c1r = fabs(0.5 * aq * r2);
             const double dc1r = bt_rnd(0.5 * (aq * dr2 + fabs(r2) * dq + dq * dr2), c1r);
-            if (!bt_sure(c1l, dp, c1r, dc1r)) return false;
+            if (!bt_sure(c1l, dp, c1r, dc1r)) BT_FAIL(8);
             bool para = false;
             if (c1l < c1r) {
-                if (!bt_sure(q, dq, 0.0, 0.0)) return false;
+                if (!bt_sure(q, dq, 0.0, 0.0)) BT_FAIL(8);
                 p = q > 0.0 ? -p : p;
                 const double ta = aq * (a - xf), dta = bt_rnd(aq * (da + dxf) + fabs(a - xf) * dq + dq * (da + dxf), ta);
-                if (!bt_sure(p, dp, ta, dta)) return false;
+                if (!bt_sure(p, dp, ta, dta)) BT_FAIL(8);
                 if (p > ta) {
                     const double tb = aq * (b - xf), dtb = bt_rnd(aq * (db + dxf) + fabs(b - xf) * dq + dq * (db + dxf), tb);
-                    if (!bt_sure(p, dp, tb, dtb)) return false;
+                    if (!bt_sure(p, dp, tb, dtb)) BT_FAIL(8);
                     para = p < tb;
                 }
             } else if (q > 0.0) {
@@ -5242,10 +5250,10 @@ __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, dou
                 const double bx = b - x, dbx = bt_rnd(db + dx, bx);
                 const bool c1 = bt_sure(xa, dxa, tol2, dtol2), r1 = xa < tol2;
                 const bool c2 = bt_sure(bx, dbx, tol2, dtol2), r2b = bx < tol2;
-                if (!((c1 && c2) || (c1 && r1) || (c2 && r2b))) return false;
+                if (!((c1 && c2) || (c1 && r1) || (c2 && r2b))) BT_FAIL(8);
                 if (r1 || r2b) {
                     const double dm = xm - xf, ddm = bt_rnd(dxm + dxf, dm);
-                    if (!bt_sure(dm, ddm, 0.0, 0.0)) return false;
+                    if (!bt_sure(dm, ddm, 0.0, 0.0)) BT_FAIL(8);
                     const double si = np_sign(dm) + ((dm == 0.0) ? 1.0 : 0.0);
                     rat = tol1 * si;
                     drat = dtol1;
@@ -5256,25 +5264,25 @@ __device__ bool bt_replay(const double* __restrict__ f, int nfev, double x1, dou
             }
         }
         if (golden) {
-            if (!bt_sure(xf, dxf, xm, dxm)) return false;
+            if (!bt_sure(xf, dxf, xm, dxm)) BT_FAIL(8);
             if (xf >= xm) { e = a - xf; de = bt_rnd(da + dxf, e); }
             else { e = b - xf; de = bt_rnd(db + dxf, e); }
             rat = golden_mean * e;
             drat = bt_rnd(golden_mean * de, rat);
         }
-        if (!bt_sure(rat, drat, 0.0, 0.0)) return false;
+        if (!bt_sure(rat, drat, 0.0, 0.0)) BT_FAIL(8);
         const double si = np_sign(rat) + ((rat == 0.0) ? 1.0 : 0.0);
         const double ar = fabs(rat);
-        if (!rat_tol && !bt_sure(ar, drat, tol1, dtol1)) return false;
+        if (!rat_tol && !bt_sure(ar, drat, tol1, dtol1)) BT_FAIL(8);
         const bool big = ar > tol1;
         x = xf + si * (big ? ar : tol1);
         dx = bt_rnd(dxf + (big ? drat : dtol1), x);
     }
-    if (num != nfev) return false;
+    if (num != nfev) BT_FAIL(1);
     // the reported x's (system_kw = xf, x_last) within 1e-7 of the oracle's
     // under the bound (the decisions above fix the path; the observed
     // differences of certified agents are ~1e-13)
-    if (dxf > 1e-7 * fmax(1.0, fabs(xf)) || dx_last > 1e-7 * fmax(1.0, fabs(x))) return false;
+    if (dxf > 1e-7 * fmax(1.0, fabs(xf)) || dx_last > 1e-7 * fmax(1.0, fabs(x))) BT_FAIL(1);
     return true;
 }
 
@@ -5402,13 +5410,20 @@ k_brent_certify(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, int6
 // ---------------------------------------------------------------------------
 // k_size_exact: the listed agents' searches in the oracle's arithmetic.  One
 // block per agent at a time (the blocks stride over the list).  Per tariff the
-// block lists each month's hours by period (time order kept within a period);
-// per evaluation a lane per (year, month, period) bin sums that bin's hours in
-// time order -- the hours of one bin are a subsequence of the month's, so the
-// sum is oracle bin_year's own -- then a thread per year bills its months in
-// order (year_bill, year_demand) and thread 0 runs the cash flow
-// (orc_cashloan).  The search state and the objective are block-uniform
-// (scalar branches).
+// block lists each month's hours by period (time order kept within a period:
+// the hours of one bin are a subsequence of the month's, so a bin summed over
+// its list in list order is oracle bin_year's own sum).  Per evaluation a wave
+// takes one (month, period) bin at a time with lane = analysis year: the
+// wave stages the bin's hours 64 at a time in LDS (load, this evaluation's
+// generation, TS rate; every hour's generation formed once, by one lane) and
+// each lane walks them in order with its year's degradation factor, so all
+// years of the bin share one pass over its hours (broadcast LDS reads).  A
+// thread per year then bills its months in order (year_bill, year_demand) and
+// thread 0 runs the cash flow (orc_cashloan).  The search state and the
+// objective are block-uniform (scalar branches).
+// (v4, one lane per (year, month, period) cell gathering its hours from global
+// memory through the hour list, was latency-bound: national 200k, 7 163 agents
+// listed, 80 ms.)
 // ---------------------------------------------------------------------------
 // a block-uniform double (every thread holds the same value, read from LDS):
 // readfirstlane makes it a scalar, so the search's branches on it are scalar
@@ -5464,33 +5479,53 @@ __device__ __forceinline__ double ex_dc_tier(double peak, const double* cap, con
     return charge;
 }
 
-// Scratch of k_size_exact: per block slot, in global memory, the agent's
-// hourly load and TS sell rate, this evaluation's hourly generation and the
-// tariff's hour lists; in LDS the bins of a block of yb years, the per-year
-// bill state and the cash-flow rows.  A cell is (year, month, period), years
-// fastest (a wave's lanes read the same hours); its lane sums that bin's hours
-// in time order from the hour lists (the hours of one period are a
-// subsequence of the month's, so each sum is oracle bin_year's own).
+// Scratch of k_size_exact.  Per block slot, in global memory: the current
+// tariff's hour list -- per month, period 0's hours, then period 1's, ...,
+// each in time order -- with every listed hour's load, generation per kW and
+// TS sell rate in list order (so an evaluation streams them contiguously),
+// and the bins of every analysis year.  In LDS: the list offsets, each wave's
+// stage of 64 hours, the per-year bill state and the cash-flow rows.
 constexpr int EX_THREADS = 256;
-constexpr int EX_BLOCKS = 2048;
-constexpr size_t EX_WS_BYTES = (size_t)3 * NH * sizeof(double) + (size_t)NH * sizeof(uint16_t) +
-                               (size_t)12 * (2 * MAXP + 1) * sizeof(int32_t);
+constexpr int EX_BLOCKS = 1024;
+constexpr int EX_HOFF = MAXP + 1;                  // list offsets per month
+static_assert(MAXY <= 64, "k_size_exact: one lane per analysis year");
+__host__ __device__ inline size_t ex_ws_base() {
+    return ((size_t)3 * NH * sizeof(double) + (size_t)NH * sizeof(uint16_t) + 255) / 256 * 256;
+}
+__host__ __device__ inline size_t ex_ws_bytes(int P, bool dcb) {
+    const size_t bins = (size_t)MAXY * 12 * (size_t)P * (3 + (dcb ? (size_t)DCP : 0)) * sizeof(double);
+    return ex_ws_base() + (bins + 255) / 256 * 256;
+}
 struct ExLds {
-    double* Lh;        // [8760] hourly load (global)
-    double* Gh;        // [8760] hourly generation at this evaluation's kW (global)
-    double* TSh;       // [8760] TS sell rate (global)
-    uint16_t* hl;      // [8760] per month, the hours of period 0, then 1, ... (each in time order; global)
-    int32_t* hoff;     // [12][2 MAXP + 1] list offsets (absolute), then fill cursors (global)
-    double* bins;      // [yb][12][2 P]: mo 0/1 net | mo 4 load, gen | mo 2/3 import, export ($ with TS)
-    double* cmax;      // [yb][12][P] each bin's largest import (the month peak: their max, from 0)
-    double* dcm;       // [yb][12][P][DCP] each bin's largest import per demand period (billed demand only)
-    double* yr;        // [yb][2 MAXP] per-year-thread credit / billed kWh
-    double* res;       // [6][MAXY + 1] aev, bill_w, bill_wo, cf_payback, cf_energy_value, atcf; + 8 scalars
+    double* Lp;        // [8760] load of the listed hours, list order (global)
+    double* Cp;        // [8760] generation per kW (cf / 1e6) of the listed hours (global)
+    double* Tp;        // [8760] TS sell rate of the listed hours (global)
+    uint16_t* hl;      // [8760] the hour list (global)
+    int32_t* hoff;     // [12][EX_HOFF] list offsets (absolute; LDS)
+    double* bins;      // [MAXY][12][2 P]: mo 0/1 net | mo 4 load, gen | mo 2/3 import, export ($ with TS) (global)
+    double* cmax;      // [MAXY][12][P] each bin's largest import (the month peak: their max, from 0) (global)
+    double* dcm;       // [MAXY][12][P][DCP] each bin's largest import per demand period (billed demand only; global)
+    double* stg;       // [waves][4][256] the wave's staged hours: load, generation, TS rate, demand period (LDS)
+    double* yr;        // [MAXY][2 MAXP] per-year-thread credit / billed kWh (LDS)
+    double* res;       // [6][MAXY + 1] aev, bill_w, bill_wo, cf_payback, cf_energy_value, atcf; + 8 scalars (LDS)
 };
 
-__host__ __device__ inline size_t ex_lds_bytes(int P, int yb, bool dcb) {
-    const size_t per_year = (size_t)12 * (3 * (size_t)P + (dcb ? (size_t)P * DCP : 0)) + 2 * MAXP;
-    return sizeof(double) * ((size_t)yb * per_year + 6 * (size_t)(MAXY + 1) + 8);
+__host__ __device__ inline size_t ex_lds_bytes() {
+    return sizeof(double) * ((size_t)(EX_THREADS / 64) * 4 * 256 + (size_t)MAXY * 2 * MAXP + 6 * (size_t)(MAXY + 1) + 8) +
+           sizeof(int32_t) * (size_t)12 * EX_HOFF;   // = ex_stg + ex_yr + ex_res + ex_hoff
+}
+
+// The LDS parts at fixed offsets of dyn_lds (the compiler then knows they
+// are LDS and emits ds_* accesses; through the generic pointers of a struct
+// they became flat loads with memory-path latency)
+constexpr size_t EX_STG_QW = (size_t)(EX_THREADS / 64) * 4 * 256;
+constexpr size_t EX_YR_QW = (size_t)MAXY * 2 * MAXP;
+constexpr size_t EX_RES_QW = 6 * (size_t)(MAXY + 1) + 8;
+__device__ __forceinline__ double* ex_stg(int wv) { return dyn_lds + (size_t)wv * 4 * 256; }
+__device__ __forceinline__ double* ex_yr() { return dyn_lds + EX_STG_QW; }
+__device__ __forceinline__ double* ex_res() { return dyn_lds + EX_STG_QW + EX_YR_QW; }
+__device__ __forceinline__ int32_t* ex_hoff() {
+    return reinterpret_cast<int32_t*>(dyn_lds + EX_STG_QW + EX_YR_QW + EX_RES_QW);
 }
 
 struct ExAgent {
@@ -5498,34 +5533,63 @@ struct ExAgent {
     int n_demand;
     bool dc_on;
     bool has_ts;
-    int N, yb;
+    int N;
     double rate_base, sys_base, yearend;
 };
 
-// the hour lists of tariff t (thread m < 12: month m; once per tariff)
+// the hour list of tariff t: wave w takes months w, w + waves, ...; lanes =
+// the month's hours 64 at a time, a ballot per period (lane order = time order)
 __device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L) {
     const int P = t.P;
-    for (int m = threadIdx.x; m < 12; m += blockDim.x) {
-        int32_t* off = L.hoff + m * (2 * MAXP + 1);
-        int32_t* cur = off + MAXP + 1;
-        for (int p = 0; p <= P; p++) off[p] = 0;
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
+    for (int m = wv; m < 12; m += nw) {
         const int h0 = c_month_start_day[m] * 24, h1 = c_month_start_day[m + 1] * 24;
-        for (int i = h0; i < h1; i++) {
+        int cnt = 0;                                   // lane p < P: hours of period p
+        for (int c = h0; c < h1; c += WAVE) {
+            const int i = c + lane;
             const int hh = i % 24;
-            const int p = ((i % 168) >= 120) ? t.wkend[m][hh] : t.wkday[m][hh];
-            off[p + 1] += 1;
+            const int per = i < h1 ? (((i % 168) >= 120) ? t.wkend[m][hh] : t.wkday[m][hh]) : -1;
+            for (int p = 0; p < P; p++) {
+                const unsigned long long b = __ballot(per == p);
+                if (lane == p) cnt += __popcll(b);
+            }
         }
-        off[0] = h0;
-        for (int p = 0; p < P; p++) {
-            off[p + 1] += off[p];
-            cur[p] = off[p];
+        // exclusive prefix over the period lanes
+        int incl = lane < P ? cnt : 0;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const int v = __shfl_up(incl, o, WAVE);
+            if (lane >= o) incl += v;
         }
-        for (int i = h0; i < h1; i++) {
+        int cur = h0 + incl - (lane < P ? cnt : 0);    // lane p: first position of period p
+        if (lane <= P) ex_hoff()[m * EX_HOFF + lane] = lane < P ? cur : h1;
+        for (int c = h0; c < h1; c += WAVE) {
+            const int i = c + lane;
             const int hh = i % 24;
-            const int p = ((i % 168) >= 120) ? t.wkend[m][hh] : t.wkday[m][hh];
-            L.hl[cur[p]] = (uint16_t)i;
-            cur[p] += 1;
+            const int per = i < h1 ? (((i % 168) >= 120) ? t.wkend[m][hh] : t.wkday[m][hh]) : -1;
+            int pos = 0;
+            for (int p = 0; p < P; p++) {
+                const unsigned long long b = __ballot(per == p);
+                const int base = __shfl(cur, p, WAVE);
+                if (per == p) pos = base + __popcll(b & below);
+                if (lane == p) cur += __popcll(b);
+            }
+            if (per >= 0) L.hl[pos] = (uint16_t)i;
         }
+    }
+}
+
+// the listed hours' load (elec.py:571-577 scale_array_sum), generation per kW
+// (cf / 1e6, ff:350) and TS sell rate (ff:182,246,372 x multiplier,
+// float32-rounded) in list order (after ex_hour_lists and a hand-off)
+__device__ void ex_list_values(const ExLds& L, const float* __restrict__ sh, double S, double kwh,
+                               const int32_t* __restrict__ cfr, const double* __restrict__ wrow, double pmul) {
+    for (int k = threadIdx.x; k < NH; k += blockDim.x) {
+        const int h = L.hl[k];
+        L.Lp[k] = ((double)sh[h] / S) * kwh;
+        L.Cp[k] = cf_per_kw(cfr[h]);
+        L.Tp[k] = wrow ? (double)(float)(wrow[h] * pmul) : 0.0;
     }
 }
 
@@ -5537,99 +5601,179 @@ __device__ __forceinline__ void ex_handoff() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
-// bin_year's bins of years [y0, y0 + ny) (gen == false: the no-system year 0).
-// Rounds of blockDim cells; within a round every lane walks the wave's longest
-// hour list (a lane past its own list adds exact zeros), so the loops are
-// wave-uniform: no exec-masked branches.
-__device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int y0, int ny, bool gen,
-                         const ExLds& L) {
+// bin_year's bins of years [0, ny) (GEN false: the no-system year 0, at
+// kW 0).  Lane = year.  Wave w takes a contiguous run of the 12 P (month,
+// period) bins -- a contiguous run of the list -- and streams it 64 hours at
+// a time through its LDS stage (the next 64 in flight while these are
+// walked; each hour's generation at kW formed once, by the lane that stages
+// it); every lane adds the hours of a bin in list order, the oracle's order,
+// and writes the bin where the next one starts.  One instantiation per
+// billing form, so an hour costs only its form's operations: EX_NEM (options
+// 0 / 1: the net kWh), EX_BA (4: load and generation), EX_NB (2 / 3: import,
+// export, x the TS rate when TS); PK: the bins' largest imports (kWh/kW tier
+// units 1 / 3, demand charges), DEM: per demand period too.  Every sum is the
+// oracle bin_year's (a skipped sum is one the bill never reads).
+constexpr int EX_NEM = 0, EX_BA = 1, EX_NB = 2;
+constexpr int EX_R = 4, EX_CH = EX_R * 64;         // hours per lane / per chunk
+template <int FORM, bool GEN, bool PK, bool DEM, bool TS>
+__device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
+                       const ExLds& L) {
     const int P = t.P;
-    const int cells = ny * 12 * P;
-    const bool ts = a.has_ts && t.mo == 2;
-    const bool mo01 = t.mo == 0 || t.mo == 1, mo4 = t.mo == 4;
-    for (int c0 = 0; c0 < cells; c0 += blockDim.x) {
-        const int c = c0 + (int)threadIdx.x;
-        const bool act = c < cells;
-        const int cc = act ? c : 0;
-        const int yl = cc % ny, mp = cc / ny;
-        const int m = mp / P, p = mp % P;
-        const double s = pow_seq(a.sys_base, y0 + yl);
-        const int32_t* off = L.hoff + m * (2 * MAXP + 1);
-        const int k0 = off[p];
-        const int len = act ? off[p + 1] - k0 : 0;
-        int lmax = len;
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    const double s = pow_seq(a.sys_base, lane);        // the lane's year's degradation factor
+    double* const sL = ex_stg(wv);
+    double* const sG = sL + EX_CH;
+    double* const sT = sG + EX_CH;
+    int* const sQ = reinterpret_cast<int*>(sT + EX_CH);
+    const int nb = 12 * P;
+    const int bA = (wv * nb) / nw, bB = ((wv + 1) * nb) / nw;
+    // list position where bin b starts (b == nb: the end of the list)
+    auto bstart = [&](int b) __attribute__((always_inline)) -> int {
+        const int m = b / P;
+        return b >= nb ? NH : __builtin_amdgcn_readfirstlane(ex_hoff()[m * EX_HOFF + (b - m * P)]);
+    };
+    if (bA >= bB) return;
+    const int kA = bstart(bA), kB = bstart(bB);
+    int b = bA, kn = bstart(bA + 1), m = bA / P;
+    double b0 = 0.0, b1 = 0.0, mx = 0.0;
+    double dq[DEM ? DCP : 1];
 #pragma unroll
-        for (int o = WAVE / 2; o > 0; o >>= 1) {
-            const int v = __shfl_xor(lmax, o, WAVE);
-            lmax = v > lmax ? v : lmax;
-        }
-        lmax = __builtin_amdgcn_readfirstlane(lmax);
-        double b0 = 0.0, b1 = 0.0, mx = 0.0;
-        double dq[DCP];
-#pragma unroll
-        for (int q = 0; q < DCP; q++) dq[q] = 0.0;
-        // branch-free (selects): a bin the hour does not feed, or an hour past
-        // the lane's list, adds an exact +0.0 (the import / export sums only
-        // grow from +0.0, so x + 0.0 == x)
-        auto hour = [&](bool ok, int i, double ld, double gv, double tv) __attribute__((always_inline)) {
-            const double g = gen ? gv * s : 0.0;
-            const double dd = ld - g;
-            mx = (ok && dd > mx) ? dd : mx;
-            const bool imp = dd > 0.0;
-            const double ex = -dd;
-            const double xv = ts ? ex * tv : ex;
-            const double a0v = mo01 ? dd : (mo4 ? ld : (imp ? dd : 0.0));
-            const double a1v = mo4 ? g : ((mo01 || imp) ? 0.0 : xv);
-            b0 += ok ? a0v : 0.0;
-            b1 += ok ? a1v : 0.0;
-            if (dem) {            // year_demand's TOU peaks: maxima, any order
-                const int hh = i % 24;
-                const int q = ((i % 168) >= 120) ? dem->wkend[m][hh] : dem->wkday[m][hh];
-#pragma unroll
-                for (int k = 0; k < DCP; k++) {
-                    const double up = (ok && dd > dq[k]) ? dd : dq[k];
-                    dq[k] = (k == q) ? up : dq[k];
-                }
-            }
-        };
-        constexpr int HB = 8;     // loads in flight
-        for (int j = 0; j < lmax; j += HB) {
-            int ix[HB];
-            bool ok[HB];
-            double lv[HB], gv[HB], tv[HB];
-#pragma unroll
-            for (int jj = 0; jj < HB; jj++) {
-                ok[jj] = j + jj < len;
-                const int kk = k0 + (ok[jj] ? j + jj : 0);
-                ix[jj] = L.hl[kk < NH ? kk : NH - 1];
-            }
-#pragma unroll
-            for (int jj = 0; jj < HB; jj++) {
-                lv[jj] = L.Lh[ix[jj]];
-                gv[jj] = gen ? L.Gh[ix[jj]] : 0.0;
-                tv[jj] = ts ? L.TSh[ix[jj]] : 0.0;
-            }
-#pragma unroll
-            for (int jj = 0; jj < HB; jj++) hour(ok[jj], ix[jj], lv[jj], gv[jj], tv[jj]);
-        }
-        if (act) {
-            double* bn = L.bins + ((size_t)yl * 12 + m) * 2 * P;
+    for (int q = 0; q < (DEM ? DCP : 1); q++) dq[q] = 0.0;
+    auto flush = [&]() __attribute__((always_inline)) {
+        if (lane < ny) {
+            const int p = b - m * P;
+            double* bn = L.bins + ((size_t)lane * 12 + m) * 2 * P;
             bn[p] = b0;
             bn[P + p] = b1;
-            L.cmax[((size_t)yl * 12 + m) * P + p] = mx;
-            if (dem) {
+            L.cmax[((size_t)lane * 12 + m) * P + p] = mx;
+            if constexpr (DEM) {
 #pragma unroll
-                for (int q = 0; q < DCP; q++) L.dcm[(((size_t)yl * 12 + m) * P + p) * DCP + q] = dq[q];
+                for (int q = 0; q < DCP; q++) L.dcm[(((size_t)lane * 12 + m) * P + p) * DCP + q] = dq[q];
             }
         }
+        b0 = 0.0; b1 = 0.0; mx = 0.0;
+#pragma unroll
+        for (int q = 0; q < (DEM ? DCP : 1); q++) dq[q] = 0.0;
+        b += 1;
+        kn = bstart(b + 1);
+        m = b / P;
+    };
+    // one hour, the oracle's operations (imports and exports as selects)
+    auto step = [&](int j) __attribute__((always_inline)) {
+        const double ld = sL[j];
+        const double g = GEN ? sG[j] * s : 0.0;
+        const double dd = ld - g;
+        if constexpr (PK) mx = dd > mx ? dd : mx;
+        if constexpr (FORM == EX_NEM) {
+            b0 += dd;
+        } else if constexpr (FORM == EX_BA) {
+            b0 += ld;
+            b1 += g;
+        } else {
+            const bool imp = dd > 0.0;
+            const double ex = -dd;
+            const double xv = TS ? ex * sT[j] : ex;
+            b0 += imp ? dd : 0.0;
+            b1 += imp ? 0.0 : xv;
+        }
+        if constexpr (DEM) {      // year_demand's TOU peaks: maxima, any order
+            const int q = sQ[j];
+#pragma unroll
+            for (int k = 0; k < DCP; k++) {
+                const double up = dd > dq[k] ? dd : dq[k];
+                dq[k] = (k == q) ? up : dq[k];
+            }
+        }
+    };
+    // the hour's demand period: from the hour and its month
+    auto dper = [&](int k) __attribute__((always_inline)) -> int {
+        const int i = L.hl[k];
+        int mm = 0;
+        while (mm < 11 && i >= c_month_start_day[mm + 1] * 24) mm++;
+        const int hh = i % 24;
+        return ((i % 168) >= 120) ? dem->wkend[mm][hh] : dem->wkday[mm][hh];
+    };
+    // chunks of EX_CH hours (EX_R per lane); the next chunk's values in
+    // registers while this one is walked (a chunk's walk outlasts the loads'
+    // latency from L2 / MALL)
+    double lv[EX_R], cv[EX_R], tv[EX_R];
+    int qv[EX_R];
+    auto fetch = [&](int c0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < EX_R; r++) {
+            const int kk = c0 + r * WAVE + lane;
+            const bool v = kk < kB;
+            lv[r] = v ? L.Lp[kk] : 0.0;
+            if constexpr (GEN) cv[r] = v ? L.Cp[kk] : 0.0;
+            if constexpr (TS) tv[r] = v ? L.Tp[kk] : 0.0;
+            if constexpr (DEM) qv[r] = v ? dper(kk) : 0;
+        }
+    };
+    fetch(kA);
+    for (int c = kA; c < kB; c += EX_CH) {
+        const int n = (kB - c) < EX_CH ? (kB - c) : EX_CH;
+        wave_lds_sync();                               // the previous chunk's reads
+#pragma unroll
+        for (int r = 0; r < EX_R; r++) {
+            const int o = r * WAVE + lane;
+            sL[o] = lv[r];
+            // ff:117-120 generation of the hour at kW, oracle perf_no_batt's order
+            if constexpr (GEN) sG[o] = ref_gen(cv[r], kw);
+            if constexpr (TS) sT[o] = tv[r];
+            if constexpr (DEM) sQ[o] = qv[r];
+        }
+        wave_lds_sync();
+        if (c + EX_CH < kB) fetch(c + EX_CH);          // the next chunk in flight
+        int j = 0;
+        while (j < n) {
+            while (c + j == kn) flush();               // the bins that end here (empty ones too)
+            const int je = (kn - c) < n ? (kn - c) : n;
+            for (; j + 4 <= je; j += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) step(j + u);
+            }
+            for (; j < je; j++) step(j);
+        }
+    }
+    // the run's last bin and any empty bins after it
+    while (b < bB) flush();
+}
+
+template <bool GEN>
+__device__ void ex_cells_g(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
+                           const ExLds& L) {
+    const bool pk = dem != nullptr || t.unit == 1 || t.unit == 3;
+    const bool ts = a.has_ts && t.mo == 2;
+    if (t.mo == 0 || t.mo == 1) {
+        if (dem) ex_run<EX_NEM, GEN, true, true, false>(a, t, dem, ny, kw, L);
+        else if (pk) ex_run<EX_NEM, GEN, true, false, false>(a, t, dem, ny, kw, L);
+        else ex_run<EX_NEM, GEN, false, false, false>(a, t, dem, ny, kw, L);
+    } else if (t.mo == 4) {
+        if (dem) ex_run<EX_BA, GEN, true, true, false>(a, t, dem, ny, kw, L);
+        else if (pk) ex_run<EX_BA, GEN, true, false, false>(a, t, dem, ny, kw, L);
+        else ex_run<EX_BA, GEN, false, false, false>(a, t, dem, ny, kw, L);
+    } else if (ts) {
+        if (dem) ex_run<EX_NB, GEN, true, true, true>(a, t, dem, ny, kw, L);
+        else if (pk) ex_run<EX_NB, GEN, true, false, true>(a, t, dem, ny, kw, L);
+        else ex_run<EX_NB, GEN, false, false, true>(a, t, dem, ny, kw, L);
+    } else {
+        if (dem) ex_run<EX_NB, GEN, true, true, false>(a, t, dem, ny, kw, L);
+        else if (pk) ex_run<EX_NB, GEN, true, false, false>(a, t, dem, ny, kw, L);
+        else ex_run<EX_NB, GEN, false, false, false>(a, t, dem, ny, kw, L);
     }
 }
 
+__device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, bool gen,
+                         double kw, const ExLds& L) {
+    if (gen) ex_cells_g<true>(a, t, dem, ny, kw, L);
+    else ex_cells_g<false>(a, t, dem, ny, kw, L);
+}
+
 // oracle year_bill (+ year_demand) of year y0 + yl from its cells
-__device__ double ex_year_bill(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int yl,
+__device__ __forceinline__ double ex_year_bill(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int yl,
                                const ExLds& L) {
     const int P = t.P;
-    double* credit = L.yr + (size_t)yl * 2 * MAXP;
+    double* credit = ex_yr() + (size_t)yl * 2 * MAXP;
     double* u = credit + MAXP;
     for (int p = 0; p < MAXP; p++) credit[p] = 0.0;
     const bool ts = a.has_ts && t.mo == 2;
@@ -5776,39 +5920,124 @@ __device__ void ex_cashloan(const dgen_agents& A, const dgen_cfg& cfg, int64_t i
     *pb_out = pb;
 }
 
-__global__ void __launch_bounds__(EX_THREADS)
+// orc_cashloan with the years on the block's threads: thread y (1 .. N)
+// forms year y's flows with the sequential form's operations (the loan
+// balance entering year y by the same recursion from year 1), thread 0 then
+// runs the NPV (Horner from year N) and payback chains over them.  Returns
+// npv, payback through sc[1], sc[2] (LDS; read after a barrier).
+__device__ void ex_cashloan_par(const dgen_agents& A, const dgen_cfg& cfg, int64_t i, int N, double C,
+                                const double* aev, double* cf_payback, double* cf_ev, double* atcf, double* sc) {
+    const bool is_res = (A.flags[i] & 1) != 0;
+    const int market = is_res ? 0 : 1;
+    const int depr_type = is_res ? 0 : 2;
+    const double infl = (A.inflation[i] * 100.0) * 0.01;
+    const double real = (A.real_discount[i] * 100.0) * 0.01;
+    const double nom = (1.0 + real) * (1.0 + infl) - 1.0;
+    const double fed = ((A.tax_rate[i] * 100.0) * 0.7) * 0.01, sta = ((A.tax_rate[i] * 100.0) * 0.3) * 0.01;
+    const double debt = (100.0 - (A.down_payment[i] * 100.0)) * 0.01 * C;
+    const double r = cfg.loan_rate_pct * 0.01;
+    const int term = A.loan_term[i];
+    double pmt = 0.0;
+    if (term > 0 && debt != 0.0) {
+        if (r != 0.0) {
+            const double f = pow_seq(1.0 + r, term);
+            pmt = debt * r / (1.0 - 1.0 / f);
+        } else {
+            pmt = debt / (double)term;
+        }
+    }
+    double itc = A.itc_frac[i] * 0.01 * C;
+    if (itc > cfg.itc_fed_max) itc = cfg.itc_fed_max;
+    const double basis = C - 0.5 * itc;
+    const double ins = cfg.insurance_rate_pct * 0.01 * C;
+    const int y = (int)threadIdx.x;
+    if (y == 0) {
+        atcf[0] = -(C - debt);
+        cf_payback[0] = -C;
+        cf_ev[0] = 0.0;
+    } else if (y <= N) {
+        double balance = debt;
+        const bool pays = pmt != 0.0;
+        for (int k = 1; k < y; k++)
+            if (k <= term && pays) balance = balance - (pmt - balance * r);
+        const double ev = aev[y];
+        const double oe = ins * pow_seq(1.0 + infl, y - 1);
+        double interest = 0.0, payment = 0.0;
+        if (y <= term && pays) {
+            interest = balance * r;
+            payment = pmt;
+        }
+        const double itc_y = (y == 1) ? itc : 0.0;
+        double sta_tax = 0.0, fed_tax = 0.0;
+        if (market != 0) {
+            const double dep = depr_frac(depr_type, y, cfg.depr_sl_years) * basis;
+            sta_tax = sta * (ev - oe - interest - dep);
+            fed_tax = fed * (ev - oe - interest - dep - sta_tax);
+        }
+        const double taxsav = itc_y - sta_tax - fed_tax;
+        atcf[y] = ev - oe - payment + taxsav;
+        cf_payback[y] = ev - oe + taxsav;
+        cf_ev[y] = ev;
+    }
+    __syncthreads();
+    if (y == 0) {
+        const double rr = 1.0 / (1.0 + nom);
+        double acc = 0.0;
+        for (int k = N; k > 0; k--) acc = rr * acc + atcf[k];
+        sc[1] = atcf[0] + acc * rr;
+        double cum = cf_payback[0];
+        double pb = 1e99;
+        for (int k = 1; k <= N; k++) {
+            cum += cf_payback[k];
+            if (cum > 0.0) {
+                pb = (cf_payback[k] != 0.0) ? (double)k - cum / cf_payback[k] : (double)k - 0.5;
+                break;
+            }
+        }
+        sc[2] = pb;
+    }
+}
+
+__global__ void __launch_bounds__(EX_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
 k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const int32_t* __restrict__ list,
-             char* exws, int yb) {
+             char* exws, int64_t wsb, int lds_ny) {
     const int cnt = list[0];
     ExLds L;
     {
-        char* g = exws + (size_t)blockIdx.x * EX_WS_BYTES;
-        L.Lh = reinterpret_cast<double*>(g);
-        L.Gh = L.Lh + NH;
-        L.TSh = L.Gh + NH;
-        L.hl = reinterpret_cast<uint16_t*>(L.TSh + NH);
-        L.hoff = reinterpret_cast<int32_t*>(L.hl + NH);
-        double* d = dyn_lds;
+        char* g = exws + (size_t)blockIdx.x * (size_t)wsb;
         const int P = T.max_periods > 0 && T.max_periods <= MAXP ? T.max_periods : MAXP;
         const bool dcb = cfg.skip_demand_charges == 0 && T.n_demand > 0;
-        L.bins = d; d += (size_t)yb * 12 * 2 * P;
-        L.cmax = d; d += (size_t)yb * 12 * P;
-        L.dcm = dcb ? d : nullptr; d += dcb ? (size_t)yb * 12 * P * DCP : 0;
-        L.yr = d; d += (size_t)yb * 2 * MAXP;
-        L.res = d;
+        L.Lp = reinterpret_cast<double*>(g);
+        L.Cp = L.Lp + NH;
+        L.Tp = L.Cp + NH;
+        L.hl = reinterpret_cast<uint16_t*>(L.Tp + NH);
+        L.bins = reinterpret_cast<double*>(g + ex_ws_base());
+        L.cmax = L.bins + (size_t)MAXY * 12 * 2 * P;
+        L.dcm = dcb ? L.cmax + (size_t)MAXY * 12 * P : nullptr;
+        double* d = dyn_lds;
+        L.stg = ex_stg(0);
+        L.yr = ex_yr();
+        L.res = ex_res();
+        L.hoff = ex_hoff();
+        if (lds_ny > 0) {
+            // the bins of lds_ny (>= every listed agent's N) years in LDS
+            double* e = reinterpret_cast<double*>(L.hoff + 12 * EX_HOFF);
+            L.bins = e;
+            L.cmax = e + (size_t)lds_ny * 12 * 2 * P;
+            L.dcm = dcb ? L.cmax + (size_t)lds_ny * 12 * P : nullptr;
+        }
     }
-    double* const aev = L.res;
-    double* const bw = L.res + (MAXY + 1);
-    double* const bwo = L.res + 2 * (MAXY + 1);
-    double* const cfpb = L.res + 3 * (MAXY + 1);
-    double* const cfev = L.res + 4 * (MAXY + 1);
-    double* const atcf = L.res + 5 * (MAXY + 1);
-    double* const sc = L.res + 6 * (MAXY + 1);          // [0] wo1, [1] npv, [2] payback
+    double* const aev = ex_res();
+    double* const bw = aev + (MAXY + 1);
+    double* const bwo = aev + 2 * (MAXY + 1);
+    double* const cfpb = aev + 3 * (MAXY + 1);
+    double* const cfev = aev + 4 * (MAXY + 1);
+    double* const atcf = aev + 5 * (MAXY + 1);
+    double* const sc = aev + 6 * (MAXY + 1);          // [0] wo1, [1] npv, [2] payback
     ExAgent a;
     a.demand = T.demand;
     a.n_demand = T.n_demand;
     a.dc_on = cfg.skip_demand_charges == 0;
-    a.yb = yb;
     a.yearend = cfg.nm_yearend_sell_rate;
     for (int w = blockIdx.x; w < cnt; w += gridDim.x) {
         const int64_t i = __builtin_amdgcn_readfirstlane(list[1 + w]);
@@ -5821,18 +6050,10 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
         a.has_ts = !is_ca && wr >= 0 && T.wholesale != nullptr;
         a.rate_base = 1.0 + (A.inflation[i] * 100.0) * 0.01 + (A.escalator[i] * 100.0) * 0.01;
         a.sys_base = 1.0 - (A.pv_deg[i] * 100.0) * 0.01;
-        // hourly load (elec.py:571-577 scale_array_sum) and TS sell rate
-        // (ff:182,246,372 x multiplier, float32-rounded), once per agent
-        {
-            const double S = T.shape_sum[lr];
-            const float* sh = T.shapes + (int64_t)lr * NH;
-            const double* wrow = a.has_ts ? T.wholesale + (int64_t)wr * NH : nullptr;
-            const double pmul = A.price_mult[i];
-            for (int h = threadIdx.x; h < NH; h += blockDim.x) {
-                L.Lh[h] = ((double)sh[h] / S) * kwh;
-                if (wrow) L.TSh[h] = (double)(float)(wrow[h] * pmul);
-            }
-        }
+        const double S = T.shape_sum[lr];
+        const float* sh = T.shapes + (int64_t)lr * NH;
+        const double* wrow = a.has_ts ? T.wholesale + (int64_t)wr * NH : nullptr;
+        const double pmul = A.price_mult[i];
         const int32_t* cfr = T.cfs + (int64_t)cr * NH;
         const double naep0 = T.cf_naep[cr];
         const double max_load = kwh / naep0;
@@ -5848,9 +6069,6 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
         int wo_tag = -1;
         double wo1 = 0.0, total = 0.0, npv = 0.0, pb = 0.0;
         auto perf = [&](double kw) __attribute__((always_inline)) -> double {
-            // ff:117-120 generation per hour, oracle perf_no_batt's order
-            for (int h = threadIdx.x; h < NH; h += blockDim.x)
-                L.Gh[h] = (((cf_per_kw(cfr[h]) * kw) * 1000.0) * 0.96) / 1000.0;
             double otc = 0.0;
             if (kw > 0.0) {
                 int nt;
@@ -5863,30 +6081,37 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
             }
             const dgen_tariff& t = T.tariffs[tariff];
             const dgen_demand* dem = (a.dc_on && t.dc > 0 && t.dc <= a.n_demand) ? a.demand + (t.dc - 1) : nullptr;
+            PH_T0(tw);
             if (wo_tag != tariff) {
                 // the tariff's hour lists and its no-system bill (orc_ur5's wo1)
-                __syncthreads();
+                __syncthreads();                          // the previous lists' and bins' readers
                 ex_hour_lists(t, L);
                 ex_handoff();
-                ex_cells(a, t, dem, 0, 1, false, L);
-                __syncthreads();
+                ex_list_values(L, sh, S, kwh, cfr, wrow, pmul);
+                ex_handoff();
+                ex_cells(a, t, dem, 1, false, 0.0, L);
+                ex_handoff();
                 if (threadIdx.x == 0) sc[0] = ex_year_bill(a, t, dem, 0, L);
                 __syncthreads();
                 wo1 = ex_uniform(sc[0]);
                 wo_tag = tariff;
-            } else {
-                ex_handoff();
             }
-            for (int y0 = 0; y0 < a.N; y0 += a.yb) {
-                const int ny = a.N - y0 < a.yb ? a.N - y0 : a.yb;
-                __syncthreads();
-                ex_cells(a, t, dem, y0, ny, true, L);
-                __syncthreads();
-                const int yl = (int)threadIdx.x;
-                if (yl < ny) {
-                    const int y = y0 + yl;
+            // (phase slots 4, 5, 6, 10, 11: the exact re-run's cells, year
+            // bills, cash flow, tariff set-up and evaluations; DGEN_PHASE_PROF)
+            PH_ADD(10, tw, threadIdx.x == 0);
+            PH_CNT(11, 1, threadIdx.x == 0);
+            // the analysis years' bins (lane = year, N <= MAXY <= 64), then a
+            // thread per year bills them
+            PH_T0(tc);
+            ex_cells(a, t, dem, a.N, true, kw, L);
+            ex_handoff();
+            PH_ADD(4, tc, threadIdx.x == 0);
+            PH_T0(ty);
+            {
+                const int y = (int)threadIdx.x;
+                if (y < a.N) {
                     const double r = pow_seq(a.rate_base, y);
-                    const double wb = ex_year_bill(a, t, dem, yl, L);
+                    const double wb = ex_year_bill(a, t, dem, y, L);
                     const double wv = wb * r;
                     const double wo = wo1 * r;
                     bw[y + 1] = wv;
@@ -5895,17 +6120,17 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
                 }
             }
             __syncthreads();
+            PH_ADD(5, ty, threadIdx.x == 0);
+            PH_T0(tf);
             total = ((A.capex[i] * kw + 0.0) * A.ccm[i]) + 0.0 + otc;
             if (threadIdx.x == 0) {
                 aev[0] = 0.0;
                 bw[0] = 0.0;
                 bwo[0] = 0.0;
-                double v, q;
-                ex_cashloan(A, cfg, i, a.N, total, aev, cfpb, cfev, atcf, &v, &q);
-                sc[1] = v;
-                sc[2] = q;
             }
+            ex_cashloan_par(A, cfg, i, a.N, total, aev, cfpb, cfev, atcf, sc);
             __syncthreads();
+            PH_ADD(6, tf, threadIdx.x == 0);
             npv = ex_uniform(sc[1]);
             pb = ex_uniform(sc[2]);
             return -npv;
@@ -6025,7 +6250,9 @@ struct dgen_ctx {
     // certified Brent paths (dgen_set_exact): the search traces, the listed
     // agents per chunk, the exact re-run's per-block hour scratch
     int exact = 1;
-    char* ex_ws = nullptr;         // [EX_BLOCKS][EX_WS_BYTES]
+    char* ex_ws = nullptr;         // [EX_BLOCKS][ex_ws_bytes(P, demand)]
+    size_t ex_ws_cap = 0;
+    int lds_max = 65536;           // the device's LDS per work-group (hipDeviceAttributeMaxSharedMemoryPerBlock)
     double* bt_buf = nullptr;      // [n][BT_MAX] objective values
     size_t bt_cap = 0;
     int32_t* ex_list = nullptr;    // chunk j: [i0 + j] count, then its rows
@@ -6107,6 +6334,13 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
     if (!c) { set_err("dgen_open: out of host memory"); return DGEN_E_ARG; }
     c->device = device;
     c->cfg = *cfg;
+    {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && v > 0)
+            c->lds_max = v;
+        else
+            (void)hipGetLastError();
+    }
     c->head = 0; c->pending = 0; c->count = 0;
     c->chunks = DGEN_DEFAULT_CHUNKS;
     c->hb_months = DGEN_DEFAULT_HOURLY_MONTHS;
@@ -6316,15 +6550,30 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             HIP_TRY(hipMalloc(&c->ex_list, (size_t)(n + dgen_ctx::MAXCH) * sizeof(int32_t)));
             c->ex_list_cap = (size_t)(n + dgen_ctx::MAXCH) * sizeof(int32_t);
         }
-        if (!c->ex_ws) HIP_TRY(hipMalloc(&c->ex_ws, (size_t)EX_BLOCKS * EX_WS_BYTES));
     }
-    // the exact re-run's block: the bins of yb years within 32 KB of LDS
+    // the exact re-run's per-block scratch (its bins sized by the table's
+    // periods and the demand records)
     const bool ex_dcb = c->cfg.skip_demand_charges == 0 && T->n_demand > 0;
     const int ex_P = (T->max_periods > 0 && T->max_periods <= MAXP) ? T->max_periods : MAXP;
-    int ex_yb = MAXY;
-    while (ex_yb > 1 && ex_lds_bytes(ex_P, ex_yb, ex_dcb) > 32768) ex_yb--;
+    const size_t ex_wsb = ex_ws_bytes(ex_P, ex_dcb);
+    if (exact_on && (size_t)EX_BLOCKS * ex_wsb > c->ex_ws_cap) {
+        if (c->ex_ws) HIP_TRY(hipFree(c->ex_ws));
+        c->ex_ws = nullptr;
+        c->ex_ws_cap = 0;
+        HIP_TRY(hipMalloc(&c->ex_ws, (size_t)EX_BLOCKS * ex_wsb));
+        c->ex_ws_cap = (size_t)EX_BLOCKS * ex_wsb;
+    }
     const int ex_threads = EX_THREADS;
-    const size_t ex_lds = ex_lds_bytes(ex_P, ex_yb, ex_dcb);
+    // the bins in LDS when the batch's analysis years and the table's periods
+    // fit the device's work-group LDS (the year bills then read LDS), else in
+    // the block's global scratch
+    const int ex_ny = (A->max_years >= 1 && A->max_years <= MAXY) ? A->max_years : MAXY;
+    const size_t ex_bins_lds = sizeof(double) * (size_t)ex_ny * 12 * (size_t)ex_P * (3 + (ex_dcb ? (size_t)DCP : 0));
+    const bool ex_lb = ex_lds_bytes() + ex_bins_lds <= (size_t)c->lds_max;
+    const size_t ex_lds = ex_lds_bytes() + (ex_lb ? ex_bins_lds : 0);
+    if (exact_on && ex_lds > 65536)
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(k_size_exact),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)ex_lds));
     double* const bt = exact_on ? c->bt_buf : nullptr;
     if (c->pending == dgen_ctx::RING) {   // fold the oldest record before reuse
         int r = fold_one(c, c->head);
@@ -6525,7 +6774,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             hipLaunchKernelGGL(k_brent_certify, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, *T, *A, *O,
                                c->cfg, i0, i1, bt, lst, c->exact);
             hipLaunchKernelGGL(k_size_exact, dim3((unsigned)(m < EX_BLOCKS ? m : EX_BLOCKS)), dim3(ex_threads),
-                               ex_lds, s, *T, *A, *O, c->cfg, lst, c->ex_ws, ex_yb);
+                               ex_lds, s, *T, *A, *O, c->cfg, lst, c->ex_ws, (int64_t)ex_wsb, ex_lb ? ex_ny : 0);
         }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
@@ -6632,8 +6881,12 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
         const dim3 tsgrid(1);
         (void)hts; (void)tsa; (void)tsb; (void)tsgrid;
         const dim3 hgrid((unsigned)((m + BLOCK - 1) / BLOCK));
-        for (int m0 = 0; rep_mask && m0 < 12; m0 += c->hb_months) {
-            const int m1 = m0 + c->hb_months < 12 ? m0 + c->hb_months : 12;
+        // one launch over the whole year: the pass runs only the agents whose
+        // split or record overflowed (none in most calls), so a month-segmented
+        // sweep's L2 reuse buys nothing and its 12 launches over the chunk's
+        // rows cost ~8 us each (national 200k: 12 of them per step)
+        for (int m0 = 0; rep_mask && m0 < 12; m0 += 12) {
+            const int m1 = 12;
             if (hourly && O->hourly_f64) DGEN_HB_LAUNCH(true, true, true);
             else if (hourly) DGEN_HB_LAUNCH(true, false, true);
             else DGEN_HB_LAUNCH(false, false, true);
