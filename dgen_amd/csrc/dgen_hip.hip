@@ -5488,12 +5488,12 @@ __device__ __forceinline__ double ex_dc_tier(double peak, const double* cap, con
 constexpr int EX_THREADS = 256;
 constexpr int EX_BLOCKS = 1024;
 constexpr int EX_HOFF = MAXP + 1;                  // list offsets per month
-static_assert(MAXY <= 64, "k_size_exact: one lane per analysis year");
+static_assert(MAXY + 1 <= 64, "k_size_exact: one lane per analysis year and the no-system year");
 __host__ __device__ inline size_t ex_ws_base() {
     return ((size_t)3 * NH * sizeof(double) + (size_t)NH * sizeof(uint16_t) + 255) / 256 * 256;
 }
 __host__ __device__ inline size_t ex_ws_bytes(int P, bool dcb) {
-    const size_t bins = (size_t)MAXY * 12 * (size_t)P * (3 + (dcb ? (size_t)DCP : 0)) * sizeof(double);
+    const size_t bins = (size_t)(MAXY + 1) * 12 * (size_t)P * (3 + (dcb ? (size_t)DCP : 0)) * sizeof(double);
     return ex_ws_base() + (bins + 255) / 256 * 256;
 }
 struct ExLds {
@@ -5511,7 +5511,7 @@ struct ExLds {
 };
 
 __host__ __device__ inline size_t ex_lds_bytes() {
-    return sizeof(double) * ((size_t)(EX_THREADS / 64) * 4 * 256 + (size_t)MAXY * 2 * MAXP + 6 * (size_t)(MAXY + 1) + 8) +
+    return sizeof(double) * ((size_t)(EX_THREADS / 64) * 4 * 256 + (size_t)(MAXY + 1) * 2 * MAXP + 6 * (size_t)(MAXY + 1) + 8) +
            sizeof(int32_t) * (size_t)12 * EX_HOFF;   // = ex_stg + ex_yr + ex_res + ex_hoff
 }
 
@@ -5519,7 +5519,7 @@ __host__ __device__ inline size_t ex_lds_bytes() {
 // are LDS and emits ds_* accesses; through the generic pointers of a struct
 // they became flat loads with memory-path latency)
 constexpr size_t EX_STG_QW = (size_t)(EX_THREADS / 64) * 4 * 256;
-constexpr size_t EX_YR_QW = (size_t)MAXY * 2 * MAXP;
+constexpr size_t EX_YR_QW = (size_t)(MAXY + 1) * 2 * MAXP;
 constexpr size_t EX_RES_QW = 6 * (size_t)(MAXY + 1) + 8;
 __device__ __forceinline__ double* ex_stg(int wv) { return dyn_lds + (size_t)wv * 4 * 256; }
 __device__ __forceinline__ double* ex_yr() { return dyn_lds + EX_STG_QW; }
@@ -5537,19 +5537,31 @@ struct ExAgent {
     double rate_base, sys_base, yearend;
 };
 
-// the hour list of tariff t: wave w takes months w, w + waves, ...; lanes =
-// the month's hours 64 at a time, a ballot per period (lane order = time order)
-__device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L) {
+// The hour list of tariff t and the listed hours' values: wave w takes
+// months w, w + waves, ...; lanes = the month's hours 64 at a time (a ballot
+// per period: lane order = time order); the month's two day-type schedules
+// come in once (lanes 0-47) and each lane takes its hour's period by a
+// shuffle.  Every hour's load (elec.py:571-577 scale_array_sum), generation
+// per kW (cf / 1e6, ff:350) and TS sell rate (ff:182,246,372 x multiplier,
+// float32-rounded) are read in time order and written at the hour's list
+// position.
+__device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L, const float* __restrict__ sh, double S,
+                              double kwh, const int32_t* __restrict__ cfr, const double* __restrict__ wrow,
+                              double pmul) {
     const int P = t.P;
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
     const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (WAVE - lane));
     for (int m = wv; m < 12; m += nw) {
         const int h0 = c_month_start_day[m] * 24, h1 = c_month_start_day[m + 1] * 24;
+        const int sched = lane < 24 ? (int)t.wkday[m][lane] : (lane < 48 ? (int)t.wkend[m][lane - 24] : 0);
+        auto period = [&](int i) __attribute__((always_inline)) -> int {
+            const int src = (((i % 168) >= 120) ? 24 : 0) + i % 24;
+            const int pr = __shfl(sched, src, WAVE);
+            return i < h1 ? pr : -1;
+        };
         int cnt = 0;                                   // lane p < P: hours of period p
         for (int c = h0; c < h1; c += WAVE) {
-            const int i = c + lane;
-            const int hh = i % 24;
-            const int per = i < h1 ? (((i % 168) >= 120) ? t.wkend[m][hh] : t.wkday[m][hh]) : -1;
+            const int per = period(c + lane);
             for (int p = 0; p < P; p++) {
                 const unsigned long long b = __ballot(per == p);
                 if (lane == p) cnt += __popcll(b);
@@ -5566,8 +5578,11 @@ __device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L) {
         if (lane <= P) ex_hoff()[m * EX_HOFF + lane] = lane < P ? cur : h1;
         for (int c = h0; c < h1; c += WAVE) {
             const int i = c + lane;
-            const int hh = i % 24;
-            const int per = i < h1 ? (((i % 168) >= 120) ? t.wkend[m][hh] : t.wkday[m][hh]) : -1;
+            const bool in = i < h1;
+            const float shv = in ? sh[i] : 0.0f;
+            const int32_t cfv = in ? cfr[i] : 0;
+            const double whv = (in && wrow) ? wrow[i] : 0.0;
+            const int per = period(i);
             int pos = 0;
             for (int p = 0; p < P; p++) {
                 const unsigned long long b = __ballot(per == p);
@@ -5575,21 +5590,13 @@ __device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L) {
                 if (per == p) pos = base + __popcll(b & below);
                 if (lane == p) cur += __popcll(b);
             }
-            if (per >= 0) L.hl[pos] = (uint16_t)i;
+            if (per >= 0) {
+                L.hl[pos] = (uint16_t)i;
+                L.Lp[pos] = ((double)shv / S) * kwh;
+                L.Cp[pos] = cf_per_kw(cfv);
+                L.Tp[pos] = wrow ? (double)(float)(whv * pmul) : 0.0;
+            }
         }
-    }
-}
-
-// the listed hours' load (elec.py:571-577 scale_array_sum), generation per kW
-// (cf / 1e6, ff:350) and TS sell rate (ff:182,246,372 x multiplier,
-// float32-rounded) in list order (after ex_hour_lists and a hand-off)
-__device__ void ex_list_values(const ExLds& L, const float* __restrict__ sh, double S, double kwh,
-                               const int32_t* __restrict__ cfr, const double* __restrict__ wrow, double pmul) {
-    for (int k = threadIdx.x; k < NH; k += blockDim.x) {
-        const int h = L.hl[k];
-        L.Lp[k] = ((double)sh[h] / S) * kwh;
-        L.Cp[k] = cf_per_kw(cfr[h]);
-        L.Tp[k] = wrow ? (double)(float)(wrow[h] * pmul) : 0.0;
     }
 }
 
@@ -5617,10 +5624,13 @@ constexpr int EX_NEM = 0, EX_BA = 1, EX_NB = 2;
 constexpr int EX_R = 4, EX_CH = EX_R * 64;         // hours per lane / per chunk
 template <int FORM, bool GEN, bool PK, bool DEM, bool TS>
 __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
-                       const ExLds& L) {
+                       const ExLds& L, int nsl) {
     const int P = t.P;
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
-    const double s = pow_seq(a.sys_base, lane);        // the lane's year's degradation factor
+    // the lane's year's degradation factor; lane nsl (when >= 0): the
+    // no-system year, factor 0 -- its generation term is +-0, so every sum
+    // is the kW-0 pass's (load - 0 == load)
+    const double s = lane == nsl ? 0.0 : pow_seq(a.sys_base, lane);
     double* const sL = ex_stg(wv);
     double* const sG = sL + EX_CH;
     double* const sT = sG + EX_CH;
@@ -5640,7 +5650,7 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
 #pragma unroll
     for (int q = 0; q < (DEM ? DCP : 1); q++) dq[q] = 0.0;
     auto flush = [&]() __attribute__((always_inline)) {
-        if (lane < ny) {
+        if (lane < ny || lane == nsl) {
             const int p = b - m * P;
             double* bn = L.bins + ((size_t)lane * 12 + m) * 2 * P;
             bn[p] = b0;
@@ -5661,7 +5671,8 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
     // one hour, the oracle's operations (imports and exports as selects)
     auto step = [&](int j) __attribute__((always_inline)) {
         const double ld = sL[j];
-        const double g = GEN ? sG[j] * s : 0.0;
+        // (option 4 sums the generation itself: the no-system lane's is +0)
+        const double g = GEN ? ((FORM == EX_BA && lane == nsl) ? 0.0 : sG[j] * s) : 0.0;
         const double dd = ld - g;
         if constexpr (PK) mx = dd > mx ? dd : mx;
         if constexpr (FORM == EX_NEM) {
@@ -5739,34 +5750,27 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
     while (b < bB) flush();
 }
 
-template <bool GEN>
-__device__ void ex_cells_g(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
-                           const ExLds& L) {
+__device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
+                         const ExLds& L, int nsl) {
     const bool pk = dem != nullptr || t.unit == 1 || t.unit == 3;
     const bool ts = a.has_ts && t.mo == 2;
     if (t.mo == 0 || t.mo == 1) {
-        if (dem) ex_run<EX_NEM, GEN, true, true, false>(a, t, dem, ny, kw, L);
-        else if (pk) ex_run<EX_NEM, GEN, true, false, false>(a, t, dem, ny, kw, L);
-        else ex_run<EX_NEM, GEN, false, false, false>(a, t, dem, ny, kw, L);
+        if (dem) ex_run<EX_NEM, true, true, true, false>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NEM, true, true, false, false>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NEM, true, false, false, false>(a, t, dem, ny, kw, L, nsl);
     } else if (t.mo == 4) {
-        if (dem) ex_run<EX_BA, GEN, true, true, false>(a, t, dem, ny, kw, L);
-        else if (pk) ex_run<EX_BA, GEN, true, false, false>(a, t, dem, ny, kw, L);
-        else ex_run<EX_BA, GEN, false, false, false>(a, t, dem, ny, kw, L);
+        if (dem) ex_run<EX_BA, true, true, true, false>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_BA, true, true, false, false>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_BA, true, false, false, false>(a, t, dem, ny, kw, L, nsl);
     } else if (ts) {
-        if (dem) ex_run<EX_NB, GEN, true, true, true>(a, t, dem, ny, kw, L);
-        else if (pk) ex_run<EX_NB, GEN, true, false, true>(a, t, dem, ny, kw, L);
-        else ex_run<EX_NB, GEN, false, false, true>(a, t, dem, ny, kw, L);
+        if (dem) ex_run<EX_NB, true, true, true, true>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NB, true, true, false, true>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NB, true, false, false, true>(a, t, dem, ny, kw, L, nsl);
     } else {
-        if (dem) ex_run<EX_NB, GEN, true, true, false>(a, t, dem, ny, kw, L);
-        else if (pk) ex_run<EX_NB, GEN, true, false, false>(a, t, dem, ny, kw, L);
-        else ex_run<EX_NB, GEN, false, false, false>(a, t, dem, ny, kw, L);
+        if (dem) ex_run<EX_NB, true, true, true, false>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NB, true, true, false, false>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NB, true, false, false, false>(a, t, dem, ny, kw, L, nsl);
     }
-}
-
-__device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, bool gen,
-                         double kw, const ExLds& L) {
-    if (gen) ex_cells_g<true>(a, t, dem, ny, kw, L);
-    else ex_cells_g<false>(a, t, dem, ny, kw, L);
 }
 
 // oracle year_bill (+ year_demand) of year y0 + yl from its cells
@@ -6012,15 +6016,15 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
         L.Tp = L.Cp + NH;
         L.hl = reinterpret_cast<uint16_t*>(L.Tp + NH);
         L.bins = reinterpret_cast<double*>(g + ex_ws_base());
-        L.cmax = L.bins + (size_t)MAXY * 12 * 2 * P;
-        L.dcm = dcb ? L.cmax + (size_t)MAXY * 12 * P : nullptr;
+        L.cmax = L.bins + (size_t)(MAXY + 1) * 12 * 2 * P;
+        L.dcm = dcb ? L.cmax + (size_t)(MAXY + 1) * 12 * P : nullptr;
         double* d = dyn_lds;
         L.stg = ex_stg(0);
         L.yr = ex_yr();
         L.res = ex_res();
         L.hoff = ex_hoff();
         if (lds_ny > 0) {
-            // the bins of lds_ny (>= every listed agent's N) years in LDS
+            // the bins of lds_ny (>= every listed agent's N + 1) years in LDS
             double* e = reinterpret_cast<double*>(L.hoff + 12 * EX_HOFF);
             L.bins = e;
             L.cmax = e + (size_t)lds_ny * 12 * 2 * P;
@@ -6082,42 +6086,41 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
             const dgen_tariff& t = T.tariffs[tariff];
             const dgen_demand* dem = (a.dc_on && t.dc > 0 && t.dc <= a.n_demand) ? a.demand + (t.dc - 1) : nullptr;
             PH_T0(tw);
-            if (wo_tag != tariff) {
-                // the tariff's hour lists and its no-system bill (orc_ur5's wo1)
-                __syncthreads();                          // the previous lists' and bins' readers
-                ex_hour_lists(t, L);
+            const bool need_wo = wo_tag != tariff;
+            if (need_wo) {
+                // the tariff's hour list (its no-system bill, orc_ur5's wo1,
+                // comes with this evaluation's bins below)
+                __syncthreads();                          // the previous list's and bins' readers
+                ex_hour_lists(t, L, sh, S, kwh, cfr, wrow, pmul);
                 ex_handoff();
-                ex_list_values(L, sh, S, kwh, cfr, wrow, pmul);
-                ex_handoff();
-                ex_cells(a, t, dem, 1, false, 0.0, L);
-                ex_handoff();
-                if (threadIdx.x == 0) sc[0] = ex_year_bill(a, t, dem, 0, L);
-                __syncthreads();
-                wo1 = ex_uniform(sc[0]);
-                wo_tag = tariff;
             }
             // (phase slots 4, 5, 6, 10, 11: the exact re-run's cells, year
             // bills, cash flow, tariff set-up and evaluations; DGEN_PHASE_PROF)
             PH_ADD(10, tw, threadIdx.x == 0);
             PH_CNT(11, 1, threadIdx.x == 0);
-            // the analysis years' bins (lane = year, N <= MAXY <= 64), then a
+            // the analysis years' bins (lane = year, N < MAXY + 1 <= 64) and,
+            // with a new tariff, the no-system year's on lane N, then a
             // thread per year bills them
             PH_T0(tc);
-            ex_cells(a, t, dem, a.N, true, kw, L);
+            ex_cells(a, t, dem, a.N, kw, L, need_wo ? a.N : -1);
             ex_handoff();
             PH_ADD(4, tc, threadIdx.x == 0);
             PH_T0(ty);
-            {
-                const int y = (int)threadIdx.x;
-                if (y < a.N) {
-                    const double r = pow_seq(a.rate_base, y);
-                    const double wb = ex_year_bill(a, t, dem, y, L);
-                    const double wv = wb * r;
-                    const double wo = wo1 * r;
-                    bw[y + 1] = wv;
-                    bwo[y + 1] = wo;
-                    aev[y + 1] = wo - wv;
-                }
+            const int y = (int)threadIdx.x;
+            if (y < a.N) bw[y + 1] = ex_year_bill(a, t, dem, y, L);
+            else if (need_wo && y == a.N) sc[0] = ex_year_bill(a, t, dem, a.N, L);
+            __syncthreads();
+            if (need_wo) {
+                wo1 = ex_uniform(sc[0]);
+                wo_tag = tariff;
+            }
+            if (y < a.N) {
+                const double r = pow_seq(a.rate_base, y);
+                const double wv = bw[y + 1] * r;
+                const double wo = wo1 * r;
+                bw[y + 1] = wv;
+                bwo[y + 1] = wo;
+                aev[y + 1] = wo - wv;
             }
             __syncthreads();
             PH_ADD(5, ty, threadIdx.x == 0);
@@ -6568,7 +6571,8 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     // fit the device's work-group LDS (the year bills then read LDS), else in
     // the block's global scratch
     const int ex_ny = (A->max_years >= 1 && A->max_years <= MAXY) ? A->max_years : MAXY;
-    const size_t ex_bins_lds = sizeof(double) * (size_t)ex_ny * 12 * (size_t)ex_P * (3 + (ex_dcb ? (size_t)DCP : 0));
+    // (N + 1 years: the no-system year rides on lane N)
+    const size_t ex_bins_lds = sizeof(double) * (size_t)(ex_ny + 1) * 12 * (size_t)ex_P * (3 + (ex_dcb ? (size_t)DCP : 0));
     const bool ex_lb = ex_lds_bytes() + ex_bins_lds <= (size_t)c->lds_max;
     const size_t ex_lds = ex_lds_bytes() + (ex_lb ? ex_bins_lds : 0);
     if (exact_on && ex_lds > 65536)
@@ -6774,7 +6778,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             hipLaunchKernelGGL(k_brent_certify, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, *T, *A, *O,
                                c->cfg, i0, i1, bt, lst, c->exact);
             hipLaunchKernelGGL(k_size_exact, dim3((unsigned)(m < EX_BLOCKS ? m : EX_BLOCKS)), dim3(ex_threads),
-                               ex_lds, s, *T, *A, *O, c->cfg, lst, c->ex_ws, (int64_t)ex_wsb, ex_lb ? ex_ny : 0);
+                               ex_lds, s, *T, *A, *O, c->cfg, lst, c->ex_ws, (int64_t)ex_wsb, ex_lb ? ex_ny + 1 : 0);
         }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
