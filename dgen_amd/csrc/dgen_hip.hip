@@ -5508,6 +5508,9 @@ struct ExLds {
     double* stg;       // [waves][4][256] the wave's staged hours: load, generation, TS rate, demand period (LDS)
     double* yr;        // [MAXY][2 MAXP] per-year-thread credit / billed kWh (LDS)
     double* res;       // [6][MAXY + 1] aev, bill_w, bill_wo, cf_payback, cf_energy_value, atcf; + 8 scalars (LDS)
+    int bny;           // the bins' year stride (LDS: the batch's N + 1; global: MAXY + 1)
+    int ptab;          // the table's periods (the bins' layout)
+    bool dcb;          // dcm present
 };
 
 __host__ __device__ inline size_t ex_lds_bytes() {
@@ -5526,6 +5529,23 @@ __device__ __forceinline__ double* ex_yr() { return dyn_lds + EX_STG_QW; }
 __device__ __forceinline__ double* ex_res() { return dyn_lds + EX_STG_QW + EX_YR_QW; }
 __device__ __forceinline__ int32_t* ex_hoff() {
     return reinterpret_cast<int32_t*>(dyn_lds + EX_STG_QW + EX_YR_QW + EX_RES_QW);
+}
+// the bins, their peaks and demand-period peaks: LB, in LDS after the list
+// offsets (ds_* accesses: the year bills' reads are latency-bound), else the
+// block's global scratch
+struct ExB {
+    double* bins;
+    double* cmax;
+    double* dcm;
+};
+template <bool LB>
+__device__ __forceinline__ ExB ex_b(const double* gbins, int bny, int P, bool dcb) {
+    ExB b;
+    if constexpr (LB) b.bins = reinterpret_cast<double*>(ex_hoff() + 12 * EX_HOFF);
+    else b.bins = const_cast<double*>(gbins);
+    b.cmax = b.bins + (size_t)bny * 12 * 2 * P;
+    b.dcm = dcb ? b.cmax + (size_t)bny * 12 * P : nullptr;
+    return b;
 }
 
 struct ExAgent {
@@ -5622,10 +5642,11 @@ __device__ __forceinline__ void ex_handoff() {
 // oracle bin_year's (a skipped sum is one the bill never reads).
 constexpr int EX_NEM = 0, EX_BA = 1, EX_NB = 2;
 constexpr int EX_R = 4, EX_CH = EX_R * 64;         // hours per lane / per chunk
-template <int FORM, bool GEN, bool PK, bool DEM, bool TS>
+template <int FORM, bool GEN, bool PK, bool DEM, bool TS, bool LB>
 __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
                        const ExLds& L, int nsl) {
     const int P = t.P;
+    const ExB B = ex_b<LB>(L.bins, L.bny, L.ptab, L.dcb);
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
     // the lane's year's degradation factor; lane nsl (when >= 0): the
     // no-system year, factor 0 -- its generation term is +-0, so every sum
@@ -5652,13 +5673,13 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
     auto flush = [&]() __attribute__((always_inline)) {
         if (lane < ny || lane == nsl) {
             const int p = b - m * P;
-            double* bn = L.bins + ((size_t)lane * 12 + m) * 2 * P;
+            double* bn = B.bins + ((size_t)lane * 12 + m) * 2 * P;
             bn[p] = b0;
             bn[P + p] = b1;
-            L.cmax[((size_t)lane * 12 + m) * P + p] = mx;
+            B.cmax[((size_t)lane * 12 + m) * P + p] = mx;
             if constexpr (DEM) {
 #pragma unroll
-                for (int q = 0; q < DCP; q++) L.dcm[(((size_t)lane * 12 + m) * P + p) * DCP + q] = dq[q];
+                for (int q = 0; q < DCP; q++) B.dcm[(((size_t)lane * 12 + m) * P + p) * DCP + q] = dq[q];
             }
         }
         b0 = 0.0; b1 = 0.0; mx = 0.0;
@@ -5750,41 +5771,44 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
     while (b < bB) flush();
 }
 
+template <bool LB>
 __device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
                          const ExLds& L, int nsl) {
     const bool pk = dem != nullptr || t.unit == 1 || t.unit == 3;
     const bool ts = a.has_ts && t.mo == 2;
     if (t.mo == 0 || t.mo == 1) {
-        if (dem) ex_run<EX_NEM, true, true, true, false>(a, t, dem, ny, kw, L, nsl);
-        else if (pk) ex_run<EX_NEM, true, true, false, false>(a, t, dem, ny, kw, L, nsl);
-        else ex_run<EX_NEM, true, false, false, false>(a, t, dem, ny, kw, L, nsl);
+        if (dem) ex_run<EX_NEM, true, true, true, false, LB>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NEM, true, true, false, false, LB>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NEM, true, false, false, false, LB>(a, t, dem, ny, kw, L, nsl);
     } else if (t.mo == 4) {
-        if (dem) ex_run<EX_BA, true, true, true, false>(a, t, dem, ny, kw, L, nsl);
-        else if (pk) ex_run<EX_BA, true, true, false, false>(a, t, dem, ny, kw, L, nsl);
-        else ex_run<EX_BA, true, false, false, false>(a, t, dem, ny, kw, L, nsl);
+        if (dem) ex_run<EX_BA, true, true, true, false, LB>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_BA, true, true, false, false, LB>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_BA, true, false, false, false, LB>(a, t, dem, ny, kw, L, nsl);
     } else if (ts) {
-        if (dem) ex_run<EX_NB, true, true, true, true>(a, t, dem, ny, kw, L, nsl);
-        else if (pk) ex_run<EX_NB, true, true, false, true>(a, t, dem, ny, kw, L, nsl);
-        else ex_run<EX_NB, true, false, false, true>(a, t, dem, ny, kw, L, nsl);
+        if (dem) ex_run<EX_NB, true, true, true, true, LB>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NB, true, true, false, true, LB>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NB, true, false, false, true, LB>(a, t, dem, ny, kw, L, nsl);
     } else {
-        if (dem) ex_run<EX_NB, true, true, true, false>(a, t, dem, ny, kw, L, nsl);
-        else if (pk) ex_run<EX_NB, true, true, false, false>(a, t, dem, ny, kw, L, nsl);
-        else ex_run<EX_NB, true, false, false, false>(a, t, dem, ny, kw, L, nsl);
+        if (dem) ex_run<EX_NB, true, true, true, false, LB>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NB, true, true, false, false, LB>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NB, true, false, false, false, LB>(a, t, dem, ny, kw, L, nsl);
     }
 }
 
 // oracle year_bill (+ year_demand) of year y0 + yl from its cells
+template <bool LB>
 __device__ __forceinline__ double ex_year_bill(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int yl,
                                const ExLds& L) {
     const int P = t.P;
+    const ExB B = ex_b<LB>(L.bins, L.bny, L.ptab, L.dcb);
     double* credit = ex_yr() + (size_t)yl * 2 * MAXP;
     double* u = credit + MAXP;
     for (int p = 0; p < MAXP; p++) credit[p] = 0.0;
     const bool ts = a.has_ts && t.mo == 2;
     double total = 0.0, carry = 0.0, dtot = 0.0;
     for (int m = 0; m < 12; m++) {
-        const double* bn = L.bins + ((size_t)yl * 12 + m) * 2 * P;
-        const double* cm = L.cmax + ((size_t)yl * 12 + m) * P;
+        const double* bn = B.bins + ((size_t)yl * 12 + m) * 2 * P;
+        const double* cm = B.cmax + ((size_t)yl * 12 + m) * P;
         double pk = 0.0;
         for (int p = 0; p < P; p++) pk = cm[p] > pk ? cm[p] : pk;
         double bill = t.fixed;
@@ -5846,7 +5870,7 @@ __device__ __forceinline__ double ex_year_bill(const ExAgent& a, const dgen_tari
             for (int q = 0; q < DCP; q++) {
                 double v = 0.0;
                 for (int p = 0; p < P; p++) {
-                    const double w = L.dcm[(((size_t)yl * 12 + m) * P + p) * DCP + q];
+                    const double w = B.dcm[(((size_t)yl * 12 + m) * P + p) * DCP + q];
                     v = w > v ? w : v;
                 }
                 c += ex_dc_tier(v, dem->tou_cap[q], dem->tou_price[q], dem->tou_nt[q]);
@@ -6018,18 +6042,15 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
         L.bins = reinterpret_cast<double*>(g + ex_ws_base());
         L.cmax = L.bins + (size_t)(MAXY + 1) * 12 * 2 * P;
         L.dcm = dcb ? L.cmax + (size_t)(MAXY + 1) * 12 * P : nullptr;
+        L.bny = MAXY + 1;
+        L.ptab = P;
+        L.dcb = dcb;
         double* d = dyn_lds;
         L.stg = ex_stg(0);
         L.yr = ex_yr();
         L.res = ex_res();
         L.hoff = ex_hoff();
-        if (lds_ny > 0) {
-            // the bins of lds_ny (>= every listed agent's N + 1) years in LDS
-            double* e = reinterpret_cast<double*>(L.hoff + 12 * EX_HOFF);
-            L.bins = e;
-            L.cmax = e + (size_t)lds_ny * 12 * 2 * P;
-            L.dcm = dcb ? L.cmax + (size_t)lds_ny * 12 * P : nullptr;
-        }
+        if (lds_ny > 0) L.bny = lds_ny;   // the bins of lds_ny (>= every listed agent's N + 1) years in LDS (ex_b<true>)
     }
     double* const aev = ex_res();
     double* const bw = aev + (MAXY + 1);
@@ -6102,13 +6123,17 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
             // with a new tariff, the no-system year's on lane N, then a
             // thread per year bills them
             PH_T0(tc);
-            ex_cells(a, t, dem, a.N, kw, L, need_wo ? a.N : -1);
+            if (lds_ny > 0) ex_cells<true>(a, t, dem, a.N, kw, L, need_wo ? a.N : -1);
+            else ex_cells<false>(a, t, dem, a.N, kw, L, need_wo ? a.N : -1);
             ex_handoff();
             PH_ADD(4, tc, threadIdx.x == 0);
             PH_T0(ty);
             const int y = (int)threadIdx.x;
-            if (y < a.N) bw[y + 1] = ex_year_bill(a, t, dem, y, L);
-            else if (need_wo && y == a.N) sc[0] = ex_year_bill(a, t, dem, a.N, L);
+            if (y < a.N || (need_wo && y == a.N)) {
+                const double wb = lds_ny > 0 ? ex_year_bill<true>(a, t, dem, y, L) : ex_year_bill<false>(a, t, dem, y, L);
+                if (y < a.N) bw[y + 1] = wb;
+                else sc[0] = wb;
+            }
             __syncthreads();
             if (need_wo) {
                 wo1 = ex_uniform(sc[0]);
