@@ -43,6 +43,8 @@ def main():
                          "diffusion_functions_elec.py:285)")
     ap.add_argument("--years", type=int, default=25, help="timed model years (2026-2050)")
     ap.add_argument("--no-batt", action="store_true", help="PV-only variant (no PV+battery forward run)")
+    ap.add_argument("--exact", type=int, default=-1, choices=[-1, 0, 1, 2],
+                    help="certified Brent paths (dgen_set_exact; bench.py --exact): -1 = the engine's default")
     ap.add_argument("--warmup", type=int, default=1, help="untimed model years, then reset")
     ap.add_argument("--hourly-chunk", type=int, default=None,
                     help="re-size chunks of this many agents for the state export")
@@ -107,7 +109,8 @@ def main():
         secs, ids = split_state_members(args.config, plan)
         sg = P.split_groups(plan, rank, secs, ids)
         n_rank = len(ag["agent_id"])
-    eng = Engine(local if ws > 1 else 0)
+    from dgen_amd.config import EngineConfig
+    eng = Engine(local if ws > 1 else 0, EngineConfig(exact_brent=args.exact))
     if args.no_batt:
         eng.set_battery(False)
     eng.load_profiles(pop.shapes, pop.cfs, pop.wholesale)
@@ -163,6 +166,7 @@ def main():
                     "/ attachment tables; no DB offline)",
             "config": {"workload": "national_loop" if args.config == "national_mixed" else f"{args.config}_loop",
                        "population": args.config, "year_step": args.step, "battery_run": not args.no_batt,
+                       "certified_brent_paths": eng.cfg.exact_mode(),
                        "agents_per_gpu": args.agents,
                        "global_agents": n_total, "years": [years[0], years[-1]],
                        "state_mix": "census" if plan is not None else "DE",
