@@ -5084,18 +5084,23 @@ __global__ void k_finance_series(Series6 src, const int32_t* __restrict__ len, i
 // every agent's Brent path, bills and NPV are the reference driver's.
 // ===========================================================================
 constexpr double BT_EPS = 2.220446049250313e-16;
-// Error model of one evaluation (k_brent_certify):
-// * a recursive sum of n terms errs by at most (n - 1) eps x the sum of their
-//   magnitudes: a (month, period) bin holds <= 744 hours, the slot / split
-//   forms add < 100 terms of their own and each hourly term <= 4 roundings, so
-//   device and oracle bins differ by <= ~850 eps x (load + generation);
+// Error model of one evaluation (k_brent_certify), u = eps / 2 the unit
+// roundoff of round-to-nearest:
+// * a recursive sum of n terms errs by at most gamma_(n-1) ~ (n - 1) u x the
+//   sum of their magnitudes (Higham, Accuracy and Stability, 4.2): a (month,
+//   period) bin holds <= 744 hours, the slot / split forms add < 100 terms of
+//   their own and each hourly term <= 4 roundings, so device and oracle bins
+//   differ by <= ~850 u x (load + generation);
 // * a bill moves by at most 2 x the largest price per kWh of bin change (a
 //   tier share's re-weighting at most doubles the marginal price; NEM credits
 //   are billed once, at a buy, sell or true-up price); so |bill_d - bill_o| <=
-//   1710 eps x price x (load + generation) <= BT_GAMMA x 2 eps x ...;
+//   1710 u x price x (load + generation) <= BT_GAMMA x 2 eps x ... with
+//   BT_GAMMA = 512 (= 2048 u; round 6's first form counted eps per rounding,
+//   BT_GAMMA 1024, twice the slack);
 // * NPV adds the years' bill differences discounted (D) with weight <= 1 (the
 //   commercial tax factors are below 1), plus the cash flow's own roundings.
-constexpr double BT_GAMMA = 1024.0;
+// Every single operation's rounding in the replay (bt_rnd) keeps eps.
+constexpr double BT_GAMMA = 512.0;
 
 struct BtModel {
     double c0, c1, ce;   // |f_device - f_oracle| <= c0 + c1 x + ce |f| at the same x
