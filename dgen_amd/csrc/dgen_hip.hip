@@ -5647,28 +5647,45 @@ __device__ __forceinline__ void ex_handoff() {
 // oracle bin_year's (a skipped sum is one the bill never reads).
 constexpr int EX_NEM = 0, EX_BA = 1, EX_NB = 2;
 constexpr int EX_R = 4, EX_CH = EX_R * 64;         // hours per lane / per chunk
-template <int FORM, bool GEN, bool PK, bool DEM, bool TS, bool LB>
+template <int FORM, bool GEN, bool PK, bool DEM, bool TS, bool LB, bool HW>
 __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
                        const ExLds& L, int nsl) {
+    // HW: two runs of bins per wave, one per half-wave (lane = year within
+    // the half: N + 1 <= 32), so 50 of 64 lanes work instead of 25
+    constexpr int HL = HW ? 32 : WAVE;                 // lanes per run
+    constexpr int CH = EX_R * HL;                      // hours per chunk per run
     const int P = t.P;
     const ExB B = ex_b<LB>(L.bins, L.bny, L.ptab, L.dcb);
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE, nw = blockDim.x / WAVE;
+    const int h = lane / HL, yl = lane % HL;
     // the lane's year's degradation factor; lane nsl (when >= 0): the
     // no-system year, factor 0 -- its generation term is +-0, so every sum
     // is the kW-0 pass's (load - 0 == load)
-    const double s = lane == nsl ? 0.0 : pow_seq(a.sys_base, lane);
-    double* const sL = ex_stg(wv);
-    double* const sG = sL + EX_CH;
-    double* const sT = sG + EX_CH;
-    int* const sQ = reinterpret_cast<int*>(sT + EX_CH);
+    const double s = yl == nsl ? 0.0 : pow_seq(a.sys_base, yl);
+    double* const sL = ex_stg(wv) + h * CH;
+    double* const sG = ex_stg(wv) + EX_CH + h * CH;
+    double* const sT = ex_stg(wv) + 2 * EX_CH + h * CH;
+    int* const sQ = reinterpret_cast<int*>(ex_stg(wv) + 3 * EX_CH) + h * CH;
     const int nb = 12 * P;
-    const int bA = (wv * nb) / nw, bB = ((wv + 1) * nb) / nw;
     // list position where bin b starts (b == nb: the end of the list)
     auto bstart = [&](int b) __attribute__((always_inline)) -> int {
         const int m = b / P;
-        return b >= nb ? NH : __builtin_amdgcn_readfirstlane(ex_hoff()[m * EX_HOFF + (b - m * P)]);
+        const int v = b >= nb ? NH : ex_hoff()[m * EX_HOFF + (b - m * P)];
+        if constexpr (HW) return v;
+        else return __builtin_amdgcn_readfirstlane(v);
     };
-    if (bA >= bB) return;
+    const int wA = (wv * nb) / nw, wB = ((wv + 1) * nb) / nw;
+    if (wA >= wB) return;
+    // the wave's bins, split between the halves at the bin nearest the
+    // middle hour of the run
+    int bA = wA, bB = wB;
+    if constexpr (HW) {
+        const int mid = (bstart(wA) + bstart(wB)) / 2;
+        int bM = wA + 1;
+        while (bM < wB && bstart(bM) < mid) bM++;
+        bA = h == 0 ? wA : bM;
+        bB = h == 0 ? bM : wB;
+    }
     const int kA = bstart(bA), kB = bstart(bB);
     int b = bA, kn = bstart(bA + 1), m = bA / P;
     double b0 = 0.0, b1 = 0.0, mx = 0.0;
@@ -5676,15 +5693,15 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
 #pragma unroll
     for (int q = 0; q < (DEM ? DCP : 1); q++) dq[q] = 0.0;
     auto flush = [&]() __attribute__((always_inline)) {
-        if (lane < ny || lane == nsl) {
+        if (yl < ny || yl == nsl) {
             const int p = b - m * P;
-            double* bn = B.bins + ((size_t)lane * 12 + m) * 2 * P;
+            double* bn = B.bins + ((size_t)yl * 12 + m) * 2 * P;
             bn[p] = b0;
             bn[P + p] = b1;
-            B.cmax[((size_t)lane * 12 + m) * P + p] = mx;
+            B.cmax[((size_t)yl * 12 + m) * P + p] = mx;
             if constexpr (DEM) {
 #pragma unroll
-                for (int q = 0; q < DCP; q++) B.dcm[(((size_t)lane * 12 + m) * P + p) * DCP + q] = dq[q];
+                for (int q = 0; q < DCP; q++) B.dcm[(((size_t)yl * 12 + m) * P + p) * DCP + q] = dq[q];
             }
         }
         b0 = 0.0; b1 = 0.0; mx = 0.0;
@@ -5698,7 +5715,7 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
     auto step = [&](int j) __attribute__((always_inline)) {
         const double ld = sL[j];
         // (option 4 sums the generation itself: the no-system lane's is +0)
-        const double g = GEN ? ((FORM == EX_BA && lane == nsl) ? 0.0 : sG[j] * s) : 0.0;
+        const double g = GEN ? ((FORM == EX_BA && yl == nsl) ? 0.0 : sG[j] * s) : 0.0;
         const double dd = ld - g;
         if constexpr (PK) mx = dd > mx ? dd : mx;
         if constexpr (FORM == EX_NEM) {
@@ -5730,7 +5747,7 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
         const int hh = i % 24;
         return ((i % 168) >= 120) ? dem->wkend[mm][hh] : dem->wkday[mm][hh];
     };
-    // chunks of EX_CH hours (EX_R per lane); the next chunk's values in
+    // chunks of CH hours per run (EX_R per lane); the next chunk's values in
     // registers while this one is walked (a chunk's walk outlasts the loads'
     // latency from L2 / MALL)
     double lv[EX_R], cv[EX_R], tv[EX_R];
@@ -5738,7 +5755,7 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
     auto fetch = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
         for (int r = 0; r < EX_R; r++) {
-            const int kk = c0 + r * WAVE + lane;
+            const int kk = c0 + r * HL + yl;
             const bool v = kk < kB;
             lv[r] = v ? L.Lp[kk] : 0.0;
             if constexpr (GEN) cv[r] = v ? L.Cp[kk] : 0.0;
@@ -5746,13 +5763,21 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
             if constexpr (DEM) qv[r] = v ? dper(kk) : 0;
         }
     };
+    // the chunk count of the wave: the longer run's (each half's own count
+    // in HW; a half past its run walks nothing)
+    int nch = (kB - kA + CH - 1) / CH;
+    if constexpr (HW) {
+        const int n0 = __builtin_amdgcn_readlane(nch, 0), n1 = __builtin_amdgcn_readlane(nch, HL);
+        nch = n0 > n1 ? n0 : n1;
+    }
     fetch(kA);
-    for (int c = kA; c < kB; c += EX_CH) {
-        const int n = (kB - c) < EX_CH ? (kB - c) : EX_CH;
+    for (int ci = 0; ci < nch; ci++) {
+        const int c = kA + ci * CH;
+        const int n = (kB - c) < CH ? ((kB - c) > 0 ? kB - c : 0) : CH;   // this run's hours in the chunk
         wave_lds_sync();                               // the previous chunk's reads
 #pragma unroll
         for (int r = 0; r < EX_R; r++) {
-            const int o = r * WAVE + lane;
+            const int o = r * HL + yl;
             sL[o] = lv[r];
             // ff:117-120 generation of the hour at kW, oracle perf_no_batt's order
             if constexpr (GEN) sG[o] = ref_gen(cv[r], kw);
@@ -5760,44 +5785,77 @@ __device__ void ex_run(const ExAgent& a, const dgen_tariff& t, const dgen_demand
             if constexpr (DEM) sQ[o] = qv[r];
         }
         wave_lds_sync();
-        if (c + EX_CH < kB) fetch(c + EX_CH);          // the next chunk in flight
-        int j = 0;
-        while (j < n) {
-            while (c + j == kn) flush();               // the bins that end here (empty ones too)
-            const int je = (kn - c) < n ? (kn - c) : n;
-            for (; j + 4 <= je; j += 4) {
+        if (ci + 1 < nch) fetch(c + CH);               // the next chunk in flight
+        if constexpr (!HW) {
+            int j = 0;
+            while (j < n) {
+                while (c + j == kn) flush();           // the bins that end here (empty ones too)
+                const int je = (kn - c) < n ? (kn - c) : n;
+                for (; j + 4 <= je; j += 4) {
 #pragma unroll
-                for (int u = 0; u < 4; u++) step(j + u);
+                    for (int u = 0; u < 4; u++) step(j + u);
+                }
+                for (; j < je; j++) step(j);
             }
-            for (; j < je; j++) step(j);
+        } else {
+            // the halves walk their own hours in step; a segment runs to the
+            // nearer of the two halves' next events (a bin's end, the run's
+            // end in this chunk), where the half it belongs to flushes
+            const int n0 = __builtin_amdgcn_readlane(n, 0), n1 = __builtin_amdgcn_readlane(n, HL);
+            const int nmax = n0 > n1 ? n0 : n1;
+            int j = 0;
+            while (j < nmax) {
+                while (j < n && c + j == kn) flush();  // this half's bins that end here
+                const int ev = j < n ? ((kn - c) < n ? (kn - c) : n) : nmax;
+                const int e0 = __builtin_amdgcn_readlane(ev, 0), e1 = __builtin_amdgcn_readlane(ev, HL);
+                const int je = e0 < e1 ? e0 : e1;
+                if (j < n) {                           // (a half past its run's hours sits out)
+                    int jj = j;
+                    for (; jj + 4 <= je; jj += 4) {
+#pragma unroll
+                        for (int u = 0; u < 4; u++) step(jj + u);
+                    }
+                    for (; jj < je; jj++) step(jj);
+                }
+                j = je;
+            }
         }
     }
     // the run's last bin and any empty bins after it
     while (b < bB) flush();
 }
 
-template <bool LB>
-__device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
+template <bool LB, bool HW>
+__device__ void ex_cells_h(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
                          const ExLds& L, int nsl) {
     const bool pk = dem != nullptr || t.unit == 1 || t.unit == 3;
     const bool ts = a.has_ts && t.mo == 2;
     if (t.mo == 0 || t.mo == 1) {
-        if (dem) ex_run<EX_NEM, true, true, true, false, LB>(a, t, dem, ny, kw, L, nsl);
-        else if (pk) ex_run<EX_NEM, true, true, false, false, LB>(a, t, dem, ny, kw, L, nsl);
-        else ex_run<EX_NEM, true, false, false, false, LB>(a, t, dem, ny, kw, L, nsl);
+        if (dem) ex_run<EX_NEM, true, true, true, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NEM, true, true, false, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NEM, true, false, false, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
     } else if (t.mo == 4) {
-        if (dem) ex_run<EX_BA, true, true, true, false, LB>(a, t, dem, ny, kw, L, nsl);
-        else if (pk) ex_run<EX_BA, true, true, false, false, LB>(a, t, dem, ny, kw, L, nsl);
-        else ex_run<EX_BA, true, false, false, false, LB>(a, t, dem, ny, kw, L, nsl);
+        if (dem) ex_run<EX_BA, true, true, true, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_BA, true, true, false, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_BA, true, false, false, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
     } else if (ts) {
-        if (dem) ex_run<EX_NB, true, true, true, true, LB>(a, t, dem, ny, kw, L, nsl);
-        else if (pk) ex_run<EX_NB, true, true, false, true, LB>(a, t, dem, ny, kw, L, nsl);
-        else ex_run<EX_NB, true, false, false, true, LB>(a, t, dem, ny, kw, L, nsl);
+        if (dem) ex_run<EX_NB, true, true, true, true, LB, HW>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NB, true, true, false, true, LB, HW>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NB, true, false, false, true, LB, HW>(a, t, dem, ny, kw, L, nsl);
     } else {
-        if (dem) ex_run<EX_NB, true, true, true, false, LB>(a, t, dem, ny, kw, L, nsl);
-        else if (pk) ex_run<EX_NB, true, true, false, false, LB>(a, t, dem, ny, kw, L, nsl);
-        else ex_run<EX_NB, true, false, false, false, LB>(a, t, dem, ny, kw, L, nsl);
+        if (dem) ex_run<EX_NB, true, true, true, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
+        else if (pk) ex_run<EX_NB, true, true, false, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
+        else ex_run<EX_NB, true, false, false, false, LB, HW>(a, t, dem, ny, kw, L, nsl);
     }
+}
+
+template <bool LB>
+__device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int ny, double kw,
+                         const ExLds& L, int nsl) {
+    // two runs per wave when the analysis years and the no-system lane fit
+    // a half-wave
+    if (ny + 1 <= 32) ex_cells_h<LB, true>(a, t, dem, ny, kw, L, nsl);
+    else ex_cells_h<LB, false>(a, t, dem, ny, kw, L, nsl);
 }
 
 // oracle year_bill (+ year_demand) of year y0 + yl from its cells
