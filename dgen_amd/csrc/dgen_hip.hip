@@ -5441,7 +5441,10 @@ __device__ __forceinline__ double ex_uniform(double v) {
 }
 
 
-__device__ __forceinline__ double ex_month_charge(const dgen_tariff& t, int m, const double* u, double peak) {
+// fr: the year thread's scratch for the periods' shares u_p / U, formed once
+// per month (the oracle forms the same quotient per tier: equal bits)
+__device__ __forceinline__ double ex_month_charge(const dgen_tariff& t, int m, const double* u, double peak,
+                                                  double* fr) {
     double U = 0.0;
     for (int p = 0; p < t.P; p++) U += u[p];
     // (the oracle returns 0 for U <= 0 first; here the charge is formed
@@ -5459,6 +5462,7 @@ __device__ __forceinline__ double ex_month_charge(const dgen_tariff& t, int m, c
     const double f_pk = (t.unit == 1 || t.unit == 3) ? peak : 1.0;
     const double f_days = (t.unit == 2 || t.unit == 3) ? days : 1.0;
     const double scale = f_pk * f_days;
+    for (int p = 0; p < t.P; p++) fr[p] = u[p] / U;
     double charge = 0.0, prev = 0.0;
     for (int k = 0; k < t.T; k++) {
         const double hi = (k == t.T - 1) ? INFINITY : t.cap[k] * scale;
@@ -5466,7 +5470,7 @@ __device__ __forceinline__ double ex_month_charge(const dgen_tariff& t, int m, c
         const double amt0 = top - prev;
         const double amt = amt0 < 0.0 ? 0.0 : amt0;
         prev = hi > prev ? hi : prev;
-        for (int p = 0; p < t.P; p++) charge += (u[p] / U) * amt * t.buy[p][k];
+        for (int p = 0; p < t.P; p++) charge += fr[p] * amt * t.buy[p][k];
     }
     return pos ? charge : 0.0;
 }
@@ -5511,7 +5515,7 @@ struct ExLds {
     double* cmax;      // [MAXY][12][P] each bin's largest import (the month peak: their max, from 0) (global)
     double* dcm;       // [MAXY][12][P][DCP] each bin's largest import per demand period (billed demand only; global)
     double* stg;       // [waves][4][256] the wave's staged hours: load, generation, TS rate, demand period (LDS)
-    double* yr;        // [MAXY][2 MAXP] per-year-thread credit / billed kWh (LDS)
+    double* yr;        // [MAXY + 1][3 MAXP] per-year-thread credit / billed kWh / period shares (LDS)
     double* res;       // [6][MAXY + 1] aev, bill_w, bill_wo, cf_payback, cf_energy_value, atcf; + 8 scalars (LDS)
     int bny;           // the bins' year stride (LDS: the batch's N + 1; global: MAXY + 1)
     int ptab;          // the table's periods (the bins' layout)
@@ -5519,7 +5523,7 @@ struct ExLds {
 };
 
 __host__ __device__ inline size_t ex_lds_bytes() {
-    return sizeof(double) * ((size_t)(EX_THREADS / 64) * 4 * 256 + (size_t)(MAXY + 1) * 2 * MAXP + 6 * (size_t)(MAXY + 1) + 8) +
+    return sizeof(double) * ((size_t)(EX_THREADS / 64) * 4 * 256 + (size_t)(MAXY + 1) * 3 * MAXP + 6 * (size_t)(MAXY + 1) + 8) +
            sizeof(int32_t) * (size_t)12 * EX_HOFF;   // = ex_stg + ex_yr + ex_res + ex_hoff
 }
 
@@ -5527,7 +5531,7 @@ __host__ __device__ inline size_t ex_lds_bytes() {
 // are LDS and emits ds_* accesses; through the generic pointers of a struct
 // they became flat loads with memory-path latency)
 constexpr size_t EX_STG_QW = (size_t)(EX_THREADS / 64) * 4 * 256;
-constexpr size_t EX_YR_QW = (size_t)(MAXY + 1) * 2 * MAXP;
+constexpr size_t EX_YR_QW = (size_t)(MAXY + 1) * 3 * MAXP;
 constexpr size_t EX_RES_QW = 6 * (size_t)(MAXY + 1) + 8;
 __device__ __forceinline__ double* ex_stg(int wv) { return dyn_lds + (size_t)wv * 4 * 256; }
 __device__ __forceinline__ double* ex_yr() { return dyn_lds + EX_STG_QW; }
@@ -5601,12 +5605,22 @@ __device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L, const float*
         }
         int cur = h0 + incl - (lane < P ? cnt : 0);    // lane p: first position of period p
         if (lane <= P) ex_hoff()[m * EX_HOFF + lane] = lane < P ? cur : h1;
+        // the next chunk's values in flight while this one is placed
+        float shn = lane < h1 - h0 ? sh[h0 + lane] : 0.0f;
+        int32_t cfn = lane < h1 - h0 ? cfr[h0 + lane] : 0;
+        double whn = (lane < h1 - h0 && wrow) ? wrow[h0 + lane] : 0.0;
         for (int c = h0; c < h1; c += WAVE) {
             const int i = c + lane;
-            const bool in = i < h1;
-            const float shv = in ? sh[i] : 0.0f;
-            const int32_t cfv = in ? cfr[i] : 0;
-            const double whv = (in && wrow) ? wrow[i] : 0.0;
+            const float shv = shn;
+            const int32_t cfv = cfn;
+            const double whv = whn;
+            {
+                const int i2 = i + WAVE;
+                const bool in2 = i2 < h1;
+                shn = in2 ? sh[i2] : 0.0f;
+                cfn = in2 ? cfr[i2] : 0;
+                whn = (in2 && wrow) ? wrow[i2] : 0.0;
+            }
             const int per = period(i);
             int pos = 0;
             for (int p = 0; p < P; p++) {
@@ -5864,7 +5878,7 @@ __device__ __forceinline__ double ex_year_bill(const ExAgent& a, const dgen_tari
                                const ExLds& L) {
     const int P = t.P;
     const ExB B = ex_b<LB>(L.bins, L.bny, L.ptab, L.dcb);
-    double* credit = ex_yr() + (size_t)yl * 2 * MAXP;
+    double* credit = ex_yr() + (size_t)yl * 3 * MAXP;     // credit, u, shares
     double* u = credit + MAXP;
     for (int p = 0; p < MAXP; p++) credit[p] = 0.0;
     const bool ts = a.has_ts && t.mo == 2;
@@ -5884,7 +5898,7 @@ __device__ __forceinline__ double ex_year_bill(const ExAgent& a, const dgen_tari
                 u[p] = pos ? n - use : 0.0;
                 credit[p] = pos ? cp - use : cp + -n;
             }
-            bill += ex_month_charge(t, m, u, pk);
+            bill += ex_month_charge(t, m, u, pk, u + MAXP);
             if (m == 11) {
                 double cc = 0.0;
                 for (int p = 0; p < P; p++) cc += credit[p];
@@ -5897,7 +5911,7 @@ __device__ __forceinline__ double ex_year_bill(const ExAgent& a, const dgen_tari
                 u[p] = n > 0.0 ? n : 0.0;
                 cr += (n < 0.0 ? -n : 0.0) * t.sell[p][0];
             }
-            const double e = ex_month_charge(t, m, u, pk) - cr - carry;
+            const double e = ex_month_charge(t, m, u, pk, u + MAXP) - cr - carry;
             carry = e < 0.0 ? -e : 0.0;
             bill += e < 0.0 ? 0.0 : e;
         } else if (t.mo == 4) {
@@ -5906,11 +5920,11 @@ __device__ __forceinline__ double ex_year_bill(const ExAgent& a, const dgen_tari
                 u[p] = bn[p];
                 cr += bn[P + p] * t.sell[p][0];
             }
-            bill += ex_month_charge(t, m, u, pk) - cr;
+            bill += ex_month_charge(t, m, u, pk, u + MAXP) - cr;
         } else {
             double cr = 0.0;
             for (int p = 0; p < P; p++) u[p] = bn[p];
-            const double charge = ex_month_charge(t, m, u, pk);
+            const double charge = ex_month_charge(t, m, u, pk, u + MAXP);
             if (ts) {
                 for (int p = 0; p < P; p++) cr += bn[P + p];
             } else {
