@@ -5872,10 +5872,160 @@ __device__ void ex_cells(const ExAgent& a, const dgen_tariff& t, const dgen_dema
     else ex_cells_h<LB, false>(a, t, dem, ny, kw, L, nsl);
 }
 
+// The same bill with the periods' credits, billed kWh and shares in
+// registers (P <= PREG, the common case): loops run to the compile-time bound
+// under the guard p < P, so every sum keeps ex_year_bill's order (and the
+// oracle's); the bins' loads of a month issue together.
+__device__ __forceinline__ double ex_month_charge_reg(const dgen_tariff& t, int m, const double (&u)[PREG],
+                                                      double peak) {
+    const int P = t.P;
+    double U = 0.0;
+#pragma unroll
+    for (int p = 0; p < PREG; p++)
+        if (p < P) U += u[p];
+    const bool pos = U > 0.0;
+    if (t.T == 1) {
+        double charge = 0.0;
+#pragma unroll
+        for (int p = 0; p < PREG; p++)
+            if (p < P) charge += u[p] * t.buy[p][0];
+        return pos ? charge : 0.0;
+    }
+    const double days = (double)c_days_in_month[m];
+    const double f_pk = (t.unit == 1 || t.unit == 3) ? peak : 1.0;
+    const double f_days = (t.unit == 2 || t.unit == 3) ? days : 1.0;
+    const double scale = f_pk * f_days;
+    double fr[PREG];
+#pragma unroll
+    for (int p = 0; p < PREG; p++) fr[p] = p < P ? u[p] / U : 0.0;
+    double charge = 0.0, prev = 0.0;
+    for (int k = 0; k < t.T; k++) {
+        const double hi = (k == t.T - 1) ? INFINITY : t.cap[k] * scale;
+        const double top = U < hi ? U : hi;
+        const double amt0 = top - prev;
+        const double amt = amt0 < 0.0 ? 0.0 : amt0;
+        prev = hi > prev ? hi : prev;
+#pragma unroll
+        for (int p = 0; p < PREG; p++)
+            if (p < P) charge += fr[p] * amt * t.buy[p][k];
+    }
+    return pos ? charge : 0.0;
+}
+
+template <bool LB>
+__device__ __forceinline__ double ex_year_bill_reg(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem,
+                                                   int yl, const ExLds& L) {
+    const int P = t.P;
+    const ExB B = ex_b<LB>(L.bins, L.bny, L.ptab, L.dcb);
+    double credit[PREG], u[PREG];
+#pragma unroll
+    for (int p = 0; p < PREG; p++) { credit[p] = 0.0; u[p] = 0.0; }
+    const bool ts = a.has_ts && t.mo == 2;
+    double total = 0.0, carry = 0.0, dtot = 0.0;
+    for (int m = 0; m < 12; m++) {
+        const double* bn = B.bins + ((size_t)yl * 12 + m) * 2 * P;
+        const double* cm = B.cmax + ((size_t)yl * 12 + m) * P;
+        double b0[PREG], b1[PREG], c0[PREG];
+#pragma unroll
+        for (int p = 0; p < PREG; p++) {
+            b0[p] = p < P ? bn[p] : 0.0;
+            b1[p] = p < P ? bn[P + p] : 0.0;
+            c0[p] = p < P ? cm[p] : 0.0;
+        }
+        double pk = 0.0;
+#pragma unroll
+        for (int p = 0; p < PREG; p++)
+            if (p < P) pk = c0[p] > pk ? c0[p] : pk;
+        double bill = t.fixed;
+        if (t.mo == 0) {
+#pragma unroll
+            for (int p = 0; p < PREG; p++) {
+                if (p < P) {
+                    const double n = b0[p];
+                    const double cp = credit[p];
+                    const double use = n < cp ? n : cp;
+                    const bool ps = n >= 0.0;
+                    u[p] = ps ? n - use : 0.0;
+                    credit[p] = ps ? cp - use : cp + -n;
+                }
+            }
+            bill += ex_month_charge_reg(t, m, u, pk);
+            if (m == 11) {
+                double cc = 0.0;
+#pragma unroll
+                for (int p = 0; p < PREG; p++)
+                    if (p < P) cc += credit[p];
+                bill -= cc * a.yearend;
+            }
+        } else if (t.mo == 1) {
+            double cr = 0.0;
+#pragma unroll
+            for (int p = 0; p < PREG; p++) {
+                if (p < P) {
+                    const double n = b0[p];
+                    u[p] = n > 0.0 ? n : 0.0;
+                    cr += (n < 0.0 ? -n : 0.0) * t.sell[p][0];
+                }
+            }
+            const double e = ex_month_charge_reg(t, m, u, pk) - cr - carry;
+            carry = e < 0.0 ? -e : 0.0;
+            bill += e < 0.0 ? 0.0 : e;
+        } else if (t.mo == 4) {
+            double cr = 0.0;
+#pragma unroll
+            for (int p = 0; p < PREG; p++) {
+                if (p < P) {
+                    u[p] = b0[p];
+                    cr += b1[p] * t.sell[p][0];
+                }
+            }
+            bill += ex_month_charge_reg(t, m, u, pk) - cr;
+        } else {
+            double cr = 0.0;
+#pragma unroll
+            for (int p = 0; p < PREG; p++)
+                if (p < P) u[p] = b0[p];
+            const double charge = ex_month_charge_reg(t, m, u, pk);
+            if (ts) {
+#pragma unroll
+                for (int p = 0; p < PREG; p++)
+                    if (p < P) cr += b1[p];
+            } else {
+#pragma unroll
+                for (int p = 0; p < PREG; p++)
+                    if (p < P) cr += b1[p] * t.sell[p][0];
+            }
+            if (t.mo == 3) {
+                const double e = charge - cr - carry;
+                carry = e < 0.0 ? -e : 0.0;
+                bill += e < 0.0 ? 0.0 : e;
+            } else {
+                bill += charge;
+                bill -= cr;
+            }
+        }
+        total += bill;
+        if (dem) {
+            double c = ex_dc_tier(pk, dem->flat_cap[m], dem->flat_price[m], dem->flat_nt[m]);
+            for (int q = 0; q < DCP; q++) {
+                double v = 0.0;
+                for (int p = 0; p < P; p++) {
+                    const double w = B.dcm[(((size_t)yl * 12 + m) * P + p) * DCP + q];
+                    v = w > v ? w : v;
+                }
+                c += ex_dc_tier(v, dem->tou_cap[q], dem->tou_price[q], dem->tou_nt[q]);
+            }
+            dtot += c;
+        }
+    }
+    return dem ? total + dtot : total;
+}
+
 // oracle year_bill (+ year_demand) of year y0 + yl from its cells
 template <bool LB>
 __device__ __forceinline__ double ex_year_bill(const ExAgent& a, const dgen_tariff& t, const dgen_demand* dem, int yl,
                                const ExLds& L) {
+    if (t.P <= PREG) return ex_year_bill_reg<LB>(a, t, dem, yl, L);
     const int P = t.P;
     const ExB B = ex_b<LB>(L.bins, L.bny, L.ptab, L.dcb);
     double* credit = ex_yr() + (size_t)yl * 3 * MAXP;     // credit, u, shares
