@@ -6255,8 +6255,13 @@ __device__ void ex_cashloan_par(const dgen_agents& A, const dgen_cfg& cfg, int64
 
 __global__ void __launch_bounds__(EX_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
 k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const int32_t* __restrict__ list,
-             char* exws, int64_t wsb, int lds_ny) {
+             char* exws, int64_t wsb, int lds_ny, int32_t* next) {
     const int cnt = list[0];
+    // next (a zeroed counter): the blocks take the listed agents one at a
+    // time from it, so a block that drew short searches takes more of them
+    // (the grid is the device's resident blocks); nullptr: block b takes
+    // agents b, b + grid, ...
+    __shared__ int s_next;
     ExLds L;
     {
         char* g = exws + (size_t)blockIdx.x * (size_t)wsb;
@@ -6291,7 +6296,14 @@ k_size_exact(dgen_tables T, dgen_agents A, dgen_outputs O, dgen_cfg cfg, const i
     a.n_demand = T.n_demand;
     a.dc_on = cfg.skip_demand_charges == 0;
     a.yearend = cfg.nm_yearend_sell_rate;
-    for (int w = blockIdx.x; w < cnt; w += gridDim.x) {
+    for (int w0 = blockIdx.x;; w0 += gridDim.x) {
+        int w = w0;
+        if (next) {
+            if (threadIdx.x == 0) s_next = atomicAdd(next, 1);
+            __syncthreads();
+            w = __builtin_amdgcn_readfirstlane(s_next);
+        }
+        if (w >= cnt) break;
         const int64_t i = __builtin_amdgcn_readfirstlane(list[1 + w]);
         const int lr = A.load_row[i], cr = A.cf_row[i];
         const double kwh = A.load_kwh[i];
@@ -6512,6 +6524,9 @@ struct dgen_ctx {
     size_t bt_cap = 0;
     int32_t* ex_list = nullptr;    // chunk j: [i0 + j] count, then its rows
     size_t ex_list_cap = 0;
+    int32_t* ex_next = nullptr;    // [MAXCH] the re-run's work counters (k_size_exact's next)
+    int ex_dyn = 1;                // 0: static agent order over EX_BLOCKS blocks (DGEN_EX_DYN=0, A/B)
+    int n_cu = 256;                // the device's compute units
     int ex_last_nch = 0;
     int64_t ex_last_off[MAXCH] = {0};
 };
@@ -6595,6 +6610,12 @@ int32_t dgen_open(int32_t device, const dgen_cfg* cfg, dgen_ctx** out) {
             c->lds_max = v;
         else
             (void)hipGetLastError();
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && v > 0)
+            c->n_cu = v;
+        else
+            (void)hipGetLastError();
+        const char* e = getenv("DGEN_EX_DYN");
+        if (e && e[0] == '0') c->ex_dyn = 0;
     }
     c->head = 0; c->pending = 0; c->count = 0;
     c->chunks = DGEN_DEFAULT_CHUNKS;
@@ -6668,6 +6689,7 @@ int32_t dgen_close(dgen_ctx* c) {
     if (c->bt_buf) (void)hipFree(c->bt_buf);
     if (c->ex_ws) (void)hipFree(c->ex_ws);
     if (c->ex_list) (void)hipFree(c->ex_list);
+    if (c->ex_next) (void)hipFree(c->ex_next);
     delete c;
     return DGEN_OK;
 }
@@ -6805,6 +6827,7 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             HIP_TRY(hipMalloc(&c->ex_list, (size_t)(n + dgen_ctx::MAXCH) * sizeof(int32_t)));
             c->ex_list_cap = (size_t)(n + dgen_ctx::MAXCH) * sizeof(int32_t);
         }
+        if (!c->ex_next) HIP_TRY(hipMalloc(&c->ex_next, (size_t)dgen_ctx::MAXCH * sizeof(int32_t)));
     }
     // the exact re-run's per-block scratch (its bins sized by the table's
     // periods and the demand records)
@@ -6825,12 +6848,25 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
     const int ex_ny = (A->max_years >= 1 && A->max_years <= MAXY) ? A->max_years : MAXY;
     // (N + 1 years: the no-system year rides on lane N)
     const size_t ex_bins_lds = sizeof(double) * (size_t)(ex_ny + 1) * 12 * (size_t)ex_P * (3 + (ex_dcb ? (size_t)DCP : 0));
-    const bool ex_lb = ex_lds_bytes() + ex_bins_lds <= (size_t)c->lds_max;
+    const bool ex_lb = ex_lds_bytes() + ex_bins_lds + 16 <= (size_t)c->lds_max;   // (+ the kernel's static s_next)
     const size_t ex_lds = ex_lds_bytes() + (ex_lb ? ex_bins_lds : 0);
     if (exact_on && ex_lds > 65536)
         HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(k_size_exact),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)ex_lds));
     double* const bt = exact_on ? c->bt_buf : nullptr;
+    // the re-run's grid: the blocks the device holds at once (work counter),
+    // at most EX_BLOCKS scratch slots
+    int ex_grid = EX_BLOCKS;
+    if (exact_on && c->ex_dyn) {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_size_exact),
+                                                         ex_threads, ex_lds) == hipSuccess && per_cu > 0) {
+            const int64_t g = (int64_t)per_cu * c->n_cu;
+            ex_grid = g < EX_BLOCKS ? (int)g : EX_BLOCKS;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     if (c->pending == dgen_ctx::RING) {   // fold the oldest record before reuse
         int r = fold_one(c, c->head);
         if (r) return r;
@@ -7027,10 +7063,13 @@ int32_t dgen_size_agents(dgen_ctx* c, const dgen_tables* T, const dgen_agents* A
             int32_t* const lst = c->ex_list + i0 + j;
             c->ex_last_off[j] = i0 + j;
             HIP_TRY(hipMemsetAsync(lst, 0, sizeof(int32_t), s));
+            int32_t* const nxt = c->ex_dyn ? c->ex_next + j : nullptr;
+            if (nxt) HIP_TRY(hipMemsetAsync(nxt, 0, sizeof(int32_t), s));
             hipLaunchKernelGGL(k_brent_certify, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, *T, *A, *O,
                                c->cfg, i0, i1, bt, lst, c->exact);
-            hipLaunchKernelGGL(k_size_exact, dim3((unsigned)(m < EX_BLOCKS ? m : EX_BLOCKS)), dim3(ex_threads),
-                               ex_lds, s, *T, *A, *O, c->cfg, lst, c->ex_ws, (int64_t)ex_wsb, ex_lb ? ex_ny + 1 : 0);
+            hipLaunchKernelGGL(k_size_exact, dim3((unsigned)(m < ex_grid ? m : ex_grid)), dim3(ex_threads),
+                               ex_lds, s, *T, *A, *O, c->cfg, lst, c->ex_ws, (int64_t)ex_wsb, ex_lb ? ex_ny + 1 : 0,
+                               nxt);
         }
         HIP_TRY(hipEventRecord(e[1], s));
         HIP_TRY(hipStreamWaitEvent(s2, e[1], 0));
