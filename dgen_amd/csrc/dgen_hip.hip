@@ -5574,6 +5574,7 @@ struct ExAgent {
 // per kW (cf / 1e6, ff:350) and TS sell rate (ff:182,246,372 x multiplier,
 // float32-rounded) are read in time order and written at the hour's list
 // position.
+constexpr int EX_HQ = 4;            // chunks of profile values in flight (ex_hour_lists)
 __device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L, const float* __restrict__ sh, double S,
                               double kwh, const int32_t* __restrict__ cfr, const double* __restrict__ wrow,
                               double pmul) {
@@ -5588,6 +5589,22 @@ __device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L, const float*
             const int pr = __shfl(sched, src, WAVE);
             return i < h1 ? pr : -1;
         };
+        // the month's first EX_HQ chunks of values in flight across the
+        // counting pass, then EX_HQ chunks ahead of the one being placed (a
+        // ring of registers; at one chunk ahead each chunk waited out its
+        // loads' latency)
+        float shq[EX_HQ];
+        int32_t cfq[EX_HQ];
+        double whq[EX_HQ];
+        auto fetch = [&](int d, int c) __attribute__((always_inline)) {
+            const int i2 = c + lane;
+            const bool in2 = i2 < h1;
+            shq[d] = in2 ? sh[i2] : 0.0f;
+            cfq[d] = in2 ? cfr[i2] : 0;
+            whq[d] = (in2 && wrow) ? wrow[i2] : 0.0;
+        };
+#pragma unroll
+        for (int d = 0; d < EX_HQ; d++) fetch(d, h0 + d * WAVE);
         int cnt = 0;                                   // lane p < P: hours of period p
         for (int c = h0; c < h1; c += WAVE) {
             const int per = period(c + lane);
@@ -5605,22 +5622,16 @@ __device__ void ex_hour_lists(const dgen_tariff& t, const ExLds& L, const float*
         }
         int cur = h0 + incl - (lane < P ? cnt : 0);    // lane p: first position of period p
         if (lane <= P) ex_hoff()[m * EX_HOFF + lane] = lane < P ? cur : h1;
-        // the next chunk's values in flight while this one is placed
-        float shn = lane < h1 - h0 ? sh[h0 + lane] : 0.0f;
-        int32_t cfn = lane < h1 - h0 ? cfr[h0 + lane] : 0;
-        double whn = (lane < h1 - h0 && wrow) ? wrow[h0 + lane] : 0.0;
-        for (int c = h0; c < h1; c += WAVE) {
+        for (int c0 = h0; c0 < h1; c0 += EX_HQ * WAVE)
+#pragma unroll
+        for (int d = 0; d < EX_HQ; d++) {
+            const int c = c0 + d * WAVE;
+            if (c >= h1) break;
             const int i = c + lane;
-            const float shv = shn;
-            const int32_t cfv = cfn;
-            const double whv = whn;
-            {
-                const int i2 = i + WAVE;
-                const bool in2 = i2 < h1;
-                shn = in2 ? sh[i2] : 0.0f;
-                cfn = in2 ? cfr[i2] : 0;
-                whn = (in2 && wrow) ? wrow[i2] : 0.0;
-            }
+            const float shv = shq[d];
+            const int32_t cfv = cfq[d];
+            const double whv = whq[d];
+            fetch(d, c + EX_HQ * WAVE);
             const int per = period(i);
             int pos = 0;
             for (int p = 0; p < P; p++) {
